@@ -1,0 +1,384 @@
+// mev_math.h — bit-exact replicas of the glibc 2.35 float libm routines the
+// reference simulator calls, usable on the gfx950 device and on the host.
+//
+// Why: the reference (cpp/Car.cpp, cpp/Lidar.cpp, cpp/IntersectionEnv.cpp,
+// cpp/TrafficFlow.cpp) is compiled against glibc, whose sinf/cosf/tanf/atan2f
+// are NOT correctly rounded (SURVEY.md §7.3 hard part 1).  A device trig that
+// differs by one ulp flips `int(cx + dx*dist)` in the LiDAR march and, through
+// trajectory chaos, every later observation.  So the device path evaluates the
+// SAME algorithms glibc 2.35 evaluates, operation for operation:
+//
+//   mev_sincosf  — glibc sysdeps/ieee754/flt-32 sincosf (optimized-routines):
+//                  double-precision polynomial, reduce_fast below 120, the
+//                  192-bit 4/pi table above.  glibc's x86-64 ifunc picks the
+//                  FMA build on FMA hosts; MEV_SINCOS_FMA selects which
+//                  contraction pattern is reproduced (tests/test_devmath.py
+//                  checks both against the host libm and pins the choice).
+//   mev_tanf     — glibc 2.35 tanf: sincosf-style reduction + fdlibm __kernel_tanf.
+//   mev_atan2f   — fdlibm e_atan2f + s_atanf (11-term polynomial).
+//   mev_hypotf   — glibc 2.35 hypotf: (float)sqrt((double)x*x + (double)y*y).
+//   mev_fmodf    — exact remainder (any correct fmodf is bit-identical).
+//
+// Every constant below was checked against the tables in this image's
+// /lib/x86_64-linux-gnu/libm.so.6 and every function is compared bit-for-bit
+// with that libm over the argument ranges the simulator uses (tests/test_devmath.py).
+// All code must be compiled with -ffp-contract=off.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define MEV_HD __host__ __device__ inline
+#else
+#include <math.h>
+#define MEV_HD static inline
+#endif
+
+#ifndef MEV_SINCOS_FMA
+#define MEV_SINCOS_FMA 1
+#endif
+
+namespace mev {
+
+MEV_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+MEV_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+MEV_HD uint64_t d2u(double d) { return __builtin_bit_cast(uint64_t, d); }
+
+MEV_HD double fma_d(double a, double b, double c) { return __builtin_fma(a, b, c); }
+MEV_HD float fabs_f(float x) { return u2f(f2u(x) & 0x7fffffffu); }
+
+// a + b*c in double, contracted or not (glibc FMA vs generic build).
+template <bool FMA>
+MEV_HD double madd(double a, double b, double c) {
+    if constexpr (FMA) return fma_d(b, c, a);
+    else return a + b * c;
+}
+
+// ---------------------------------------------------------------- sincosf ---
+struct SinCosTab {
+    double sign[4];
+    double hpi_inv;
+    double hpi;
+    double c0, c1, s1, c2, s2, c3, s3, c4;
+};
+
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+static constexpr SinCosTab kSinCos[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+     0x1p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
+     0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, 0x1.99343027bf8c3p-16},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+     -0x1p+0, 0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
+     0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16},
+};
+
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+static constexpr uint32_t kInvPio4[24] = {
+    0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
+    0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,
+    0x2757d1f5u, 0x57d1f534u, 0xd1f534ddu, 0xf534ddc0u, 0x34ddc0dbu, 0xddc0db62u,
+    0xc0db6295u, 0xdb629599u, 0x6295993cu, 0x95993c43u, 0x993c4390u, 0x3c439041u,
+};
+
+MEV_HD uint32_t abstop12(float x) { return (f2u(x) >> 20) & 0x7ffu; }
+
+template <bool FMA>
+MEV_HD void sincosf_poly(double x, double x2, const SinCosTab& p, int n, float* sinp, float* cosp) {
+    const double x4 = x2 * x2;
+    const double x3 = x2 * x;
+    const double c2 = madd<FMA>(p.c3, x2, p.c4);
+    const double s1 = madd<FMA>(p.s2, x2, p.s3);
+    const double c1 = madd<FMA>(p.c0, x2, p.c1);
+    const double x5 = x3 * x2;
+    const double x6 = x4 * x2;
+    const double s = madd<FMA>(x, x3, p.s1);
+    const double c = madd<FMA>(c1, x4, p.c2);
+    const float sv = (float)madd<FMA>(s, x5, s1);
+    const float cv = (float)madd<FMA>(c, x6, c2);
+    if (n & 1) { *sinp = cv; *cosp = sv; }
+    else { *sinp = sv; *cosp = cv; }
+}
+
+template <bool FMA>
+MEV_HD double reduce_fast(double x, const SinCosTab& p, int* np) {
+    const double r = x * p.hpi_inv;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    if constexpr (FMA) return fma_d(-(double)n, p.hpi, x);
+    else return x - n * p.hpi;
+}
+
+MEV_HD double reduce_large(uint32_t xi, int* np) {
+    const uint32_t* arr = &kInvPio4[(xi >> 26) & 15];
+    const int shift = (xi >> 23) & 7;
+    xi = (xi & 0xffffffu) | 0x800000u;
+    xi <<= shift;
+    uint64_t res0 = xi * arr[0];
+    const uint64_t res1 = (uint64_t)xi * arr[4];
+    const uint64_t res2 = (uint64_t)xi * arr[8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    const uint64_t n = (res0 + (1ull << 61)) >> 62;
+    res0 -= n << 62;
+    const double x = (double)(int64_t)res0;
+    *np = (int)n;
+    return x * 0x1.921fb54442d18p-62;
+}
+
+template <bool FMA>
+MEV_HD void sincosf_impl(float y, float* sinp, float* cosp) {
+    double x = y;
+    int n;
+    const SinCosTab* p = &kSinCos[0];
+    if (abstop12(y) < abstop12(0x1.921fb6p-1f)) {
+        const double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) {
+            *sinp = y;
+            *cosp = 1.0f;
+            return;
+        }
+        sincosf_poly<FMA>(x, x2, *p, 0, sinp, cosp);
+    } else if (abstop12(y) < abstop12(120.0f)) {
+        x = reduce_fast<FMA>(x, *p, &n);
+        const double s = p->sign[n & 3];
+        if (n & 2) p = &kSinCos[1];
+        sincosf_poly<FMA>(x * s, x * x, *p, n, sinp, cosp);
+    } else if (abstop12(y) < abstop12(__builtin_inff())) {
+        const uint32_t xi = f2u(y);
+        const int sign = xi >> 31;
+        x = reduce_large(xi, &n);
+        const double s = p->sign[(n + sign) & 3];
+        if ((n + sign) & 2) p = &kSinCos[1];
+        sincosf_poly<FMA>(x * s, x * x, *p, n, sinp, cosp);
+    } else {
+        *sinp = *cosp = y - y;  // NaN for inf / NaN input
+    }
+}
+
+MEV_HD void sincosf(float y, float* s, float* c) { sincosf_impl<MEV_SINCOS_FMA != 0>(y, s, c); }
+
+// ------------------------------------------------------------------ tanf ---
+MEV_HD float kernel_tanf(float x, float y, int iy) {
+    constexpr float one = 1.0f;
+    constexpr float pio4 = 7.8539812565e-01f;    // 0x3f490fda
+    constexpr float pio4lo = 3.7748947079e-08f;  // 0x33222168
+    const float T0 = u2f(0x3eaaaaabu), T1 = u2f(0x3e088889u), T2 = u2f(0x3d5d0dd1u), T3 = u2f(0x3cb327a4u),
+                T4 = u2f(0x3c11371fu), T5 = u2f(0x3b6b6916u), T6 = u2f(0x3abede48u), T7 = u2f(0x3a1a26c8u),
+                T8 = u2f(0x398137b9u), T9 = u2f(0x38a3f445u), T10 = u2f(0x3895c07au), T11 = u2f(0xb79bae5fu),
+                T12 = u2f(0x37d95384u);
+    float z, r, v, w, s;
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    if (ix < 0x39000000) {
+        if ((int)x == 0) {
+            if ((ix | (iy + 1)) == 0) return one / fabs_f(x);
+            else if (iy == 1) return x;
+            else return -one / x;
+        }
+    }
+    if (ix >= 0x3f2ca140) {
+        if (hx < 0) { x = -x; y = -y; }
+        z = pio4 - x;
+        w = pio4lo - y;
+        x = z + w;
+        y = 0.0f;
+        if (fabs_f(x) < 0x1p-13f) return (float)((1 - ((hx >> 30) & 2)) * iy) * (1.0f - (float)(2 * iy) * x);
+    }
+    z = x * x;
+    w = z * z;
+    r = T1 + w * (T3 + w * (T5 + w * (T7 + w * (T9 + w * T11))));
+    v = z * (T2 + w * (T4 + w * (T6 + w * (T8 + w * (T10 + w * T12)))));
+    s = z * x;
+    r = y + z * (s * (r + v) + y);
+    r += T0 * s;
+    w = x + r;
+    if (ix >= 0x3f2ca140) {
+        v = (float)iy;
+        return (float)(1 - ((hx >> 30) & 2)) * (v - 2.0f * (x - (w * w / (w + v) - r)));
+    }
+    if (iy == 1) return w;
+    float a, t;
+    z = u2f(f2u(w) & 0xfffff000u);
+    v = r - (z - x);
+    t = a = -1.0f / w;
+    t = u2f(f2u(t) & 0xfffff000u);
+    s = 1.0f + t * z;
+    return t + a * (s + t * v);
+}
+
+MEV_HD float tanf(float x) {
+    const uint32_t ix = f2u(x) & 0x7fffffffu;
+    if (ix <= 0x3f490fdau) return kernel_tanf(x, 0.0f, 1);
+    if (ix >= 0x7f800000u) return x - x;
+    int n;
+    double xd;
+    if (abstop12(x) < abstop12(120.0f)) {
+        // glibc 2.35 s_tanf.c: reduce_fast without the FMA build (tanf is not an ifunc).
+        const double r = (double)x * 0x1.45f306dc9c883p+23;
+        n = ((int32_t)r + 0x800000) >> 24;
+        xd = (double)x - (double)n * 0x1.921fb54442d18p+0;
+    } else {
+        const uint32_t xi = f2u(x);
+        xd = reduce_large(xi, &n);
+        if (xi >> 31) { xd = -xd; n = -n; }
+    }
+    const float y0 = (float)xd;
+    const float y1 = (float)(xd - (double)y0);
+    return kernel_tanf(y0, y1, 1 - ((n & 1) << 1));
+}
+
+// ----------------------------------------------------------------- atanf ---
+MEV_HD float atanf(float x) {
+    const float atanhi0 = u2f(0x3eed6338u), atanhi1 = u2f(0x3f490fdau), atanhi2 = u2f(0x3f7b985eu),
+                atanhi3 = u2f(0x3fc90fdau);
+    const float atanlo0 = u2f(0x31ac3769u), atanlo1 = u2f(0x33222168u), atanlo2 = u2f(0x33140fb4u),
+                atanlo3 = u2f(0x33a22168u);
+    const float aT0 = u2f(0x3eaaaaabu), aT1 = u2f(0xbe4ccccdu), aT2 = u2f(0x3e124925u), aT3 = u2f(0xbde38e38u),
+                aT4 = u2f(0x3dba2e6eu), aT5 = u2f(0xbd9d8795u), aT6 = u2f(0x3d886b35u), aT7 = u2f(0xbd6ef16bu),
+                aT8 = u2f(0x3d4bda59u), aT9 = u2f(0xbd15a221u), aT10 = u2f(0x3c8569d7u);
+    constexpr float one = 1.0f;
+    float w, s1, s2, z, hi = 0.0f, lo = 0.0f;
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {
+        if (ix > 0x7f800000) return x + x;
+        return hx > 0 ? atanhi3 + atanlo3 : -atanhi3 - atanlo3;
+    }
+    if (ix < 0x3ee00000) {
+        if (ix < 0x31000000) return x;
+        id = -1;
+    } else {
+        x = fabs_f(x);
+        if (ix < 0x3f980000) {
+            if (ix < 0x3f300000) { id = 0; x = (2.0f * x - one) / (2.0f + x); hi = atanhi0; lo = atanlo0; }
+            else { id = 1; x = (x - one) / (x + one); hi = atanhi1; lo = atanlo1; }
+        } else {
+            if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (one + 1.5f * x); hi = atanhi2; lo = atanlo2; }
+            else { id = 3; x = -1.0f / x; hi = atanhi3; lo = atanlo3; }
+        }
+    }
+    z = x * x;
+    w = z * z;
+    s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    z = hi - ((x * (s1 + s2) - lo) - x);
+    return hx < 0 ? -z : z;
+}
+
+MEV_HD float atan2f(float y, float x) {
+    constexpr float tiny = 1.0e-30f;
+    const float pi_o_4 = u2f(0x3f490fdbu), pi_o_2 = u2f(0x3fc90fdbu), pi = u2f(0x40490fdbu),
+                pi_lo = u2f(0xb3bbbd2eu);
+    float z;
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)f2u(y);
+    const int32_t iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return atanf(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0) {
+        switch (m) {
+            case 0:
+            case 1: return y;
+            case 2: return pi + tiny;
+            default: return -pi - tiny;
+        }
+    }
+    if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            switch (m) {
+                case 0: return pi_o_4 + tiny;
+                case 1: return -pi_o_4 - tiny;
+                case 2: return 3.0f * pi_o_4 + tiny;
+                default: return -3.0f * pi_o_4 - tiny;
+            }
+        } else {
+            switch (m) {
+                case 0: return 0.0f;
+                case 1: return -0.0f;
+                case 2: return pi + tiny;
+                default: return -pi - tiny;
+            }
+        }
+    }
+    if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = (iy - ix) >> 23;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0f;
+    else z = atanf(fabs_f(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return u2f(f2u(z) ^ 0x80000000u);
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
+
+// ---------------------------------------------------------------- hypotf ---
+MEV_HD float hypotf(float x, float y) {
+    // glibc 2.35 e_hypotf.c (finite inputs): one double evaluation, one rounding.
+    const double dx = x, dy = y;
+    return (float)__builtin_sqrt(dx * dx + dy * dy);
+}
+
+// ----------------------------------------------------------------- fmodf ---
+// Exact IEEE remainder x - trunc(x/y)*y (bit-level, after musl's fmodf).
+MEV_HD float fmodf(float x, float y) {
+    uint32_t ux = f2u(x), uy = f2u(y);
+    int ex = (ux >> 23) & 0xff;
+    int ey = (uy >> 23) & 0xff;
+    const uint32_t sx = ux & 0x80000000u;
+    uint32_t i;
+    if ((uy << 1) == 0 || ex == 0xff || ((uy & 0x7fffffffu) > 0x7f800000u)) return (x * y) / (x * y);
+    if ((ux << 1) <= (uy << 1)) {
+        if ((ux << 1) == (uy << 1)) return 0.0f * x;
+        return x;
+    }
+    if (!ex) {
+        for (i = ux << 9; (int32_t)i >= 0; ex--, i <<= 1) {}
+        ux <<= -ex + 1;
+    } else {
+        ux &= 0xffffffffu >> 9;
+        ux |= 1u << 23;
+    }
+    if (!ey) {
+        for (i = uy << 9; (int32_t)i >= 0; ey--, i <<= 1) {}
+        uy <<= -ey + 1;
+    } else {
+        uy &= 0xffffffffu >> 9;
+        uy |= 1u << 23;
+    }
+    for (; ex > ey; ex--) {
+        i = ux - uy;
+        if ((int32_t)i >= 0) {
+            if (i == 0) return 0.0f * x;
+            ux = i;
+        }
+        ux <<= 1;
+    }
+    i = ux - uy;
+    if ((int32_t)i >= 0) {
+        if (i == 0) return 0.0f * x;
+        ux = i;
+    }
+    for (; (ux >> 23) == 0; ux <<= 1, ex--) {}
+    if (ex > 0) {
+        ux -= 1u << 23;
+        ux |= (uint32_t)ex << 23;
+    } else {
+        ux >>= -ex + 1;
+    }
+    ux |= sx;
+    return u2f(ux);
+}
+
+}  // namespace mev

@@ -1,0 +1,230 @@
+"""Generate the golden vectors in tests/golden/*.npz from the REAL reference.
+
+TEST INFRASTRUCTURE.  Runs only in the build container, where /root/reference
+exists and oracle/build_ref.sh has produced oracle/_ref/libref_harness.so (the
+unmodified reference simulator + our harness).  The .npz files it writes are
+committed; the GPU box never needs the reference.
+
+    python tests/golden/gen_golden.py            # (re)writes every scenario
+
+Each scenario file holds the configuration (``meta`` JSON), the initial state
+the device path is loaded with, the per-step inputs (actions, and for traffic
+mode the route index of the NPC the reference's unseeded RNG spawned that step)
+and the reference's per-step outputs: observations (N x 127), rewards, done,
+status codes, (terminated, truncated, agents_alive, step) and the full ego/NPC
+state after the step (incl. fields pybind does not expose).
+
+Status codes: 0 ALIVE, 1 DEAD, 2 SUCCESS, 3 CRASH_WALL, 4 CRASH_LINE, 5 CRASH_CAR.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import refharness as R  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+ROUTES3 = [("IN_1", "OUT_4"), ("IN_2", "OUT_8"), ("IN_3", "OUT_12"), ("IN_4", "OUT_7"),
+           ("IN_5", "OUT_11"), ("IN_6", "OUT_3"), ("IN_7", "OUT_10"), ("IN_8", "OUT_2"),
+           ("IN_9", "OUT_6"), ("IN_10", "OUT_1"), ("IN_11", "OUT_5"), ("IN_12", "OUT_9")]
+ROUTES2 = [("IN_1", "OUT_3"), ("IN_2", "OUT_6"), ("IN_3", "OUT_5"), ("IN_4", "OUT_8"),
+           ("IN_6", "OUT_2"), ("IN_7", "OUT_1"), ("IN_8", "OUT_4")]
+DEFAULT_REWARD = [10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2]
+
+
+def policy(obs: np.ndarray, rng: np.random.Generator, target_v=3.5, noise=0.05) -> np.ndarray:
+    """Route-following driver used to produce realistic action streams (the
+    actions are stored; the device path never runs this)."""
+    n = obs.shape[0]
+    a = np.zeros((n, 2), np.float32)
+    v = obs[:, 2] * 8.0
+    th = obs[:, 5] * math.pi
+    a[:, 1] = np.clip(2.0 * th, -1.0, 1.0)
+    a[:, 0] = np.clip((target_v - v) * 0.5, -1.0, 1.0)
+    a += rng.normal(0.0, noise, a.shape).astype(np.float32)
+    return np.clip(a, -1.0, 1.0).astype(np.float32)
+
+
+def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_steps=2000,
+        traffic=False, density=0.5, lanes=3, ego_routes=None, reward=None, steps=200,
+        act="random", seed=0, dt=1.0 / 60.0, act_scale=1.0, zero_throttle_p=0.0,
+        inject=None, notes=""):
+    routes = ROUTES3 if lanes == 3 else ROUTES2
+    if ego_routes is None:
+        ego_routes = [routes[i % len(routes)] for i in range(n_agents)]
+    reward = list(DEFAULT_REWARD if reward is None else reward)
+    env = R.RefEnv(num_lanes=lanes, use_team=use_team and not traffic, respawn=respawn, max_steps=max_steps,
+                   traffic=traffic, density=density, routes=routes, reward=reward, rays=rays)
+    env.reset()
+    for i, (s, e) in enumerate(ego_routes):
+        assert env.add_car(s, e, tag=routes.index((s, e)) if (s, e) in routes else -1) == 0
+    rng = np.random.default_rng(seed)
+    if inject is not None:
+        inject(env, rng)
+    n = env.n
+    ef, ei = env.cars(0)
+    nf, ni = env.cars(1)
+    init_obs = env.obs()
+    A, O, RW, D, ST, FL, SP, EF, EI, NC, LD = [], [], [], [], [], [], [], [], [], [], []
+    NFl, NIl = [], []
+    cur_obs = init_obs
+    for t in range(steps):
+        if act == "random":
+            a = (rng.uniform(-1.0, 1.0, (n, 2)) * act_scale).astype(np.float32)
+        else:
+            a = policy(cur_obs, rng)
+        if zero_throttle_p > 0:
+            a[rng.uniform(size=n) < zero_throttle_p, 0] = 0.0
+        r = env.step(a, dt)
+        cur_obs = r["obs"]
+        A.append(a)
+        O.append(r["obs"])
+        RW.append(r["rew"])
+        D.append(r["done"].astype(np.uint8))
+        ST.append(r["status"].astype(np.uint8))
+        FL.append([r["terminated"], r["truncated"], r["agents_alive"], r["step"]])
+        SP.append(r["spawned"])
+        f, i = env.cars(0)
+        EF.append(f)
+        EI.append(i)
+        f, i = env.cars(1)
+        NC.append(len(f))
+        NFl.append(f)
+        NIl.append(i)
+        LD.append(env.lidar())
+    kmax = max([len(x) for x in NFl] + [1])
+    npc_f = np.zeros((steps, kmax, R.NF), np.float32)
+    npc_i = np.zeros((steps, kmax, R.NI), np.int32)
+    for t in range(steps):
+        npc_f[t, : NC[t]] = NFl[t]
+        npc_i[t, : NC[t]] = NIl[t]
+    meta = dict(name=name, num_lanes=lanes, n_agents=n, rays=rays, use_team=bool(use_team and not traffic),
+                respawn=respawn, max_steps=max_steps, traffic=traffic, density=density,
+                reward=reward, ego_routes=ego_routes, traffic_routes=routes, dt=dt, steps=steps,
+                act=act, seed=seed, notes=notes)
+    arrays = dict(
+        meta=np.array(json.dumps(meta)),
+        init_ego_f=ef, init_ego_i=ei, init_npc_f=nf.reshape(-1, R.NF), init_npc_i=ni.reshape(-1, R.NI),
+        init_obs=init_obs, actions=np.asarray(A, np.float32), obs=np.asarray(O, np.float32),
+        rew=np.asarray(RW, np.float32), done=np.asarray(D, np.uint8), status=np.asarray(ST, np.uint8),
+        flags=np.asarray(FL, np.int32), spawned=np.asarray(SP, np.int32), ego_f=np.asarray(EF, np.float32),
+        ego_i=np.asarray(EI, np.int32), npc_count=np.asarray(NC, np.int32), npc_f=npc_f, npc_i=npc_i,
+    )
+    if rays > 96:
+        arrays["lidar"] = np.asarray(LD, np.float32)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **arrays)
+    env.close()
+    st = np.asarray(ST)
+    hist = {int(c): int((st == c).sum()) for c in range(6)}
+    print(f"{name:28s} n={n} R={rays} steps={steps} max_npc={max(NC) if NC else 0} "
+          f"spawns={int((np.asarray(SP) >= 0).sum())} status={hist} -> {os.path.getsize(path)//1024} KB")
+
+
+def inject_random_egos(env: R.RefEnv, rng: np.random.Generator):
+    """Scatter the egos over the road area with random headings/speeds/controls."""
+    f, i = env.cars(0)
+    for k in range(len(f)):
+        if rng.uniform() < 0.5:  # somewhere in the cross
+            x, y = rng.uniform(249, 501), rng.uniform(0, 750)
+            if rng.uniform() < 0.5:
+                x, y = y, x
+        else:  # near the box
+            x, y = rng.uniform(230, 520, 2)
+        f[k, 0], f[k, 1] = x, y
+        f[k, 2] = rng.uniform(0, 8)
+        f[k, 3] = rng.uniform(-math.pi, math.pi)
+        f[k, 4] = rng.uniform(-15, 15)
+        f[k, 5] = rng.uniform(-0.6, 0.6)
+        f[k, 10] = rng.uniform(0, 600) if rng.uniform() < 0.8 else 0.0
+        f[k, 11], f[k, 12] = rng.uniform(-1, 1, 2)
+        i[k, 2] = int(rng.integers(0, 150))
+        env.set_car(k, f[k], i[k])
+
+
+def inject_dead(env: R.RefEnv, rng: np.random.Generator):
+    inject_random_egos(env, rng)
+    f, i = env.cars(0)
+    for k in range(len(f)):
+        if k % 3 == 1:
+            i[k, 0] = 0
+            env.set_car(k, f[k], i[k])
+
+
+def inject_npcs(kcount: int):
+    def _inj(env: R.RefEnv, rng: np.random.Generator):
+        """Place NPCs on points of random traffic routes (on their own path,
+        path-aligned heading), at least 70 px apart and away from the ego."""
+        ef, _ = env.cars(0)
+        placed = [(float(ef[0, 0]), float(ef[0, 1]))]
+        tries = 0
+        while len(placed) < kcount + 1 and tries < 1000:
+            tries += 1
+            route = int(rng.integers(0, 12))
+            path = env.route_path(route)
+            idx = int(rng.integers(0, 150))
+            x, y = float(path[idx, 0]), float(path[idx, 1])
+            if min((x - px) ** 2 + (y - py) ** 2 for px, py in placed) < 70.0 ** 2:
+                continue
+            dx, dy = path[idx + 1] - path[idx]
+            f = np.zeros(R.NF, np.float32)
+            f[0], f[1] = x + rng.normal(0, 1.0), y + rng.normal(0, 1.0)
+            f[2] = rng.uniform(0, 5)
+            f[3] = math.atan2(-dy, dx) + rng.normal(0, 0.05)
+            f[6], f[7], f[9] = path[0, 0], path[0, 1], math.atan2(-(path[1, 1] - path[0, 1]), path[1, 0] - path[0, 0])
+            f[13], f[14] = 54.0, 24.0
+            i = np.array([1, 0, max(0, idx - 2), route], np.int32)
+            assert env.add_npc(route, f, i) == 0
+            placed.append((x, y))
+    return _inj
+
+
+def main():
+    # Config 1 shape: 1 env x 1 agent, 16 beams.
+    run("cfg1_r16_random", n_agents=1, rays=16, steps=400, act="random", seed=0)
+    run("cfg1_r16_policy", n_agents=1, rays=16, steps=300, act="policy", seed=1)
+    # Config 2 shape, every route (straight / left / right), policy-driven to SUCCESS.
+    for r in range(12):
+        run(f"cfg2_r64_route{r:02d}", n_agents=1, rays=64, steps=160, act="policy", seed=10 + r,
+            ego_routes=[ROUTES3[r]])
+    # Config 3 shape: 8 agents, team reward, 64 beams.
+    run("cfg3_team_random_s0", n_agents=8, rays=64, use_team=True, steps=300, act="random", seed=0)
+    run("cfg3_team_random_s1", n_agents=8, rays=64, use_team=True, steps=300, act="random", seed=1)
+    run("cfg3_team_policy", n_agents=8, rays=64, use_team=True, steps=400, act="policy", seed=2)
+    # Native 127-D observation (96 beams), all 12 routes; 16 agents forces spawn ties.
+    run("n12_r96_policy", n_agents=12, rays=96, steps=300, act="policy", seed=3)
+    run("n16_r96_ties", n_agents=16, rays=96, steps=60, act="policy", seed=4)
+    # Config 5 shape: 8 agents, 128 beams (obs truncates at 127; raw lidar stored).
+    run("cfg5_r128_team", n_agents=8, rays=128, use_team=True, steps=150, act="random", seed=5)
+    # respawn off / truncation / unclipped actions / exact-zero throttle / other dt.
+    run("respawn_off_policy", n_agents=8, rays=64, respawn=False, steps=250, act="policy", seed=6)
+    run("truncate_50", n_agents=2, rays=32, max_steps=50, steps=80, act="random", seed=7)
+    run("unclipped_x3", n_agents=4, rays=64, steps=200, act="random", act_scale=3.0, seed=8)
+    run("zero_throttle", n_agents=4, rays=64, steps=200, act="random", zero_throttle_p=0.5, seed=9)
+    run("dt_1_30_custom_reward", n_agents=6, rays=48, use_team=True, steps=200, act="policy", seed=10,
+        dt=1.0 / 30.0, reward=[5.0, 2.0, -0.05, -7.0, -3.0, 4.0, -0.1, 0.5])
+    # 2-lane layout.
+    run("lanes2_policy", n_agents=7, rays=64, lanes=2, steps=300, act="policy", seed=11)
+    # Traffic mode (config 4 shape) with recorded spawns.
+    run("traffic_d05", n_agents=1, rays=64, traffic=True, density=0.5, steps=1500, act="policy", seed=12)
+    run("traffic_d5", n_agents=1, rays=64, traffic=True, density=5.0, steps=800, act="policy", seed=13)
+    run("traffic_d20", n_agents=1, rays=64, traffic=True, density=20.0, steps=500, act="policy", seed=14)
+    run("traffic_d20_random", n_agents=1, rays=64, traffic=True, density=20.0, steps=400, act="random", seed=15)
+    # State injection.
+    for c in range(6):
+        run(f"inject_egos_c{c}", n_agents=8, rays=64, steps=3, act="random", seed=100 + c, inject=inject_random_egos)
+    run("inject_dead", n_agents=6, rays=64, steps=20, act="random", seed=200, inject=inject_dead)
+    for k in (2, 5, 9):
+        run(f"inject_npc_k{k}", n_agents=1, rays=64, traffic=True, density=0.0, steps=150, act="policy",
+            seed=300 + k, inject=inject_npcs(k))
+
+
+if __name__ == "__main__":
+    main()
