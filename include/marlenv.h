@@ -1,0 +1,169 @@
+/*
+ * marlenv.h — C ABI of libmarlenv_hip.so, the MI355X (gfx950) batched
+ * intersection environment.
+ *
+ * This is the drop-in boundary that replaces the reference's pybind11 module
+ * `MARLEnv` (reference cpp/bindings.cpp:11-95) as reached through
+ * cpp_backend.py (reference cpp_backend.py:30-66) and env.py (reference
+ * env.py:80-221).  One handle holds E independent environment instances
+ * ("envs") of the reference's IntersectionEnv (reference
+ * cpp/IntersectionEnv.h:23-105), each with N ego agents and (traffic mode) up
+ * to max_npcs NPC cars, resident on ONE GPU in structure-of-arrays layout.
+ *
+ * Conventions
+ *  - Every function returns 0 on success or a negative MEV_E* code; the
+ *    message is available from mev_last_error() (thread-local).  No C++
+ *    exception crosses this boundary.
+ *  - Buffers are caller-owned.  Host pointers unless MEV_DEVICE_PTRS is set in
+ *    the call's flags, in which case every pointer in that call is a device
+ *    pointer on the handle's device and the call does not synchronise.
+ *  - All work of a handle is ordered on one HIP stream (mev_set_stream).
+ *  - Lane points are numbered 0..8L-1: "IN_k" -> k-1, "OUT_k" -> 4L+k-1
+ *    (reference cpp/RouteGen.cpp:7-53).  A route is a (start point, end point)
+ *    pair (reference IntersectionEnv::add_car_with_route,
+ *    cpp/IntersectionEnv.cpp:78-131).
+ *  - Status codes: 0 ALIVE, 1 DEAD, 2 SUCCESS, 3 CRASH_WALL, 4 CRASH_LINE,
+ *    5 CRASH_CAR (the strings of reference cpp/Reward.h:16-29 / env.py:193).
+ */
+#ifndef MARLENV_H
+#define MARLENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MEV_ABI_VERSION 1
+
+enum {
+    MEV_OK = 0,
+    MEV_E_INVALID = -1,  /* bad argument / configuration          */
+    MEV_E_HIP = -2,      /* HIP runtime error                      */
+    MEV_E_NOMEM = -3,    /* device or host allocation failed       */
+    MEV_E_RANGE = -4     /* index out of range (std::out_of_range) */
+};
+
+enum { MEV_ALIVE = 0, MEV_DEAD = 1, MEV_SUCCESS = 2, MEV_CRASH_WALL = 3, MEV_CRASH_LINE = 4, MEV_CRASH_CAR = 5 };
+
+/* flags for mev_step / mev_reset / mev_get_outputs */
+#define MEV_DEVICE_PTRS 0x1u /* all pointers in this call are device pointers; no host sync */
+#define MEV_AUTO_RESET 0x2u  /* an env whose previous step ended (terminated|truncated) is reset
+                                before this step (gym-style vector auto-reset) */
+
+typedef struct mev_handle mev_handle;
+
+/* Configuration: fields mirror reference env.py:81-131 config keys and
+ * IntersectionEnv::configure* (cpp/IntersectionEnv.cpp:50-64). */
+typedef struct {
+    int32_t num_envs;        /* E >= 1                                                     */
+    int32_t num_agents;      /* N, 1..64 ego cars per env                                   */
+    int32_t num_lanes;       /* lanes per direction (reference default 3)                  */
+    int32_t lidar_rays;      /* R >= 1 (reference hard-codes 96, IntersectionEnv.cpp:113)  */
+    float lidar_fov_deg;     /* 360                                                        */
+    float lidar_max_dist;    /* 250 px                                                     */
+    float lidar_step;        /* 4 px                                                       */
+    int32_t obs_dim;         /* 0 => 31 + R; 127 reproduces the reference layout exactly   */
+    int32_t traffic_flow;    /* NPC traffic mode (TrafficFlow.cpp)                          */
+    float traffic_density;   /* arrival rate (1/s), clamped >= 0                            */
+    int32_t use_team_reward;
+    int32_t respawn_enabled;
+    int32_t max_steps;       /* truncation; <= 0 disables                                   */
+    float reward[8];         /* k_prog, v_min_ms, k_stuck, k_cv, k_co, k_succ, k_sm, alpha  */
+    int32_t max_npcs;        /* NPC slots per env, 0..64 (overflowing spawns are dropped)    */
+    uint64_t seed;           /* on-device Philox stream for NPC spawns                      */
+    int32_t device;          /* HIP device ordinal                                          */
+} mev_config;
+
+/* Per-step arguments (reference IntersectionEnv::step, cpp/IntersectionEnv.cpp:133-392,
+ * + get_observations :418-520). */
+typedef struct {
+    const float* actions;       /* [E][N][2] (throttle, steer); never clipped (Car.cpp:9-40) */
+    float dt;                   /* seconds (reference default 1/60)                          */
+    const int32_t* spawn_route; /* optional [E]: traffic-route index the NPC spawner uses this
+                                   step (-1 = no spawn attempt); NULL = on-device Philox draw.
+                                   Replays the reference's RNG decisions (TrafficFlow.cpp:275-329). */
+    float* obs;                 /* optional [E][N][obs_dim]                                  */
+    float* reward;              /* optional [E][N]                                           */
+    uint8_t* done;              /* optional [E][N]                                           */
+    uint8_t* status;            /* optional [E][N]                                           */
+    uint8_t* terminated;        /* optional [E]                                              */
+    uint8_t* truncated;         /* optional [E]                                              */
+    int32_t* agents_alive;      /* optional [E]                                              */
+    int32_t* step;              /* optional [E] step counter after this step                 */
+    uint32_t flags;             /* MEV_DEVICE_PTRS | MEV_AUTO_RESET                           */
+} mev_step_args;
+
+/* Full simulator state, SoA.  Ego arrays are [E][N], NPC arrays [E][max_npcs].
+ * Any NULL pointer is skipped.  Replaces EnvState/get_state/set_state
+ * (reference cpp/EnvState.h:9-15, cpp/IntersectionEnv.cpp:394-416) and exposes
+ * the Car fields the pybind layer hides (acc, steering_angle, spawn_state,
+ * prev_dist_to_goal, prev_action; cpp/Car.h:16-46). */
+typedef struct {
+    float *x, *y, *v, *heading, *acc, *steering, *prev_dist, *prev_a0, *prev_a1;
+    float *spawn_x, *spawn_y, *spawn_v, *spawn_heading;
+    int32_t *path_index, *route, *intention;
+    uint8_t* alive;
+    float *npc_x, *npc_y, *npc_v, *npc_heading, *npc_acc, *npc_steering;
+    int32_t *npc_path_index, *npc_route, *npc_intention;
+    uint8_t* npc_alive;
+    int32_t* npc_count;  /* [E] */
+    int32_t* step_count; /* [E] */
+} mev_state;
+
+const char* mev_last_error(void);
+int mev_abi_version(void);
+int mev_device_count(int32_t* count);
+
+int mev_config_default(mev_config* cfg);
+int mev_create(const mev_config* cfg, mev_handle** out);
+int mev_destroy(mev_handle* h);
+int mev_get_config(const mev_handle* h, mev_config* cfg);
+int mev_obs_dim(const mev_handle* h, int32_t* obs_dim);
+/* hipStream_t to order this handle's work on (NULL = the handle's own stream). */
+int mev_set_stream(mev_handle* h, void* stream);
+int mev_sync(mev_handle* h);
+
+/* Lane points / routes (reference cpp/RouteGen.cpp). */
+int mev_num_points(const mev_handle* h, int32_t* n);
+int mev_point_xy(const mev_handle* h, int32_t point, float* xy);
+int mev_route_id(const mev_handle* h, int32_t start_point, int32_t end_point, int32_t* route);
+/* path [160][2], intent, spawn (x, y, heading) of a route */
+int mev_route_info(const mev_handle* h, int32_t route, float* path, int32_t* intent, float* spawn);
+int mev_path_len(void);
+/* Ego routes for every (env, agent): route ids [E][N] (reference env.py:104-106,148-151). */
+int mev_set_ego_routes(mev_handle* h, const int32_t* routes);
+/* NPC route list (reference configure_routes / init_traffic_routes, TrafficFlow.cpp:198-238). */
+int mev_set_traffic_routes(mev_handle* h, const int32_t* routes, int32_t count);
+int mev_default_traffic_routes(const mev_handle* h, int32_t* routes, int32_t* count);
+
+/* Reset the envs selected by env_mask ([E], NULL = all): reference
+ * IntersectionEnv::reset + add_car_with_route per agent (cpp/IntersectionEnv.cpp:66-131).
+ * Writes the reset observation (LiDAR block = 1.0: no cast at reset). */
+int mev_reset(mev_handle* h, const uint8_t* env_mask, float* obs, uint32_t flags);
+
+/* One step of every env. */
+int mev_step(mev_handle* h, const mev_step_args* args);
+
+/* Outputs of the last step / reset, from the handle's own device buffers. */
+int mev_get_outputs(mev_handle* h, float* obs, float* reward, uint8_t* done, uint8_t* status,
+                    uint8_t* terminated, uint8_t* truncated, int32_t* agents_alive, int32_t* step,
+                    uint32_t flags);
+
+/* State snapshot / restore (host pointers).  mev_set_state recomputes the
+ * observation with LiDAR = 1.0, as after a reset. */
+int mev_get_state(mev_handle* h, const mev_state* out);
+int mev_set_state(mev_handle* h, const mev_state* in);
+
+/* Device pointers of the handle's internal output buffers (zero-copy consumers). */
+int mev_device_outputs(mev_handle* h, float** obs, float** reward, uint8_t** done, uint8_t** status,
+                       uint8_t** terminated, uint8_t** truncated);
+
+/* Diagnostics: spawns dropped because max_npcs was full (cumulative). */
+int mev_npc_overflow(mev_handle* h, int64_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MARLENV_H */

@@ -1,0 +1,63 @@
+"""Build the gfx950 extension in-tree: marl-traffic-intersection_amd/libmarlenv_hip.so.
+
+hipcc cross-compiles for gfx950 without a GPU, so this runs in the build
+container (``__graft_entry__.build()``) and the resulting .so travels to the GPU
+box with the repository snapshot.  All simulator code is compiled with
+-ffp-contract=off: the reference is an SSE (no-FMA) x86-64 build and the
+device path must round exactly like it ("Bit-exactness").
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+LIB_NAME = "libmarlenv_hip.so"
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+SOURCES = ["mev_kernels.hip", "mev_capi.cpp"]
+ARCH = os.environ.get("MEV_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (ROCm required to build libmarlenv_hip.so)")
+
+
+def _inputs():
+    files = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "marlenv.h"), __file__]
+    return [f for f in files if os.path.isfile(f)]
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return False
+    t = os.path.getmtime(LIB_PATH)
+    return all(os.path.getmtime(f) <= t for f in _inputs())
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC]
+    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    cmd += ["-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

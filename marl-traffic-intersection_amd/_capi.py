@@ -1,0 +1,331 @@
+"""ctypes binding of libmarlenv_hip.so (include/marlenv.h).
+
+The product path: every simulator computation happens in the gfx950 library;
+this module only marshals buffers.  Importing works without a GPU (the CPU
+test-suite checks the exported symbols), but creating a handle requires the
+HIP runtime and a device — there is NO CPU fallback: a missing library or
+device raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _build
+
+LIB_PATH = _build.LIB_PATH
+
+MEV_DEVICE_PTRS = 0x1
+MEV_AUTO_RESET = 0x2
+
+STATUS_NAMES = ("ALIVE", "DEAD", "SUCCESS", "CRASH_WALL", "CRASH_LINE", "CRASH_CAR")
+PATH_LEN = 160
+
+# exported symbols that include/marlenv.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED = (
+    "mev_last_error", "mev_abi_version", "mev_device_count", "mev_config_default", "mev_create", "mev_destroy",
+    "mev_get_config", "mev_obs_dim", "mev_set_stream", "mev_sync", "mev_num_points", "mev_point_xy",
+    "mev_route_id", "mev_route_info", "mev_path_len", "mev_set_ego_routes", "mev_set_traffic_routes",
+    "mev_default_traffic_routes", "mev_reset", "mev_step", "mev_get_outputs", "mev_get_state", "mev_set_state",
+    "mev_device_outputs", "mev_npc_overflow",
+)
+
+
+class MevConfig(ctypes.Structure):
+    _fields_ = [
+        ("num_envs", ctypes.c_int32), ("num_agents", ctypes.c_int32), ("num_lanes", ctypes.c_int32),
+        ("lidar_rays", ctypes.c_int32), ("lidar_fov_deg", ctypes.c_float), ("lidar_max_dist", ctypes.c_float),
+        ("lidar_step", ctypes.c_float), ("obs_dim", ctypes.c_int32), ("traffic_flow", ctypes.c_int32),
+        ("traffic_density", ctypes.c_float), ("use_team_reward", ctypes.c_int32), ("respawn_enabled", ctypes.c_int32),
+        ("max_steps", ctypes.c_int32), ("reward", ctypes.c_float * 8), ("max_npcs", ctypes.c_int32),
+        ("seed", ctypes.c_uint64), ("device", ctypes.c_int32),
+    ]
+
+
+_vp = ctypes.c_void_p
+
+
+class MevStepArgs(ctypes.Structure):
+    _fields_ = [
+        ("actions", _vp), ("dt", ctypes.c_float), ("spawn_route", _vp), ("obs", _vp), ("reward", _vp),
+        ("done", _vp), ("status", _vp), ("terminated", _vp), ("truncated", _vp), ("agents_alive", _vp),
+        ("step", _vp), ("flags", ctypes.c_uint32),
+    ]
+
+
+# (name, dtype, per) — per: "ego" [E*N], "npc" [E*K], "env" [E]; order == struct mev_state
+STATE_FIELDS = (
+    ("x", np.float32, "ego"), ("y", np.float32, "ego"), ("v", np.float32, "ego"), ("heading", np.float32, "ego"),
+    ("acc", np.float32, "ego"), ("steering", np.float32, "ego"), ("prev_dist", np.float32, "ego"),
+    ("prev_a0", np.float32, "ego"), ("prev_a1", np.float32, "ego"), ("spawn_x", np.float32, "ego"),
+    ("spawn_y", np.float32, "ego"), ("spawn_v", np.float32, "ego"), ("spawn_heading", np.float32, "ego"),
+    ("path_index", np.int32, "ego"), ("route", np.int32, "ego"), ("intention", np.int32, "ego"),
+    ("alive", np.uint8, "ego"),
+    ("npc_x", np.float32, "npc"), ("npc_y", np.float32, "npc"), ("npc_v", np.float32, "npc"),
+    ("npc_heading", np.float32, "npc"), ("npc_acc", np.float32, "npc"), ("npc_steering", np.float32, "npc"),
+    ("npc_path_index", np.int32, "npc"), ("npc_route", np.int32, "npc"), ("npc_intention", np.int32, "npc"),
+    ("npc_alive", np.uint8, "npc"), ("npc_count", np.int32, "env"), ("step_count", np.int32, "env"),
+)
+
+
+class MevState(ctypes.Structure):
+    _fields_ = [(name, _vp) for name, _, _ in STATE_FIELDS]
+
+
+_lib = None
+
+
+def lib_available() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+def load_library():
+    """Load libmarlenv_hip.so (building it first when hipcc is present)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not _build.up_to_date():
+        try:
+            _build.build()
+        except Exception as exc:  # no hipcc on this machine: use a prebuilt library if it is there
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"libmarlenv_hip.so is missing and could not be built: {exc}") from exc
+    L = ctypes.CDLL(LIB_PATH)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    f32p = ctypes.POINTER(ctypes.c_float)
+    L.mev_last_error.restype = ctypes.c_char_p
+    L.mev_config_default.argtypes = [ctypes.POINTER(MevConfig)]
+    L.mev_create.argtypes = [ctypes.POINTER(MevConfig), ctypes.POINTER(_vp)]
+    L.mev_destroy.argtypes = [_vp]
+    L.mev_get_config.argtypes = [_vp, ctypes.POINTER(MevConfig)]
+    L.mev_obs_dim.argtypes = [_vp, i32p]
+    L.mev_set_stream.argtypes = [_vp, _vp]
+    L.mev_sync.argtypes = [_vp]
+    L.mev_num_points.argtypes = [_vp, i32p]
+    L.mev_point_xy.argtypes = [_vp, ctypes.c_int32, f32p]
+    L.mev_route_id.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, i32p]
+    L.mev_route_info.argtypes = [_vp, ctypes.c_int32, f32p, i32p, f32p]
+    L.mev_set_ego_routes.argtypes = [_vp, i32p]
+    L.mev_set_traffic_routes.argtypes = [_vp, i32p, ctypes.c_int32]
+    L.mev_default_traffic_routes.argtypes = [_vp, i32p, i32p]
+    L.mev_reset.argtypes = [_vp, _vp, _vp, ctypes.c_uint32]
+    L.mev_step.argtypes = [_vp, ctypes.POINTER(MevStepArgs)]
+    L.mev_get_outputs.argtypes = [_vp] + [_vp] * 8 + [ctypes.c_uint32]
+    L.mev_get_state.argtypes = [_vp, ctypes.POINTER(MevState)]
+    L.mev_set_state.argtypes = [_vp, ctypes.POINTER(MevState)]
+    L.mev_device_outputs.argtypes = [_vp] + [ctypes.POINTER(_vp)] * 6
+    L.mev_npc_overflow.argtypes = [_vp, ctypes.POINTER(ctypes.c_int64)]
+    L.mev_device_count.argtypes = [i32p]
+    _lib = L
+    return L
+
+
+class MevError(RuntimeError):
+    pass
+
+
+class IndexRangeError(MevError, IndexError):
+    """MEV_E_RANGE: mirrors the reference's std::out_of_range -> IndexError."""
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = load_library().mev_last_error().decode(errors="replace")
+        if rc == -4:
+            raise IndexRangeError(msg)
+        raise MevError(f"libmarlenv_hip error {rc}: {msg}")
+
+
+def _ptr(a) -> Optional[int]:
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"], "arrays passed to libmarlenv_hip must be C-contiguous"
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):  # torch tensor (device pointer mode)
+        return int(a.data_ptr())
+    return int(a)
+
+
+def default_config() -> Dict:
+    c = MevConfig()
+    _check(load_library().mev_config_default(ctypes.byref(c)))
+    d = {name: getattr(c, name) for name, _ in MevConfig._fields_}
+    d["reward"] = list(c.reward)
+    return d
+
+
+class Handle:
+    """One device-resident batch of E intersection envs (owner of a mev_handle)."""
+
+    def __init__(self, **cfg):
+        L = load_library()
+        c = MevConfig()
+        _check(L.mev_config_default(ctypes.byref(c)))
+        for k, v in cfg.items():
+            if k == "reward":
+                for j, x in enumerate(v):
+                    c.reward[j] = float(x)
+            elif not hasattr(c, k):
+                raise TypeError(f"unknown config key {k!r}")
+            else:
+                setattr(c, k, v)
+        h = _vp()
+        _check(L.mev_create(ctypes.byref(c), ctypes.byref(h)))
+        self._h = h
+        self._lib = L
+        out = MevConfig()
+        _check(L.mev_get_config(h, ctypes.byref(out)))
+        self.config = {name: getattr(out, name) for name, _ in MevConfig._fields_}
+        self.config["reward"] = list(out.reward)
+        self.E = out.num_envs
+        self.N = out.num_agents
+        self.K = out.max_npcs
+        self.R = out.lidar_rays
+        self.D = out.obs_dim
+        n = ctypes.c_int32()
+        _check(L.mev_num_points(h, ctypes.byref(n)))
+        self.num_points = n.value
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.mev_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_ptr: Optional[int]):
+        _check(self._lib.mev_set_stream(self._h, stream_ptr))
+
+    def sync(self):
+        _check(self._lib.mev_sync(self._h))
+
+    # -- routes -----------------------------------------------------------
+    def route_id(self, start_point: int, end_point: int) -> int:
+        r = ctypes.c_int32()
+        _check(self._lib.mev_route_id(self._h, int(start_point), int(end_point), ctypes.byref(r)))
+        return r.value
+
+    def route_info(self, route: int):
+        path = np.zeros((PATH_LEN, 2), np.float32)
+        intent = ctypes.c_int32()
+        spawn = np.zeros(3, np.float32)
+        _check(self._lib.mev_route_info(self._h, int(route), path.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                        ctypes.byref(intent), spawn.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+        return path, intent.value, spawn
+
+    def point_xy(self, point: int):
+        xy = np.zeros(2, np.float32)
+        _check(self._lib.mev_point_xy(self._h, int(point), xy.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+        return xy
+
+    def set_ego_routes(self, routes):
+        r = np.ascontiguousarray(np.broadcast_to(np.asarray(routes, np.int32), (self.E, self.N)), np.int32)
+        _check(self._lib.mev_set_ego_routes(self._h, r.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+
+    def set_traffic_routes(self, routes):
+        r = np.ascontiguousarray(np.asarray(routes, np.int32).reshape(-1))
+        _check(self._lib.mev_set_traffic_routes(self._h, r.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(r)))
+
+    def default_traffic_routes(self):
+        cnt = ctypes.c_int32()
+        buf = np.zeros(1024, np.int32)
+        _check(self._lib.mev_default_traffic_routes(self._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                    ctypes.byref(cnt)))
+        return buf[: cnt.value].copy()
+
+    # -- reset / step -----------------------------------------------------
+    def reset(self, env_mask=None, obs=None, device: bool = False):
+        mask = None if env_mask is None else (env_mask if device else np.ascontiguousarray(env_mask, np.uint8))
+        _check(self._lib.mev_reset(self._h, _ptr(mask), _ptr(obs), MEV_DEVICE_PTRS if device else 0))
+        return obs
+
+    def alloc_outputs(self):
+        E, N, D = self.E, self.N, self.D
+        return dict(obs=np.zeros((E, N, D), np.float32), reward=np.zeros((E, N), np.float32),
+                    done=np.zeros((E, N), np.uint8), status=np.zeros((E, N), np.uint8),
+                    terminated=np.zeros(E, np.uint8), truncated=np.zeros(E, np.uint8),
+                    agents_alive=np.zeros(E, np.int32), step=np.zeros(E, np.int32))
+
+    def step(self, actions, dt: float = 1.0 / 60.0, out: Optional[dict] = None, spawn_route=None,
+             auto_reset: bool = False, device: bool = False):
+        """Host mode (default): numpy in/out, synchronous.  device=True: every
+        array is a device tensor/pointer on this handle's device; asynchronous."""
+        if not device:
+            actions = np.ascontiguousarray(actions, np.float32)
+            if actions.size != self.E * self.N * 2:
+                raise ValueError(f"actions must have {self.E}x{self.N}x2 elements, got {actions.shape}")
+            if spawn_route is not None:
+                spawn_route = np.ascontiguousarray(np.broadcast_to(np.asarray(spawn_route, np.int32), (self.E,)))
+            if out is None:
+                out = self.alloc_outputs()
+        a = MevStepArgs()
+        a.actions = _ptr(actions)
+        a.dt = float(dt)
+        a.spawn_route = _ptr(spawn_route)
+        out = out or {}
+        for k in ("obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step"):
+            setattr(a, k, _ptr(out.get(k)))
+        a.flags = (MEV_DEVICE_PTRS if device else 0) | (MEV_AUTO_RESET if auto_reset else 0)
+        _check(self._lib.mev_step(self._h, ctypes.byref(a)))
+        return out
+
+    def get_outputs(self, out: Optional[dict] = None):
+        out = out or self.alloc_outputs()
+        _check(self._lib.mev_get_outputs(self._h, *[_ptr(out.get(k)) for k in (
+            "obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step")], 0))
+        return out
+
+    def observations(self) -> np.ndarray:
+        obs = np.zeros((self.E, self.N, self.D), np.float32)
+        _check(self._lib.mev_get_outputs(self._h, _ptr(obs), None, None, None, None, None, None, None, 0))
+        return obs
+
+    # -- state ------------------------------------------------------------
+    def _shape(self, per):
+        return {"ego": (self.E, self.N), "npc": (self.E, self.K), "env": (self.E,)}[per]
+
+    def get_state(self) -> Dict[str, np.ndarray]:
+        st = MevState()
+        arrays = {}
+        for name, dt, per in STATE_FIELDS:
+            a = np.zeros(self._shape(per), dt)
+            arrays[name] = a
+            setattr(st, name, _ptr(a) if a.size else None)
+        _check(self._lib.mev_get_state(self._h, ctypes.byref(st)))
+        return arrays
+
+    def set_state(self, state: Dict[str, np.ndarray]):
+        st = MevState()
+        keep = []
+        for name, dt, per in STATE_FIELDS:
+            if name in state and state[name] is not None:
+                a = np.ascontiguousarray(np.broadcast_to(np.asarray(state[name], dt), self._shape(per)))
+                if a.size == 0:
+                    continue
+                keep.append(a)
+                setattr(st, name, _ptr(a))
+        _check(self._lib.mev_set_state(self._h, ctypes.byref(st)))
+
+    def npc_overflow(self) -> int:
+        v = ctypes.c_int64()
+        _check(self._lib.mev_npc_overflow(self._h, ctypes.byref(v)))
+        return v.value
+
+
+def device_count() -> int:
+    n = ctypes.c_int32()
+    load_library().mev_device_count(ctypes.byref(n))
+    return n.value

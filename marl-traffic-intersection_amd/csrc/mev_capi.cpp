@@ -1,0 +1,537 @@
+// mev_capi.cpp — the extern "C" boundary (include/marlenv.h): handle
+// lifetime, route tables, device buffers and the host side of reset / step /
+// state transfer.  Replaces the reference's pybind11 module MARLEnv
+// (cpp/bindings.cpp:11-95); see INTEGRATION.md for the caller-side bindings.
+#include "marlenv.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "mev_kernels.h"
+#include "mev_routes.h"
+#include "mev_world.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess) return fail(MEV_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+// reference utils.py:29-52 default ego route mappings (IN_k -> OUT_m), as point indices
+const int kMap3[12][2] = {{1, 4}, {2, 8}, {3, 12}, {4, 7}, {5, 11}, {6, 3},
+                          {7, 10}, {8, 2}, {9, 6}, {10, 1}, {11, 5}, {12, 9}};
+const int kMap2[7][2] = {{1, 3}, {2, 6}, {3, 5}, {4, 8}, {6, 2}, {7, 1}, {8, 4}};
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+    return hipMalloc(reinterpret_cast<void**>(p), (n ? n : 1) * sizeof(T));
+}
+
+}  // namespace
+
+struct mev_handle {
+    mev_config cfg{};
+    int D = 0, lidar_slots = 0, P = 0, nroutes = 0;
+    std::vector<mev::LanePoint> pts;
+    std::vector<float> h_paths, h_spawn;
+    std::vector<int32_t> h_intent;
+    std::vector<int32_t> h_traffic;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::vector<void*> allocs;
+    mev::SimParams sp{};
+    mev::Outputs internal{};
+    mev::Outputs last{};  // where the most recent outputs were written
+    float* d_actions = nullptr;
+    int32_t* d_spawn = nullptr;
+    uint8_t* d_mask = nullptr;
+    float* d_paths = nullptr;
+    float* d_spawn_tab = nullptr;
+    int32_t* d_intent = nullptr;
+    float* d_rel = nullptr;
+    int32_t* d_traffic = nullptr;
+    uint64_t rng_counter = 0;
+
+    template <class T>
+    hipError_t alloc(T** p, size_t n) {
+        hipError_t e = dalloc(p, n);
+        if (e == hipSuccess) {
+            allocs.push_back(*p);
+            e = hipMemsetAsync(*p, 0, (n ? n : 1) * sizeof(T), stream);
+        }
+        return e;
+    }
+    ~mev_handle() {
+        for (void* p : allocs) (void)hipFree(p);
+        if (own_stream) (void)hipStreamDestroy(own_stream);
+    }
+};
+
+extern "C" {
+
+const char* mev_last_error(void) { return g_err.c_str(); }
+int mev_abi_version(void) { return MEV_ABI_VERSION; }
+int mev_path_len(void) { return mev::PATH_LEN; }
+
+int mev_device_count(int32_t* count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    if (count) *count = n;
+    return MEV_OK;
+}
+
+int mev_config_default(mev_config* c) {
+    if (!c) return fail(MEV_E_INVALID, "null config");
+    memset(c, 0, sizeof(*c));
+    c->num_envs = 1;
+    c->num_agents = 1;
+    c->num_lanes = 3;
+    c->lidar_rays = 96;  // cpp/IntersectionEnv.cpp:113-116
+    c->lidar_fov_deg = 360.0f;
+    c->lidar_max_dist = 250.0f;
+    c->lidar_step = 4.0f;
+    c->obs_dim = 0;
+    c->traffic_flow = 0;
+    c->traffic_density = 0.5f;  // cpp/IntersectionEnv.h:35
+    c->use_team_reward = 0;
+    c->respawn_enabled = 1;
+    c->max_steps = 2000;
+    const float rc[8] = {10.0f, 1.0f, -0.01f, -10.0f, -5.0f, 10.0f, -0.02f, 0.2f};  // cpp/Reward.h:5-14
+    memcpy(c->reward, rc, sizeof(rc));
+    c->max_npcs = 32;
+    c->seed = 0;
+    c->device = 0;
+    return MEV_OK;
+}
+
+int mev_create(const mev_config* cfg, mev_handle** out) {
+    if (!cfg || !out) return fail(MEV_E_INVALID, "null argument");
+    const mev_config& c = *cfg;
+    if (c.num_envs < 1) return fail(MEV_E_INVALID, "num_envs must be >= 1");
+    if (c.num_agents < 1 || c.num_agents > 64) return fail(MEV_E_INVALID, "num_agents must be in [1, 64]");
+    if (c.num_lanes < 1 || c.num_lanes > 8) return fail(MEV_E_INVALID, "num_lanes must be in [1, 8]");
+    if (c.lidar_rays < 1 || c.lidar_rays > 4096) return fail(MEV_E_INVALID, "lidar_rays must be in [1, 4096]");
+    if (!(c.lidar_step > 0.0f) || !(c.lidar_max_dist > 0.0f)) return fail(MEV_E_INVALID, "lidar step/max_dist must be > 0");
+    if (c.max_npcs < 0 || c.max_npcs > 64) return fail(MEV_E_INVALID, "max_npcs must be in [0, 64]");
+    const int D = c.obs_dim > 0 ? c.obs_dim : mev::OBS_HEAD + c.lidar_rays;
+    if (D < mev::OBS_HEAD) return fail(MEV_E_INVALID, "obs_dim must be >= 31");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MEV_E_HIP, "no HIP device available");
+    if (c.device < 0 || c.device >= ndev) return fail(MEV_E_INVALID, "device ordinal out of range");
+    HIP_TRY(hipSetDevice(c.device));
+
+    auto* h = new mev_handle();
+    h->cfg = c;
+    if (h->cfg.traffic_density < 0.0f) h->cfg.traffic_density = 0.0f;  // configure_traffic (:56-60)
+    h->D = D;
+    h->lidar_slots = std::min(c.lidar_rays, D - mev::OBS_HEAD);
+    h->P = 8 * c.num_lanes;
+    h->nroutes = h->P * h->P;
+    h->pts = mev::build_lane_points(c.num_lanes);
+    h->h_paths.resize(size_t(h->nroutes) * 2 * mev::PATH_LEN);
+    h->h_intent.resize(size_t(h->nroutes));
+    h->h_spawn.resize(size_t(h->nroutes) * 3);
+    for (int s = 0; s < h->P; ++s)
+        for (int e = 0; e < h->P; ++e) {
+            const int r = s * h->P + e;
+            float* path = &h->h_paths[size_t(r) * 2 * mev::PATH_LEN];
+            h->h_intent[size_t(r)] = mev::generate_route(h->pts, c.num_lanes, s, e, path);
+            h->h_spawn[size_t(3 * r)] = h->pts[size_t(s)].x;
+            h->h_spawn[size_t(3 * r + 1)] = h->pts[size_t(s)].y;
+            h->h_spawn[size_t(3 * r + 2)] = mev::spawn_heading(path);
+        }
+    // LiDAR beam offsets, cpp/IntersectionEnv.cpp:119-127 (== Lidar.cpp:4-14)
+    std::vector<float> rel(size_t(c.lidar_rays));
+    {
+        const float start_angle_deg = -c.lidar_fov_deg * 0.5f;
+        const float step_deg = (c.lidar_rays > 1) ? (c.lidar_fov_deg / float(c.lidar_rays - 1)) : 0.0f;
+        const float PI_F2 = 3.14159265358979323846f;
+        for (int ii = 0; ii < c.lidar_rays; ++ii) {
+            const float deg = start_angle_deg + float(ii) * step_deg;
+            rel[size_t(ii)] = deg * PI_F2 / 180.0f;
+        }
+    }
+    h->h_traffic = mev::default_traffic_routes(c.num_lanes);
+
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return fail(MEV_E_HIP, "hipStreamCreate failed");
+    }
+    h->stream = h->own_stream;
+    const int E = c.num_envs, N = c.num_agents, K = std::max(1, c.max_npcs);
+    const size_t EN = size_t(E) * size_t(N), EK = size_t(E) * size_t(K);
+    mev::SimParams& p = h->sp;
+    hipError_t err = hipSuccess;
+    auto A = [&](auto** ptr, size_t n) { if (err == hipSuccess) err = h->alloc(ptr, n); };
+    // state
+    A(&p.ego.x, EN); A(&p.ego.y, EN); A(&p.ego.v, EN); A(&p.ego.h, EN); A(&p.ego.acc, EN); A(&p.ego.steer, EN);
+    A(&p.ego.prev_dist, EN); A(&p.ego.pa0, EN); A(&p.ego.pa1, EN);
+    A(&p.ego.sx, EN); A(&p.ego.sy, EN); A(&p.ego.sv, EN); A(&p.ego.sh, EN);
+    A(&p.ego.pidx, EN); A(&p.ego.route, EN); A(&p.ego.intent, EN); A(&p.ego.alive, EN);
+    A(&p.npc.x, EK); A(&p.npc.y, EK); A(&p.npc.v, EK); A(&p.npc.h, EK); A(&p.npc.acc, EK); A(&p.npc.steer, EK);
+    A(&p.npc.pidx, EK); A(&p.npc.route, EK); A(&p.npc.intent, EK); A(&p.npc.alive, EK); A(&p.npc.count, size_t(E));
+    A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 1);
+    // outputs
+    A(&h->internal.obs, EN * size_t(D)); A(&h->internal.rew, EN); A(&h->internal.done, EN); A(&h->internal.status, EN);
+    A(&h->internal.term, size_t(E)); A(&h->internal.trunc, size_t(E)); A(&h->internal.alive_cnt, size_t(E));
+    A(&h->internal.step, size_t(E));
+    // inputs & tables
+    A(&h->d_actions, EN * 2); A(&h->d_spawn, size_t(E)); A(&h->d_mask, size_t(E));
+    A(&h->d_paths, h->h_paths.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
+    A(&h->d_rel, rel.size()); A(&h->d_traffic, size_t(h->P) * size_t(h->P));
+    if (err != hipSuccess) {
+        std::string m = hipGetErrorString(err);
+        delete h;
+        return fail(MEV_E_NOMEM, "device allocation failed: " + m);
+    }
+    h->last = h->internal;
+    // upload tables
+    err = hipMemcpyAsync(h->d_paths, h->h_paths.data(), h->h_paths.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(h->d_spawn_tab, h->h_spawn.data(), h->h_spawn.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(h->d_intent, h->h_intent.data(), h->h_intent.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(h->d_rel, rel.data(), rel.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(h->d_traffic, h->h_traffic.data(), h->h_traffic.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
+    // default ego routes: reference env.py:138-145 (mapping routes, cyclic)
+    std::vector<int32_t> ego(EN);
+    {
+        const int L = c.num_lanes;
+        const int (*map)[2] = (L == 2) ? kMap2 : kMap3;
+        const int M = (L == 2) ? 7 : 12;
+        std::vector<int32_t> valid;
+        for (int k = 0; k < M; ++k) {
+            const int s = map[k][0] - 1, e = 4 * L + map[k][1] - 1;
+            if (map[k][0] <= 4 * L && map[k][1] <= 4 * L) valid.push_back(s * h->P + e);
+        }
+        if (valid.empty()) valid = h->h_traffic;
+        for (size_t i = 0; i < EN; ++i) ego[i] = valid[(i % size_t(N)) % valid.size()];
+    }
+    if (err == hipSuccess) err = hipMemcpyAsync(p.ego.route, ego.data(), ego.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(h->stream);
+    if (err != hipSuccess) {
+        std::string m = hipGetErrorString(err);
+        delete h;
+        return fail(MEV_E_HIP, "table upload failed: " + m);
+    }
+    // parameters
+    p.E = E; p.N = N; p.R = c.lidar_rays; p.K = c.max_npcs; p.D = D;
+    p.lidar_slots = h->lidar_slots;
+    p.num_lanes = c.num_lanes;
+    p.irw = int(c.num_lanes * int(mev::LANE_WIDTH_PX));
+    p.line_stop = int(c.num_lanes * int(mev::LANE_WIDTH_PX)) + int(mev::CORNER_RADIUS);  // LineMask.cpp:52-54
+    p.rw = c.num_lanes * mev::LANE_WIDTH_PX;  // RoadGeometry.h:16
+    p.use_team = c.use_team_reward;
+    p.respawn = c.respawn_enabled;
+    p.traffic = c.traffic_flow;
+    p.max_steps = c.max_steps;
+    p.k_prog = c.reward[0]; p.v_min = c.reward[1]; p.k_stuck = c.reward[2]; p.k_cv = c.reward[3];
+    p.k_co = c.reward[4]; p.k_succ = c.reward[5]; p.k_sm = c.reward[6]; p.alpha = c.reward[7];
+    p.max_progress = mev::hypotf(float(mev::WIDTH), float(mev::HEIGHT));  // IntersectionEnv.cpp:22
+    p.lidar_max = c.lidar_max_dist;
+    p.lidar_step = c.lidar_step;
+    p.lidar_inv = (c.lidar_max_dist > 0.0f) ? (1.0f / c.lidar_max_dist) : 0.0f;  // Lidar.cpp:94
+    p.spawn_prob = 0.0f;
+    p.seed = c.seed;
+    p.rt.path = h->d_paths;
+    p.rt.intent = h->d_intent;
+    p.rt.spawn = h->d_spawn_tab;
+    p.rt.nroutes = h->nroutes;
+    p.rel_angles = h->d_rel;
+    p.traffic_routes = h->d_traffic;
+    p.n_traffic_routes = int(h->h_traffic.size());
+    *out = h;
+    // initial state = a reset (the reference env.py constructor ends with reset(), env.py:136)
+    return mev_reset(h, nullptr, nullptr, 0);
+}
+
+int mev_destroy(mev_handle* h) {
+    if (!h) return MEV_OK;
+    (void)hipSetDevice(h->cfg.device);
+    (void)hipStreamSynchronize(h->stream);
+    delete h;
+    return MEV_OK;
+}
+
+int mev_get_config(const mev_handle* h, mev_config* cfg) {
+    if (!h || !cfg) return fail(MEV_E_INVALID, "null argument");
+    *cfg = h->cfg;
+    cfg->obs_dim = h->D;
+    return MEV_OK;
+}
+
+int mev_obs_dim(const mev_handle* h, int32_t* d) {
+    if (!h || !d) return fail(MEV_E_INVALID, "null argument");
+    *d = h->D;
+    return MEV_OK;
+}
+
+int mev_set_stream(mev_handle* h, void* stream) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    return MEV_OK;
+}
+
+int mev_sync(mev_handle* h) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+int mev_num_points(const mev_handle* h, int32_t* n) {
+    if (!h || !n) return fail(MEV_E_INVALID, "null argument");
+    *n = h->P;
+    return MEV_OK;
+}
+
+int mev_point_xy(const mev_handle* h, int32_t point, float* xy) {
+    if (!h || !xy) return fail(MEV_E_INVALID, "null argument");
+    if (point < 0 || point >= h->P) return fail(MEV_E_RANGE, "lane point out of range");
+    xy[0] = h->pts[size_t(point)].x;
+    xy[1] = h->pts[size_t(point)].y;
+    return MEV_OK;
+}
+
+int mev_route_id(const mev_handle* h, int32_t s, int32_t e, int32_t* route) {
+    if (!h || !route) return fail(MEV_E_INVALID, "null argument");
+    if (s < 0 || s >= h->P || e < 0 || e >= h->P) return fail(MEV_E_RANGE, "lane point out of range");
+    *route = s * h->P + e;
+    return MEV_OK;
+}
+
+int mev_route_info(const mev_handle* h, int32_t route, float* path, int32_t* intent, float* spawn) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (route < 0 || route >= h->nroutes) return fail(MEV_E_RANGE, "route out of range");
+    if (path) memcpy(path, &h->h_paths[size_t(route) * 2 * mev::PATH_LEN], sizeof(float) * 2 * mev::PATH_LEN);
+    if (intent) *intent = h->h_intent[size_t(route)];
+    if (spawn) memcpy(spawn, &h->h_spawn[size_t(3 * route)], sizeof(float) * 3);
+    return MEV_OK;
+}
+
+int mev_set_ego_routes(mev_handle* h, const int32_t* routes) {
+    if (!h || !routes) return fail(MEV_E_INVALID, "null argument");
+    const size_t EN = size_t(h->cfg.num_envs) * size_t(h->cfg.num_agents);
+    for (size_t i = 0; i < EN; ++i)
+        if (routes[i] < 0 || routes[i] >= h->nroutes) return fail(MEV_E_RANGE, "ego route id out of range");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipMemcpyAsync(h->sp.ego.route, routes, EN * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+int mev_set_traffic_routes(mev_handle* h, const int32_t* routes, int32_t count) {
+    if (!h || (count > 0 && !routes)) return fail(MEV_E_INVALID, "null argument");
+    if (count < 0 || count > h->nroutes) return fail(MEV_E_INVALID, "bad traffic route count");
+    for (int i = 0; i < count; ++i)
+        if (routes[i] < 0 || routes[i] >= h->nroutes) return fail(MEV_E_RANGE, "traffic route id out of range");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    h->h_traffic.assign(routes, routes + count);
+    if (count > 0)
+        HIP_TRY(hipMemcpyAsync(h->d_traffic, routes, size_t(count) * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->sp.n_traffic_routes = count;
+    return MEV_OK;
+}
+
+int mev_default_traffic_routes(const mev_handle* h, int32_t* routes, int32_t* count) {
+    if (!h || !count) return fail(MEV_E_INVALID, "null argument");
+    const auto d = mev::default_traffic_routes(h->cfg.num_lanes);
+    if (routes) memcpy(routes, d.data(), d.size() * sizeof(int32_t));
+    *count = int32_t(d.size());
+    return MEV_OK;
+}
+
+static mev::Outputs resolve_outputs(mev_handle* h, float* obs, float* rew, uint8_t* done, uint8_t* status, uint8_t* term,
+                                    uint8_t* trunc, int32_t* alive, int32_t* step, bool device) {
+    mev::Outputs o = h->internal;
+    if (device) {
+        if (obs) o.obs = obs;
+        if (rew) o.rew = rew;
+        if (done) o.done = done;
+        if (status) o.status = status;
+        if (term) o.term = term;
+        if (trunc) o.trunc = trunc;
+        if (alive) o.alive_cnt = alive;
+        if (step) o.step = step;
+    }
+    return o;
+}
+
+static int copy_out(mev_handle* h, const mev::Outputs& src, float* obs, float* rew, uint8_t* done, uint8_t* status,
+                    uint8_t* term, uint8_t* trunc, int32_t* alive, int32_t* step, hipMemcpyKind kind) {
+    const size_t E = size_t(h->cfg.num_envs), EN = E * size_t(h->cfg.num_agents);
+    auto cp = [&](void* dst, const void* s, size_t bytes) -> hipError_t {
+        if (!dst || dst == s) return hipSuccess;
+        return hipMemcpyAsync(dst, s, bytes, kind, h->stream);
+    };
+    HIP_TRY(cp(obs, src.obs, EN * size_t(h->D) * sizeof(float)));
+    HIP_TRY(cp(rew, src.rew, EN * sizeof(float)));
+    HIP_TRY(cp(done, src.done, EN));
+    HIP_TRY(cp(status, src.status, EN));
+    HIP_TRY(cp(term, src.term, E));
+    HIP_TRY(cp(trunc, src.trunc, E));
+    HIP_TRY(cp(alive, src.alive_cnt, E * sizeof(int32_t)));
+    HIP_TRY(cp(step, src.step, E * sizeof(int32_t)));
+    return MEV_OK;
+}
+
+int mev_reset(mev_handle* h, const uint8_t* env_mask, float* obs, uint32_t flags) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
+    const uint8_t* d_mask = nullptr;
+    if (env_mask) {
+        if (dev) d_mask = env_mask;
+        else {
+            HIP_TRY(hipMemcpyAsync(h->d_mask, env_mask, size_t(h->cfg.num_envs), hipMemcpyHostToDevice, h->stream));
+            d_mask = h->d_mask;
+        }
+    }
+    mev::Outputs o = h->internal;
+    if (dev && obs) o.obs = obs;
+    HIP_TRY(mev::launch_reset(h->sp, d_mask, o, h->stream));
+    h->last.obs = o.obs;
+    if (!dev) {
+        if (obs) HIP_TRY(hipMemcpyAsync(obs, o.obs, size_t(h->cfg.num_envs) * size_t(h->cfg.num_agents) * size_t(h->D) * sizeof(float),
+                                        hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    return MEV_OK;
+}
+
+int mev_step(mev_handle* h, const mev_step_args* a) {
+    if (!h || !a) return fail(MEV_E_INVALID, "null argument");
+    if (!a->actions) return fail(MEV_E_INVALID, "actions required");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const bool dev = (a->flags & MEV_DEVICE_PTRS) != 0;
+    const size_t E = size_t(h->cfg.num_envs), EN = E * size_t(h->cfg.num_agents);
+    mev::StepInputs in{};
+    in.dt = a->dt;
+    in.auto_reset = (a->flags & MEV_AUTO_RESET) ? 1 : 0;
+    in.rng_counter = h->rng_counter++;
+    if (dev) {
+        in.actions = a->actions;
+        in.spawn_route = a->spawn_route;
+    } else {
+        HIP_TRY(hipMemcpyAsync(h->d_actions, a->actions, EN * 2 * sizeof(float), hipMemcpyHostToDevice, h->stream));
+        in.actions = h->d_actions;
+        if (a->spawn_route) {
+            HIP_TRY(hipMemcpyAsync(h->d_spawn, a->spawn_route, E * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+            in.spawn_route = h->d_spawn;
+        }
+    }
+    // spawn probability, TrafficFlow.cpp:321-322 (host glibc expf, bit-identical to the reference)
+    h->sp.spawn_prob = 1.0f - expf(-h->cfg.traffic_density * a->dt);
+    const mev::Outputs o = resolve_outputs(h, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated,
+                                           a->agents_alive, a->step, dev);
+    HIP_TRY(mev::launch_step(h->sp, in, o, h->stream));
+    h->last = o;
+    if (!dev) {
+        int r = copy_out(h, o, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated, a->agents_alive,
+                         a->step, hipMemcpyDeviceToHost);
+        if (r) return r;
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    return MEV_OK;
+}
+
+int mev_get_outputs(mev_handle* h, float* obs, float* rew, uint8_t* done, uint8_t* status, uint8_t* term,
+                    uint8_t* trunc, int32_t* alive, int32_t* step, uint32_t flags) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
+    int r = copy_out(h, h->last, obs, rew, done, status, term, trunc, alive, step,
+                     dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost);
+    if (r) return r;
+    if (!dev) HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+#define STATE_FIELDS(X)                                                                                    \
+    X(x, ego.x, EN, float) X(y, ego.y, EN, float) X(v, ego.v, EN, float) X(heading, ego.h, EN, float)      \
+    X(acc, ego.acc, EN, float) X(steering, ego.steer, EN, float) X(prev_dist, ego.prev_dist, EN, float)    \
+    X(prev_a0, ego.pa0, EN, float) X(prev_a1, ego.pa1, EN, float) X(spawn_x, ego.sx, EN, float)            \
+    X(spawn_y, ego.sy, EN, float) X(spawn_v, ego.sv, EN, float) X(spawn_heading, ego.sh, EN, float)        \
+    X(path_index, ego.pidx, EN, int32_t) X(route, ego.route, EN, int32_t)                                  \
+    X(intention, ego.intent, EN, int32_t) X(alive, ego.alive, EN, uint8_t)                                 \
+    X(npc_x, npc.x, EK, float) X(npc_y, npc.y, EK, float) X(npc_v, npc.v, EK, float)                        \
+    X(npc_heading, npc.h, EK, float) X(npc_acc, npc.acc, EK, float) X(npc_steering, npc.steer, EK, float)  \
+    X(npc_path_index, npc.pidx, EK, int32_t) X(npc_route, npc.route, EK, int32_t)                          \
+    X(npc_intention, npc.intent, EK, int32_t) X(npc_alive, npc.alive, EK, uint8_t)                         \
+    X(npc_count, npc.count, E, int32_t) X(step_count, step_count, E, int32_t)
+
+int mev_get_state(mev_handle* h, const mev_state* s) {
+    if (!h || !s) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const size_t E = size_t(h->cfg.num_envs), EN = E * size_t(h->cfg.num_agents);
+    const size_t EK = E * size_t(h->cfg.max_npcs);
+#define GET(f, dev, n, T) \
+    if (s->f) HIP_TRY(hipMemcpyAsync(s->f, h->sp.dev, (n) * sizeof(T), hipMemcpyDeviceToHost, h->stream));
+    STATE_FIELDS(GET)
+#undef GET
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+int mev_set_state(mev_handle* h, const mev_state* s) {
+    if (!h || !s) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const size_t E = size_t(h->cfg.num_envs), EN = E * size_t(h->cfg.num_agents);
+    const size_t EK = E * size_t(h->cfg.max_npcs);
+    if (s->route)
+        for (size_t i = 0; i < EN; ++i)
+            if (s->route[i] < 0 || s->route[i] >= h->nroutes) return fail(MEV_E_RANGE, "route id out of range");
+    if (s->npc_count)
+        for (size_t e = 0; e < E; ++e)
+            if (s->npc_count[e] < 0 || s->npc_count[e] > h->cfg.max_npcs) return fail(MEV_E_RANGE, "npc_count out of range");
+    if (s->npc_route)
+        for (size_t i = 0; i < EK; ++i)
+            if (s->npc_route[i] < 0 || s->npc_route[i] >= h->nroutes) return fail(MEV_E_RANGE, "npc route id out of range");
+#define SET(f, dev, n, T) \
+    if (s->f) HIP_TRY(hipMemcpyAsync(h->sp.dev, s->f, (n) * sizeof(T), hipMemcpyHostToDevice, h->stream));
+    STATE_FIELDS(SET)
+#undef SET
+    HIP_TRY(hipMemsetAsync(h->sp.pending_reset, 0, E, h->stream));
+    HIP_TRY(mev::launch_observe_reset_lidar(h->sp, h->internal, h->stream));
+    h->last.obs = h->internal.obs;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+int mev_device_outputs(mev_handle* h, float** obs, float** rew, uint8_t** done, uint8_t** status, uint8_t** term,
+                       uint8_t** trunc) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (obs) *obs = h->internal.obs;
+    if (rew) *rew = h->internal.rew;
+    if (done) *done = h->internal.done;
+    if (status) *status = h->internal.status;
+    if (term) *term = h->internal.term;
+    if (trunc) *trunc = h->internal.trunc;
+    return MEV_OK;
+}
+
+int mev_npc_overflow(mev_handle* h, int64_t* count) {
+    if (!h || !count) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    unsigned long long v = 0;
+    HIP_TRY(hipMemcpyAsync(&v, h->sp.overflow, sizeof(v), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    *count = int64_t(v);
+    return MEV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// mev_kernels.h — device-side data layout and kernel launchers of the
+// batched intersection environment (gfx950).
+//
+// HBM layout (structure of arrays; env e, agent i, NPC slot k):
+//   ego field f      : f[e*N + i]            (x, y, v, heading, acc, steering, prev_dist,
+//                                             prev_a0, prev_a1, spawn_x/y/v/heading: f32;
+//                                             path_index, route, intention: i32; alive: u8)
+//   npc field f      : f[e*K + k]  K = max_npcs, live slots are a prefix of length npc_count[e]
+//   per-env          : step_count, npc_count (i32), pending_reset (u8)
+//   outputs          : obs[(e*N + i)*D + c] f32 (D = obs_dim), reward/done/status [e*N+i],
+//                      terminated/truncated/agents_alive/step [e]
+//   constant tables  : route paths [P*P][160][2] f32 (P = 8L lane points), route intent /
+//                      spawn (x, y, heading) / success axis, LiDAR beam offsets [R] f32,
+//                      NPC route list [M] i32
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mev {
+
+struct EgoSoA {
+    float *x, *y, *v, *h, *acc, *steer, *prev_dist, *pa0, *pa1, *sx, *sy, *sv, *sh;
+    int32_t *pidx, *route, *intent;
+    uint8_t* alive;
+};
+
+struct NpcSoA {
+    float *x, *y, *v, *h, *acc, *steer;
+    int32_t *pidx, *route, *intent;
+    uint8_t* alive;
+    int32_t* count;
+};
+
+struct RouteTab {
+    const float* path;      // [nroutes][160][2]
+    const int32_t* intent;  // [nroutes]
+    const float* spawn;     // [nroutes][3]  x, y, heading
+    int32_t nroutes;
+};
+
+struct Outputs {
+    float* obs;
+    float* rew;
+    uint8_t* done;
+    uint8_t* status;
+    uint8_t* term;
+    uint8_t* trunc;
+    int32_t* alive_cnt;
+    int32_t* step;
+};
+
+struct SimParams {
+    int32_t E, N, R, K, D;   // envs, agents, beams, npc slots, obs_dim
+    int32_t lidar_slots;     // min(R, D - 31)
+    int32_t num_lanes;
+    int32_t irw;             // road half width in px (L*42)
+    int32_t line_stop;       // LineMask stop offset int(L*42) + 84
+    float rw;                // road half width (float)
+    int32_t use_team, respawn, traffic, max_steps;
+    float k_prog, v_min, k_stuck, k_cv, k_co, k_succ, k_sm, alpha;
+    float max_progress;      // hypot(750, 750)
+    float lidar_max, lidar_step, lidar_inv;
+    float spawn_prob;        // 1 - expf(-density * dt) computed on host with glibc
+    uint64_t seed;
+    EgoSoA ego;
+    NpcSoA npc;
+    RouteTab rt;
+    const float* rel_angles;  // [R]
+    const int32_t* traffic_routes;  // [M] route ids
+    int32_t n_traffic_routes;
+    int32_t* step_count;      // [E]
+    uint8_t* pending_reset;   // [E]
+    unsigned long long* overflow;  // [1]
+};
+
+struct StepInputs {
+    const float* actions;      // [E*N*2]
+    const int32_t* spawn_route;  // [E] or null
+    float dt;
+    int32_t auto_reset;
+    uint64_t rng_counter;      // handle-wide step counter (Philox counter for NPC spawns)
+};
+
+hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s);
+hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s);
+// recompute the observation rows from the current state with LiDAR = max (after set_state)
+hipError_t launch_observe_reset_lidar(const SimParams& p, const Outputs& out, hipStream_t s);
+
+}  // namespace mev

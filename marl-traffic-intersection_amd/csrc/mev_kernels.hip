@@ -1,0 +1,895 @@
+// mev_kernels.hip — the hot path: one fused step of E intersection envs on gfx950.
+//
+// Mapping: one 64-lane wavefront == one workgroup == one env.  Per-env state
+// (<= 64 egos, <= 64 NPCs) is staged in LDS; lanes take agents for the
+// per-car phases, (agent, beam) pairs for the LiDAR march, ghost-path points
+// for the NPC conflict scan and car pairs for SAT collision.  The reference's
+// order-dependent loops (greedy collision marking, Gauss-Seidel NPC control,
+// order-preserving NPC erase) are kept exact with 64-bit lane masks
+// (ballot / popcount) instead of serial loops over cars.
+//
+// Reference: cpp/IntersectionEnv.cpp:133-392 (step), :418-520 (observations),
+// cpp/TrafficFlow.cpp:22-196, 317-367 (NPCs), cpp/Car.cpp (kinematics, SAT),
+// cpp/Lidar.cpp:16-90 (ray march).  Compiled with -ffp-contract=off.
+#include <type_traits>
+
+#include "mev_kernels.h"
+#include "mev_world.h"
+
+namespace mev {
+
+constexpr int WAVE = 64;
+constexpr int MAXN = 64;
+constexpr int MAXK = 64;
+constexpr int MAXOB = MAXN + MAXK;
+
+// --------------------------------------------------------------- helpers ---
+__device__ inline unsigned long long ballot(bool p) { return __ballot(p); }
+
+__device__ inline float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float w = __shfl_xor(v, o);
+        v = (w < v) ? w : v;
+    }
+    return v;
+}
+
+// argmin over lanes of (d, i), ties -> smaller i; NaN treated as +inf.
+__device__ inline int wave_argmin_first(float d, int i) {
+    if (d != d) d = __builtin_inff();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float d2 = __shfl_xor(d, o);
+        const int i2 = __shfl_xor(i, o);
+        if (d2 < d || (d2 == d && i2 < i)) { d = d2; i = i2; }
+    }
+    return i;
+}
+
+// Philox4x32-10 (Salmon et al. 2011), counter (a, b, c, 0), key seed.
+__device__ inline void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint64_t seed, uint32_t* r0, uint32_t* r1) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = 0x9e3779b9u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * x0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * x2;
+        const uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ k0;
+        const uint32_t y2 = (uint32_t)(p0 >> 32) ^ x3 ^ k1;
+        x1 = (uint32_t)p1;
+        x3 = (uint32_t)p0;
+        x0 = y0;
+        x2 = y2;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    *r0 = x0;
+    *r1 = x1;
+}
+
+__device__ inline float u01(uint32_t r) { return (float)(r >> 8) * 0x1p-24f; }
+
+// Car::update_path_index (cpp/Car.cpp:47-74): argmin of squared distance over
+// path[idx, idx+50) — one window point per lane, strict '<' => first minimum wins.
+__device__ inline int path_index_update(const float* path, int idx, float x, float y, int lane) {
+    int start_i = idx < 0 ? 0 : idx;
+    int end_i = start_i + 50;
+    if (end_i > PATH_LEN) end_i = PATH_LEN;
+    const int i = start_i + lane;
+    float d = __builtin_inff();
+    if (lane < 50 && i < end_i) {
+        const float dx = path[2 * i] - x;
+        const float dy = path[2 * i + 1] - y;
+        d = dx * dx + dy * dy;
+    }
+    const int best = wave_argmin_first(d, (lane < 50 && i < end_i) ? i : 0x7fffffff);
+    return best == 0x7fffffff ? start_i : best;
+}
+
+// -------------------------------------------------------- shared state ---
+struct EgoLDS {
+    float x[MAXN], y[MAXN], v[MAXN], h[MAXN], c[MAXN], s[MAXN];
+    float cx[MAXN][4], cy[MAXN][4];
+    int32_t pidx[MAXN], intent[MAXN];
+    uint8_t alive[MAXN], done[MAXN], status[MAXN];
+    float rew[MAXN];
+    unsigned long long col[MAXN];
+    uint8_t colnpc[MAXN];
+};
+
+struct NpcLDS {
+    float x[MAXK], y[MAXK], v[MAXK], h[MAXK], c[MAXK], s[MAXK], acc[MAXK], steer[MAXK];
+    int32_t pidx[MAXK], route[MAXK], intent[MAXK];
+    uint8_t alive[MAXK];
+    float cx[MAXK][4], cy[MAXK][4];
+    unsigned long long col[MAXK];
+    uint8_t pair_ok[MAXK], yield_far[MAXK];
+};
+
+struct ObsLDS {
+    int x0[MAXOB], x1[MAXOB], y0[MAXOB], y1[MAXOB];
+    float px[MAXOB], py[MAXOB], ph[MAXOB];
+};
+
+// --------------------------------------------------- NPC traffic phase ---
+// update_traffic_flow, cpp/TrafficFlow.cpp:317-367, for env e.  Egos are read
+// (spawn blocking) but not moved.  On return NpcLDS holds the compacted NPCs.
+__device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NpcLDS& nl, int lane) {
+    const int K = p.K;
+    // load
+    if (lane < cnt) {
+        const int g = e * K + lane;
+        nl.x[lane] = p.npc.x[g];
+        nl.y[lane] = p.npc.y[g];
+        nl.v[lane] = p.npc.v[g];
+        nl.h[lane] = p.npc.h[g];
+        nl.acc[lane] = p.npc.acc[g];
+        nl.steer[lane] = p.npc.steer[g];
+        nl.pidx[lane] = p.npc.pidx[g];
+        nl.route[lane] = p.npc.route[g];
+        nl.intent[lane] = p.npc.intent[g];
+        nl.alive[lane] = p.npc.alive[g];
+    }
+    // -- spawn (TrafficFlow.cpp:320-329, try_spawn_traffic_car :275-315)
+    int r = -1;
+    if (in.spawn_route) {
+        r = in.spawn_route[e];
+        if (r >= p.n_traffic_routes) r = -1;
+    } else if (p.n_traffic_routes > 0) {
+        uint32_t a0, a1;
+        philox((uint32_t)in.rng_counter, (uint32_t)(in.rng_counter >> 32), (uint32_t)e, p.seed, &a0, &a1);
+        if (u01(a0) < p.spawn_prob) {
+            r = (int)(((uint64_t)a1 * (uint32_t)p.n_traffic_routes) >> 32);
+        }
+    }
+    if (r >= 0) {
+        const int rid = p.traffic_routes[r];
+        const float sx = p.rt.spawn[3 * rid], sy = p.rt.spawn[3 * rid + 1];
+        const float min_dist = CAR_LENGTH * 2.5f;
+        const float min_d2 = min_dist * min_dist;
+        // is_spawn_blocked (:240-259): every ego (alive or not) and every NPC
+        bool blk = false;
+        for (int base = 0; base < p.N; base += WAVE) {
+            const int i = base + lane;
+            bool b = false;
+            if (i < p.N) {
+                const float dx = p.ego.x[e * p.N + i] - sx;
+                const float dy = p.ego.y[e * p.N + i] - sy;
+                b = dx * dx + dy * dy < min_d2;
+            }
+            blk |= ballot(b) != 0ull;
+        }
+        {
+            bool b = false;
+            if (lane < cnt) {
+                const float dx = nl.x[lane] - sx;
+                const float dy = nl.y[lane] - sy;
+                b = dx * dx + dy * dy < min_d2;
+            }
+            blk |= ballot(b) != 0ull;
+        }
+        if (!blk) {
+            if (cnt < K) {
+                if (lane == 0) {
+                    nl.x[cnt] = sx;
+                    nl.y[cnt] = sy;
+                    nl.v[cnt] = 0.0f;
+                    nl.h[cnt] = p.rt.spawn[3 * rid + 2];
+                    nl.acc[cnt] = 0.0f;
+                    nl.steer[cnt] = 0.0f;
+                    nl.pidx[cnt] = 0;
+                    nl.route[cnt] = rid;
+                    nl.intent[cnt] = p.rt.intent[rid];
+                    nl.alive[cnt] = 1;
+                }
+                ++cnt;
+            } else if (lane == 0) {
+                atomicAdd(p.overflow, 1ull);
+            }
+        }
+    }
+    __syncthreads();
+    if (lane < cnt) {
+        float s, c;
+        sincosf(nl.h[lane], &s, &c);
+        nl.s[lane] = s;
+        nl.c[lane] = c;
+    }
+    __syncthreads();
+
+    // -- sequential controller over NPCs in vector order (Gauss-Seidel, :337-344)
+    const float CXf = WIDTH * 0.5f, CYf = HEIGHT * 0.5f;
+    for (int k = 0; k < cnt; ++k) {
+        if (!nl.alive[k]) continue;
+        const float* path = p.rt.path + (size_t)nl.route[k] * (2 * PATH_LEN);
+        float x = nl.x[k], y = nl.y[k];
+        int pidx = path_index_update(path, nl.pidx[k], x, y, lane);
+        const float h = nl.h[k], v = nl.v[k];
+        const float ck = nl.c[k], sk = nl.s[k];
+
+        // plan_npc_action_tf (:49-196) — 1) lateral
+        int tidx = pidx + 12;
+        if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
+        const float tdx = path[2 * tidx] - x;
+        const float tdy = path[2 * tidx + 1] - y;
+        const float heading_err = wrap_angle(atan2f(-tdy, tdx) - h);
+        float steer_cmd = heading_err * 3.0f;
+        steer_cmd = (1.0f < steer_cmd) ? 1.0f : steer_cmd;  // std::min(1, .)
+        steer_cmd = (steer_cmd < -1.0f) ? -1.0f : steer_cmd;  // std::max(-1, .)
+        // 2) longitudinal cruise + front car (get_front_car_dist_tf :22-47)
+        const float target_speed = PHYSICS_MAX_SPEED * 0.4f;
+        float acc_thr = 0.0f;
+        if (v < target_speed) acc_thr = 0.5f;
+        else if (v > target_speed + 1.0f) acc_thr = -0.1f;
+        const float vx = ck, vy = -sk;
+        float fd = 1e9f;
+        const int j = lane;
+        bool jvalid = j < cnt && j != k && nl.alive[j];
+        float oxj = 0, oyj = 0, ohj = 0, ovj = 0, ocj = 0, osj = 0;
+        if (j < cnt) {
+            oxj = nl.x[j]; oyj = nl.y[j]; ohj = nl.h[j]; ovj = nl.v[j]; ocj = nl.c[j]; osj = nl.s[j];
+        }
+        if (jvalid) {
+            const float dx = oxj - x;
+            const float dy = oyj - y;
+            const float dist = hypotf(dx, dy);
+            if (!(dist > 80.0f)) {
+                const float dot = (dx * vx + dy * vy) / (dist + 1e-5f);
+                if (dot > 0.8f) {
+                    const float angle_diff = fabs_f(wrap_angle(h - ohj));
+                    if (angle_diff < (45.0f * PI_F / 180.0f)) fd = dist;
+                }
+            }
+        }
+        fd = wave_min(fd);
+        if (fd < 30.0f) acc_thr = -1.0f;
+        else if (fd < 50.0f) acc_thr = (-0.2f < acc_thr) ? -0.2f : acc_thr;
+
+        // 3) ghost path scan: per-other terms first (independent of the ghost point)
+        const float my_dist_to_center = hypotf(x - CXf, y - CYf);
+        uint8_t pok = 0, yfar = 0;
+        if (jvalid) {
+            const float angle_diff = fabs_f(wrap_angle(h - ohj));
+            pok = 1;
+            if (angle_diff < (60.0f * PI_F / 180.0f)) pok = 0;
+            if (pok) {
+                const float dxo = oxj - x;
+                const float dyo = oyj - y;
+                const float dist_o = hypotf(dxo, dyo);
+                if (dist_o > 1e-5f) {
+                    const float mdx = ck, mdy = -sk;
+                    const float two_pi_m = 2.0f * PI_F - angle_diff;
+                    const float adn = (two_pi_m < angle_diff) ? two_pi_m : angle_diff;
+                    const bool parallel = (adn < (30.0f * PI_F / 180.0f)) || (adn > (150.0f * PI_F / 180.0f));
+                    if (parallel) {
+                        const float lon = dxo * mdx + dyo * mdy;
+                        float lsq = dist_o * dist_o - lon * lon;
+                        lsq = (0.0f < lsq) ? lsq : 0.0f;  // std::max(0, .)
+                        const float lat = __builtin_sqrtf(lsq);
+                        const bool sideways = fabs_f(lat) < (LANE_WIDTH_PX * 1.5f);
+                        const bool near_lon = fabs_f(lon) < (CAR_LENGTH * 2.0f);
+                        if (sideways && near_lon) {
+                            const float fdist = 20.0f;
+                            const float mfx = x + mdx * fdist;
+                            const float mfy = y + mdy * fdist;
+                            const float odx = ocj, ody = -osj;
+                            const float ofx = oxj + odx * fdist;
+                            const float ofy = oyj + ody * fdist;
+                            const float fdx = ofx - mfx;
+                            const float fdy = ofy - mfy;
+                            const float fmag = hypotf(fdx, fdy);
+                            if (fmag > 1e-5f) {
+                                const float flon = fdx * mdx + fdy * mdy;
+                                float flsq = fmag * fmag - flon * flon;
+                                flsq = (0.0f < flsq) ? flsq : 0.0f;
+                                const float flat = __builtin_sqrtf(flsq);
+                                const float change = fabs_f(flat - lat);
+                                if (change < (LANE_WIDTH_PX * 0.5f)) pok = 0;  // side by side: skip
+                            }
+                        }
+                    }
+                }
+            }
+            if (pok) {
+                const float odc = hypotf(oxj - CXf, oyj - CYf);
+                if (v < 1.0f && ovj > 3.0f && odc < my_dist_to_center + 25.0f) yfar = 1;
+                else if (odc < my_dist_to_center - 5.0f) yfar = 1;
+                else if (fabs_f(odc - my_dist_to_center) <= 5.0f) yfar = (k < j) ? 1 : 0;  // address order
+            }
+        }
+        if (j < MAXK) {
+            nl.pair_ok[j] = pok;
+            nl.yield_far[j] = yfar;
+        }
+        __syncthreads();
+        // scan ghost points path[pidx, min(pidx+120, 160)); first conflicting point wins
+        const int g_start = pidx;
+        int g_end = pidx + 120;
+        if (g_end > PATH_LEN) g_end = PATH_LEN;
+        const float SAFE = CAR_WIDTH * 2.0f;
+        const float SAFE_SQ = SAFE * SAFE;
+        bool conflict = false;
+        float min_conflict = 1e9f;
+        for (int base = g_start; base < g_end; base += WAVE) {
+            const int gi = base + lane;
+            bool hit = false;
+            float dtc = 0.0f;
+            if (gi < g_end) {
+                const float gx = path[2 * gi], gy = path[2 * gi + 1];
+                dtc = hypotf(gx - x, gy - y);
+                for (int o = 0; o < cnt; ++o) {
+                    if (!nl.pair_ok[o]) continue;
+                    const float dxg = nl.x[o] - gx;
+                    const float dyg = nl.y[o] - gy;
+                    if (dxg * dxg + dyg * dyg < SAFE_SQ && (dtc < 15.0f || nl.yield_far[o])) { hit = true; break; }
+                }
+            }
+            const unsigned long long m = ballot(hit);
+            if (m) {
+                const int first = __builtin_ctzll(m);
+                min_conflict = __shfl(dtc, first);
+                conflict = true;
+                break;
+            }
+        }
+        // 4) compose
+        float thr = acc_thr;
+        if (conflict) {
+            if (min_conflict < 35.0f) thr = -1.0f;
+            else if (min_conflict < 60.0f) thr = -0.8f;
+            else thr = (0.0f < thr) ? 0.0f : thr;
+        }
+        // Car::update + second path-index update (:342-343); every lane computes it redundantly
+        Kin kin{x, y, v, h, nl.acc[k], nl.steer[k]};
+        float cn, sn;
+        car_update(kin, thr, steer_cmd, in.dt, &cn, &sn);
+        pidx = path_index_update(path, pidx, kin.x, kin.y, lane);
+        __syncthreads();
+        if (lane == 0) {
+            nl.x[k] = kin.x; nl.y[k] = kin.y; nl.v[k] = kin.v; nl.h[k] = kin.h;
+            nl.acc[k] = kin.acc; nl.steer[k] = kin.steer; nl.pidx[k] = pidx;
+            nl.c[k] = cn; nl.s[k] = sn;
+        }
+        __syncthreads();
+    }
+
+    // -- NPC-NPC collision: greedy i<j, both removed (:347-356)
+    if (lane < cnt) {
+        car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
+        nl.col[lane] = 0ull;
+    }
+    __syncthreads();
+    for (int pbase = 0; pbase < cnt * cnt; pbase += WAVE) {
+        const int pi = pbase + lane;
+        if (pi < cnt * cnt) {
+            const int a = pi / cnt, b = pi % cnt;
+            if (a < b && sat_collide(nl.cx[a], nl.cy[a], nl.c[a], nl.s[a], nl.cx[b], nl.cy[b], nl.c[b], nl.s[b]))
+                atomicOr(&nl.col[a], 1ull << b);
+        }
+    }
+    __syncthreads();
+    unsigned long long alive_m = ballot(lane < cnt && nl.alive[lane]);
+    for (int i = 0; i < cnt; ++i) {
+        if (!((alive_m >> i) & 1ull)) continue;
+        const unsigned long long hits = nl.col[i] & alive_m;  // col[i] holds only j > i
+        if (hits) alive_m &= ~(hits | (1ull << i));
+    }
+    // -- erase dead / arrived / out-of-screen, order preserving (:359-366)
+    bool keep = false;
+    if (lane < cnt && ((alive_m >> lane) & 1ull)) {
+        const float* path = p.rt.path + (size_t)nl.route[lane] * (2 * PATH_LEN);
+        const float gx = path[2 * (PATH_LEN - 1)], gy = path[2 * (PATH_LEN - 1) + 1];
+        const bool arrived = hypotf(nl.x[lane] - gx, nl.y[lane] - gy) < 20.0f;
+        const float x = nl.x[lane], y = nl.y[lane];
+        const float m = 100.0f;
+        const bool oos = x < -m || x > float(WIDTH) + m || y < -m || y > float(HEIGHT) + m;
+        keep = !arrived && !oos;
+    }
+    const unsigned long long keep_m = ballot(keep);
+    const int dst = __builtin_popcountll(keep_m & ((1ull << lane) - 1ull));
+    float kx = 0, ky = 0, kv = 0, kh = 0, ka = 0, ks = 0, kc = 0, ksn = 0;
+    int kp = 0, kr = 0, ki = 0;
+    if (keep) {
+        kx = nl.x[lane]; ky = nl.y[lane]; kv = nl.v[lane]; kh = nl.h[lane]; ka = nl.acc[lane]; ks = nl.steer[lane];
+        kc = nl.c[lane]; ksn = nl.s[lane]; kp = nl.pidx[lane]; kr = nl.route[lane]; ki = nl.intent[lane];
+    }
+    __syncthreads();
+    if (keep) {
+        nl.x[dst] = kx; nl.y[dst] = ky; nl.v[dst] = kv; nl.h[dst] = kh; nl.acc[dst] = ka; nl.steer[dst] = ks;
+        nl.c[dst] = kc; nl.s[dst] = ksn; nl.pidx[dst] = kp; nl.route[dst] = kr; nl.intent[dst] = ki; nl.alive[dst] = 1;
+    }
+    const int newcnt = __builtin_popcountll(keep_m);
+    __syncthreads();
+    // store back + corners of the survivors (for ego-NPC SAT)
+    if (lane < newcnt) {
+        const int g = e * K + lane;
+        p.npc.x[g] = nl.x[lane]; p.npc.y[g] = nl.y[lane]; p.npc.v[g] = nl.v[lane]; p.npc.h[g] = nl.h[lane];
+        p.npc.acc[g] = nl.acc[lane]; p.npc.steer[g] = nl.steer[lane]; p.npc.pidx[g] = nl.pidx[lane];
+        p.npc.route[g] = nl.route[lane]; p.npc.intent[g] = nl.intent[lane]; p.npc.alive[g] = 1;
+        car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
+    }
+    if (lane == 0) p.npc.count[e] = newcnt;
+    __syncthreads();
+    return newcnt;
+}
+
+// ---------------------------------------------------- observation rows ---
+// get_observations (cpp/IntersectionEnv.cpp:418-520) minus the LiDAR block:
+// ego features, path look-ahead, 5 nearest alive neighbours (egos first, then
+// NPCs; stable by distance == libstdc++ insertion sort for <= 16 candidates).
+template <bool TRAFFIC>
+__device__ void write_obs_head(const SimParams& p, int i, const EgoLDS& el, const NpcLDS* nl, int ncnt,
+                               const float* path, int pidx, float* row) {
+    const float x = el.x[i], y = el.y[i], v = el.v[i], h = el.h[i];
+    row[0] = x / float(WIDTH);
+    row[1] = y / float(HEIGHT);
+    row[2] = v / PHYSICS_MAX_SPEED;
+    row[3] = h / PI_F;
+    int tidx = pidx + 10;
+    if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
+    const float dxd = path[2 * tidx] - x;
+    const float dyd = path[2 * tidx + 1] - y;
+    row[4] = __builtin_sqrtf(dxd * dxd + dyd * dyd) / float(WIDTH);
+    row[5] = wrap_angle(atan2f(-dyd, dxd) - h) / PI_F;
+    // top-5 insertion (stable)
+    float bd[NEIGHBOR_COUNT];
+    int bi[NEIGHBOR_COUNT];
+    int nb = 0;
+    const int ncand = p.N + (TRAFFIC ? ncnt : 0);
+    for (int j = 0; j < ncand; ++j) {
+        float ox, oy;
+        if (j < p.N) {
+            if (j == i || !el.alive[j]) continue;
+            ox = el.x[j]; oy = el.y[j];
+        } else {
+            const int k = j - p.N;
+            if (!nl->alive[k]) continue;
+            ox = nl->x[k]; oy = nl->y[k];
+        }
+        const float dx = ox - x;
+        const float dy = oy - y;
+        const float d = __builtin_sqrtf(dx * dx + dy * dy);
+        // stable insertion into the first 5 slots
+        int pos = nb;
+        while (pos > 0 && bd[pos - 1] > d) --pos;
+        if (pos >= NEIGHBOR_COUNT) continue;
+        const int last = nb < NEIGHBOR_COUNT ? nb : NEIGHBOR_COUNT - 1;
+        for (int q = last; q > pos; --q) { bd[q] = bd[q - 1]; bi[q] = bi[q - 1]; }
+        bd[pos] = d;
+        bi[pos] = j < p.N ? j : MAXN + (j - p.N);
+        if (nb < NEIGHBOR_COUNT) ++nb;
+    }
+    for (int q = 0; q < NEIGHBOR_COUNT; ++q) {
+        float* o = row + 6 + 5 * q;
+        if (q < nb) {
+            const int id = bi[q];
+            float ox, oy, ov, oh;
+            int oi;
+            if (id < MAXN) { ox = el.x[id]; oy = el.y[id]; ov = el.v[id]; oh = el.h[id]; oi = el.intent[id]; }
+            else { const int k = id - MAXN; ox = nl->x[k]; oy = nl->y[k]; ov = nl->v[k]; oh = nl->h[k]; oi = nl->intent[k]; }
+            o[0] = (ox - x) / float(WIDTH);
+            o[1] = (oy - y) / float(HEIGHT);
+            o[2] = (ov - v) / PHYSICS_MAX_SPEED;
+            o[3] = wrap_angle(oh - h) / PI_F;
+            o[4] = float(oi);
+        } else {
+            o[0] = o[1] = o[2] = o[3] = o[4] = 0.0f;
+        }
+    }
+    for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
+}
+
+// ------------------------------------------------------------- the step ---
+template <bool TRAFFIC>
+__global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outputs out) {
+    const int e = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int N = p.N;
+    __shared__ EgoLDS el;
+    __shared__ ObsLDS ob;
+    __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
+    NpcLDS* nl = nullptr;
+    if constexpr (TRAFFIC) nl = &nl_storage;
+
+    // vector auto-reset of an env whose previous step ended
+    const bool do_reset = in.auto_reset && p.pending_reset[e];
+    const int prev_step = do_reset ? 0 : p.step_count[e];
+    const int prev_npcs = TRAFFIC ? (do_reset ? 0 : p.npc.count[e]) : 0;
+    if (do_reset) {
+        for (int i = lane; i < N; i += WAVE) {
+            const int g = e * N + i;
+            const int rid = p.ego.route[g];
+            p.ego.x[g] = p.rt.spawn[3 * rid];
+            p.ego.y[g] = p.rt.spawn[3 * rid + 1];
+            p.ego.v[g] = 0.0f;
+            p.ego.h[g] = p.rt.spawn[3 * rid + 2];
+            p.ego.sx[g] = p.ego.x[g]; p.ego.sy[g] = p.ego.y[g]; p.ego.sv[g] = 0.0f; p.ego.sh[g] = p.ego.h[g];
+            p.ego.acc[g] = 0.0f; p.ego.steer[g] = 0.0f; p.ego.prev_dist[g] = 0.0f;
+            p.ego.pa0[g] = 0.0f; p.ego.pa1[g] = 0.0f; p.ego.pidx[g] = 0;
+            p.ego.intent[g] = p.rt.intent[rid]; p.ego.alive[g] = 1;
+        }
+        __syncthreads();
+    }
+    const int step_no = prev_step + 1;  // res.step = ++step_count (:137)
+    if (lane == 0) p.step_count[e] = step_no;
+
+    int ncnt = 0;
+    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, lane);
+
+    // ---- ego physics + base reward (:151-163) + status (:165-290); lane = agent
+    for (int i = lane; i < N; i += WAVE) {
+        const int g = e * N + i;
+        const int rid = p.ego.route[g];
+        const float* path = p.rt.path + (size_t)rid * (2 * PATH_LEN);
+        Kin k{p.ego.x[g], p.ego.y[g], p.ego.v[g], p.ego.h[g], p.ego.acc[g], p.ego.steer[g]};
+        const bool alive = p.ego.alive[g] != 0;
+        float cH, sH;
+        float rew = 0.0f;
+        uint8_t done = 0, status = ST_ALIVE;
+        int pidx = p.ego.pidx[g];
+        if (alive) {
+            const float thr = in.actions[2 * g], st = in.actions[2 * g + 1];
+            car_update(k, thr, st, in.dt, &cH, &sH);
+            // update_path_index (serial per lane; 50 points)
+            {
+                int start_i = pidx < 0 ? 0 : pidx;
+                int end_i = start_i + 50;
+                if (end_i > PATH_LEN) end_i = PATH_LEN;
+                float min_d = __builtin_inff();
+                int best = start_i;
+                for (int q = start_i; q < end_i; ++q) {
+                    const float dx = path[2 * q] - k.x;
+                    const float dy = path[2 * q + 1] - k.y;
+                    const float d = dx * dx + dy * dy;
+                    if (d < min_d) { min_d = d; best = q; }
+                }
+                pidx = best;
+            }
+            // compute_progress / compute_stuck / compute_smooth (:15-46)
+            const float gx = path[2 * (PATH_LEN - 1)], gy = path[2 * (PATH_LEN - 1) + 1];
+            const float cur = hypotf(k.x - gx, k.y - gy);
+            const float prev = p.ego.prev_dist[g];
+            float r_prog = 0.0f;
+            if (prev > 0.0f) {
+                const float progress = prev - cur;
+                const float normalized = (p.max_progress > 0.0f) ? (progress / p.max_progress) : 0.0f;
+                r_prog = p.k_prog * normalized;
+            }
+            p.ego.prev_dist[g] = cur;
+            const float speed_ms = (k.v * FPS) / SCALE;
+            const float r_stuck = (speed_ms < p.v_min) ? p.k_stuck : 0.0f;
+            const float an = k.acc / MAX_ACC;
+            const float sn = k.steer / MAX_STEERING_ANGLE;
+            const float d0 = an - p.ego.pa0[g];
+            const float d1 = sn - p.ego.pa1[g];
+            const float diff2 = d0 * d0 + d1 * d1;
+            const float r_smooth = p.k_sm * diff2;
+            p.ego.pa0[g] = an;
+            p.ego.pa1[g] = sn;
+            rew = r_prog + r_stuck + r_smooth;
+
+            // status: SUCCESS by the last path segment's axis
+            const float ex = path[2 * (PATH_LEN - 1)], ey = path[2 * (PATH_LEN - 1) + 1];
+            const float px = path[2 * (PATH_LEN - 2)], py = path[2 * (PATH_LEN - 2) + 1];
+            const float dxr = ex - px, dyr = ey - py;
+            bool succ;
+            if (fabs_f(dxr) > fabs_f(dyr)) succ = fabs_f(k.y - ey) < 15.0f && fabs_f(k.x - ex) < 40.0f;
+            else succ = fabs_f(k.x - ex) < 15.0f && fabs_f(k.y - ey) < 40.0f;
+            float ccx[4], ccy[4];
+            car_corners(k.x, k.y, cH, sH, ccx, ccy);
+            if (succ) {
+                done = 1; status = ST_SUCCESS;
+            } else {
+                const float M = 100.0f;
+                bool oos = false, off = false, line = false;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    oos |= ccx[q] < -M || ccx[q] > float(WIDTH) + M || ccy[q] < -M || ccy[q] > float(HEIGHT) + M;
+                if (oos) { done = 1; status = ST_CRASH_WALL; }
+                else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) off |= !is_on_road(ccx[q], ccy[q], p.rw);
+                    if (off) { done = 1; status = ST_CRASH_WALL; }
+                    else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) line |= hits_yellow_line(ccx[q], ccy[q], p.rw);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int q2 = (q + 1) & 3;
+                            const float mx = 0.5f * (ccx[q] + ccx[q2]);
+                            const float my = 0.5f * (ccy[q] + ccy[q2]);
+                            line |= is_line_px((int)mx, (int)my, p.line_stop);
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) line |= is_line_px((int)ccx[q], (int)ccy[q], p.line_stop);
+                        if (line) { done = 1; status = ST_CRASH_LINE; }
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { el.cx[i][q] = ccx[q]; el.cy[i][q] = ccy[q]; }
+        } else {
+            done = 1;
+            status = ST_DEAD;
+            sincosf(k.h, &sH, &cH);
+        }
+        el.x[i] = k.x; el.y[i] = k.y; el.v[i] = k.v; el.h[i] = k.h; el.c[i] = cH; el.s[i] = sH;
+        el.pidx[i] = pidx; el.intent[i] = p.ego.intent[g];
+        el.alive[i] = alive; el.done[i] = done; el.status[i] = status; el.rew[i] = rew;
+        el.col[i] = 0ull; el.colnpc[i] = 0;
+        // write back kinematics (respawn may overwrite below)
+        p.ego.x[g] = k.x; p.ego.y[g] = k.y; p.ego.v[g] = k.v; p.ego.h[g] = k.h;
+        p.ego.acc[g] = k.acc; p.ego.steer[g] = k.steer; p.ego.pidx[g] = pidx;
+    }
+    __syncthreads();
+
+    // ---- car-car SAT (:292-318): ego pairs (i<j) and ego x NPC, one pair per lane
+    for (int pbase = 0; pbase < N * N; pbase += WAVE) {
+        const int pi = pbase + lane;
+        if (pi < N * N) {
+            const int a = pi / N, b = pi % N;
+            if (a < b && el.alive[a] && el.alive[b] &&
+                sat_collide(el.cx[a], el.cy[a], el.c[a], el.s[a], el.cx[b], el.cy[b], el.c[b], el.s[b]))
+                atomicOr(&el.col[a], 1ull << b);
+        }
+    }
+    if constexpr (TRAFFIC) {
+        for (int pbase = 0; pbase < N * ncnt; pbase += WAVE) {
+            const int pi = pbase + lane;
+            if (pi < N * ncnt) {
+                const int a = pi / ncnt, b = pi % ncnt;
+                if (el.alive[a] && sat_collide(el.cx[a], el.cy[a], el.c[a], el.s[a], nl->cx[b], nl->cy[b], nl->c[b], nl->s[b]))
+                    el.colnpc[a] = 1;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- greedy resolution in (i, j) order, bonuses, team mix, respawn, flags (:292-370)
+    // lane 0 owns the order-dependent scan; masks are 64-bit (N <= 64)
+    if (lane == 0) {
+        unsigned long long donem = 0ull, crash = 0ull;
+        for (int i = 0; i < N; ++i) if (el.done[i] || !el.alive[i]) donem |= 1ull << i;
+        for (int i = 0; i < N; ++i) {
+            if ((donem >> i) & 1ull) continue;
+            const unsigned long long higher = (i == 63) ? 0ull : (~0ull << (i + 1));
+            const unsigned long long hits = el.col[i] & ~donem & higher;
+            if (hits) { donem |= hits | (1ull << i); crash |= hits | (1ull << i); }
+            if (TRAFFIC && el.colnpc[i]) { donem |= 1ull << i; crash |= 1ull << i; }
+        }
+        for (int i = 0; i < N; ++i)
+            if ((crash >> i) & 1ull) { el.done[i] = 1; el.status[i] = ST_CRASH_CAR; }
+    }
+    __syncthreads();
+    for (int i = lane; i < N; i += WAVE) {
+        if (el.done[i]) {
+            const uint8_t st = el.status[i];
+            if (st == ST_CRASH_CAR) el.rew[i] += p.k_cv;
+            else if (st == ST_CRASH_WALL || st == ST_CRASH_LINE) el.rew[i] += p.k_co;
+            else if (st == ST_SUCCESS) el.rew[i] += p.k_succ;
+        }
+    }
+    __syncthreads();
+    if (lane == 0) {
+        if (p.use_team && N > 0) {
+            float avg = 0.0f;
+            for (int i = 0; i < N; ++i) avg += el.rew[i];
+            avg /= float(N);
+            for (int i = 0; i < N; ++i) el.rew[i] = (1.0f - p.alpha) * el.rew[i] + p.alpha * avg;
+        }
+        bool terminated = false;
+        int alive_cnt = 0, succ_cnt = 0;
+        for (int i = 0; i < N; ++i) {
+            if (!el.alive[i]) continue;
+            ++alive_cnt;
+            if (el.done[i] && el.status[i] == ST_SUCCESS) ++succ_cnt;
+        }
+        if (p.respawn) {
+            if (succ_cnt > 0 && succ_cnt == alive_cnt) terminated = true;
+        } else {
+            for (int i = 0; i < N; ++i) if (el.done[i]) { terminated = true; break; }
+        }
+        const bool truncated = p.max_steps > 0 && step_no >= p.max_steps;
+        out.term[e] = terminated;
+        out.trunc[e] = truncated;
+        out.alive_cnt[e] = alive_cnt;
+        out.step[e] = step_no;
+        p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
+    }
+    __syncthreads();
+    // respawn crashed egos (:339-351); lane = agent
+    for (int i = lane; i < N; i += WAVE) {
+        const int g = e * N + i;
+        out.rew[g] = el.rew[i];
+        out.done[g] = el.done[i];
+        out.status[g] = el.status[i];
+        const uint8_t st = el.status[i];
+        if (p.respawn && el.alive[i] && el.done[i] && (st == ST_CRASH_CAR || st == ST_CRASH_WALL || st == ST_CRASH_LINE)) {
+            const float sx = p.ego.sx[g], sy = p.ego.sy[g], sv = p.ego.sv[g], sh = p.ego.sh[g];
+            p.ego.x[g] = sx; p.ego.y[g] = sy; p.ego.v[g] = sv; p.ego.h[g] = sh;
+            p.ego.pidx[g] = 0; p.ego.prev_dist[g] = 0.0f; p.ego.pa0[g] = 0.0f; p.ego.pa1[g] = 0.0f;
+            p.ego.acc[g] = 0.0f; p.ego.steer[g] = 0.0f;
+            float s, c;
+            sincosf(sh, &s, &c);
+            el.x[i] = sx; el.y[i] = sy; el.v[i] = sv; el.h[i] = sh; el.c[i] = c; el.s[i] = s; el.pidx[i] = 0;
+        }
+    }
+    __syncthreads();
+
+    // ---- LiDAR obstacle table (:374-388): every ego (alive or not), then NPCs
+    const int nob = N + ncnt;
+    for (int o = lane; o < nob; o += WAVE) {
+        float x, y, h, c, s;
+        if (o < N) { x = el.x[o]; y = el.y[o]; h = el.h[o]; c = el.c[o]; s = el.s[o]; }
+        else { const int k = o - N; x = nl->x[k]; y = nl->y[k]; h = nl->h[k]; c = nl->c[k]; s = nl->s[k]; }
+        const PxBox b = aabb_px(x, y, c, s);
+        ob.x0[o] = b.x0; ob.x1[o] = b.x1; ob.y0[o] = b.y0; ob.y1[o] = b.y1;
+        ob.px[o] = x; ob.py[o] = y; ob.ph[o] = h;
+    }
+    __syncthreads();
+
+    // ---- LiDAR march (Lidar::update, cpp/Lidar.cpp:16-90); lane = (agent, beam)
+    const int R = p.R;
+    const int total = N * R;
+    const float maxd = p.lidar_max, stp = p.lidar_step;
+    for (int w0 = 0; w0 < total; w0 += WAVE) {
+        const int w = w0 + lane;
+        if (w >= total) break;
+        const int a = w / R, b = w - a * R;
+        const int g = e * N + a;
+        float* row = out.obs + (size_t)g * p.D;
+        if (!el.alive[a]) {
+            if (b < p.lidar_slots) row[OBS_HEAD + b] = 0.0f;
+            continue;
+        }
+        const float cx = el.x[a], cy = el.y[a], ch = el.h[a];
+        float sn, cs;
+        sincosf(ch + p.rel_angles[b], &sn, &cs);
+        const float dx = cs, dy = -sn;
+        // candidate obstacles: not self, not state-identical to self, and the
+        // ray segment passes within 2 px of the box (march points are truncated
+        // by < 1 px, so this never drops a box the march could enter)
+        unsigned long long cand[2] = {0ull, 0ull};
+        for (int o = 0; o < nob; ++o) {
+            if (o == a) continue;
+            if (fabs_f(ob.px[o] - cx) < 1e-3f && fabs_f(ob.py[o] - cy) < 1e-3f && fabs_f(ob.ph[o] - ch) < 1e-3f) continue;
+            float t0 = 0.0f, t1 = maxd;
+            const float bx0 = (float)ob.x0[o] - 2.0f, bx1 = (float)ob.x1[o] + 2.0f;
+            const float by0 = (float)ob.y0[o] - 2.0f, by1 = (float)ob.y1[o] + 2.0f;
+            bool ok = true;
+            if (fabs_f(dx) < 1e-9f) ok = cx >= bx0 && cx <= bx1;
+            else {
+                const float inv = 1.0f / dx;
+                float ta = (bx0 - cx) * inv, tb = (bx1 - cx) * inv;
+                if (ta > tb) { const float tt = ta; ta = tb; tb = tt; }
+                t0 = ta > t0 ? ta : t0;
+                t1 = tb < t1 ? tb : t1;
+            }
+            if (ok) {
+                if (fabs_f(dy) < 1e-9f) ok = cy >= by0 && cy <= by1;
+                else {
+                    const float inv = 1.0f / dy;
+                    float ta = (by0 - cy) * inv, tb = (by1 - cy) * inv;
+                    if (ta > tb) { const float tt = ta; ta = tb; tb = tt; }
+                    t0 = ta > t0 ? ta : t0;
+                    t1 = tb < t1 ? tb : t1;
+                }
+            }
+            if (ok && t0 <= t1 + 1.0f) cand[o >> 6] |= 1ull << (o & 63);
+        }
+        float final_dist = maxd;
+        for (float dist = 0.0f; dist < maxd; dist += stp) {
+            const int px = (int)(cx + dx * dist);
+            const int py = (int)(cy + dy * dist);
+            if (px < 0 || px >= WIDTH || py < 0 || py >= HEIGHT) break;
+            if (dist > 0.0f) {
+                if (!is_on_road_px(px, py, p.irw)) { final_dist = dist; break; }
+                bool hit = false;
+#pragma unroll
+                for (int wd = 0; wd < 2; ++wd) {
+                    unsigned long long m = cand[wd];
+                    while (m) {
+                        const int o = (wd << 6) + __builtin_ctzll(m);
+                        m &= m - 1ull;
+                        if (px >= ob.x0[o] && px <= ob.x1[o] && py >= ob.y0[o] && py <= ob.y1[o]) { hit = true; break; }
+                    }
+                    if (hit) break;
+                }
+                if (hit) { final_dist = dist; break; }
+            }
+        }
+        if (b < p.lidar_slots) row[OBS_HEAD + b] = final_dist * p.lidar_inv;
+    }
+
+    // ---- observation head (:418-520); lane = agent
+    for (int i = lane; i < N; i += WAVE) {
+        const int g = e * N + i;
+        float* row = out.obs + (size_t)g * p.D;
+        if (!el.alive[i]) {
+            for (int c = 0; c < OBS_HEAD; ++c) row[c] = 0.0f;
+            for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
+            continue;
+        }
+        const float* path = p.rt.path + (size_t)p.ego.route[g] * (2 * PATH_LEN);
+        write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row);
+    }
+}
+
+// ------------------------------------------------- reset / re-observe ---
+// IntersectionEnv::reset + add_car_with_route (cpp/IntersectionEnv.cpp:66-131)
+// and the reset observation (LiDAR block = max_dist / max_dist).
+template <bool TRAFFIC>
+__global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask, Outputs out, int do_reset) {
+    const int e = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int N = p.N;
+    if (mask && !mask[e]) return;
+    __shared__ EgoLDS el;
+    __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
+    NpcLDS* nl = nullptr;
+    if constexpr (TRAFFIC) nl = &nl_storage;
+    for (int i = lane; i < N; i += WAVE) {
+        const int g = e * N + i;
+        if (do_reset) {
+            const int rid = p.ego.route[g];
+            p.ego.x[g] = p.rt.spawn[3 * rid];
+            p.ego.y[g] = p.rt.spawn[3 * rid + 1];
+            p.ego.v[g] = 0.0f;
+            p.ego.h[g] = p.rt.spawn[3 * rid + 2];
+            p.ego.sx[g] = p.ego.x[g]; p.ego.sy[g] = p.ego.y[g]; p.ego.sv[g] = 0.0f; p.ego.sh[g] = p.ego.h[g];
+            p.ego.acc[g] = 0.0f; p.ego.steer[g] = 0.0f; p.ego.prev_dist[g] = 0.0f;
+            p.ego.pa0[g] = 0.0f; p.ego.pa1[g] = 0.0f; p.ego.pidx[g] = 0;
+            p.ego.intent[g] = p.rt.intent[rid]; p.ego.alive[g] = 1;
+        }
+        el.x[i] = p.ego.x[g]; el.y[i] = p.ego.y[g]; el.v[i] = p.ego.v[g]; el.h[i] = p.ego.h[g];
+        el.alive[i] = p.ego.alive[g]; el.intent[i] = p.ego.intent[g]; el.pidx[i] = p.ego.pidx[g];
+    }
+    int ncnt = 0;
+    if (do_reset) {
+        if (lane == 0) {
+            p.step_count[e] = 0;
+            p.pending_reset[e] = 0;
+            if (TRAFFIC) p.npc.count[e] = 0;
+        }
+    } else if constexpr (TRAFFIC) {
+        ncnt = p.npc.count[e];
+        if (lane < ncnt) {
+            const int g = e * p.K + lane;
+            nl->x[lane] = p.npc.x[g]; nl->y[lane] = p.npc.y[g]; nl->v[lane] = p.npc.v[g]; nl->h[lane] = p.npc.h[g];
+            nl->intent[lane] = p.npc.intent[g]; nl->alive[lane] = p.npc.alive[g];
+        }
+    }
+    __syncthreads();
+    for (int i = lane; i < N; i += WAVE) {
+        const int g = e * N + i;
+        float* row = out.obs + (size_t)g * p.D;
+        if (!el.alive[i]) {
+            for (int c = 0; c < p.D; ++c) row[c] = 0.0f;
+            continue;
+        }
+        const float* path = p.rt.path + (size_t)p.ego.route[g] * (2 * PATH_LEN);
+        write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row);
+        for (int b = 0; b < p.lidar_slots; ++b) row[OBS_HEAD + b] = p.lidar_max * p.lidar_inv;
+    }
+}
+
+hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s) {
+    if (p.traffic) hipLaunchKernelGGL(k_step<true>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
+    else hipLaunchKernelGGL(k_step<false>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s) {
+    if (p.traffic) hipLaunchKernelGGL(k_reset<true>, dim3(p.E), dim3(WAVE), 0, s, p, env_mask, out, 1);
+    else hipLaunchKernelGGL(k_reset<false>, dim3(p.E), dim3(WAVE), 0, s, p, env_mask, out, 1);
+    return hipGetLastError();
+}
+
+hipError_t launch_observe_reset_lidar(const SimParams& p, const Outputs& out, hipStream_t s) {
+    if (p.traffic) hipLaunchKernelGGL(k_reset<true>, dim3(p.E), dim3(WAVE), 0, s, p, nullptr, out, 0);
+    else hipLaunchKernelGGL(k_reset<false>, dim3(p.E), dim3(WAVE), 0, s, p, nullptr, out, 0);
+    return hipGetLastError();
+}
+
+}  // namespace mev

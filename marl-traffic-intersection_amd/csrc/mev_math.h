@@ -63,9 +63,6 @@ struct SinCosTab {
     double c0, c1, s1, c2, s2, c3, s3, c4;
 };
 
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
 static constexpr SinCosTab kSinCos[2] = {
     {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
      0x1p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
@@ -75,9 +72,6 @@ static constexpr SinCosTab kSinCos[2] = {
      0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13, -0x1.99343027bf8c3p-16},
 };
 
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
 static constexpr uint32_t kInvPio4[24] = {
     0xa2u,       0xa2f9u,     0xa2f983u,   0xa2f9836eu, 0xf9836e4eu, 0x836e4e44u,
     0x6e4e4415u, 0x4e441529u, 0x441529fcu, 0x1529fc27u, 0x29fc2757u, 0xfc2757d1u,

@@ -225,6 +225,24 @@ int rh_route_path(void* p, int route, float* out) {
     return int(path.size());
 }
 
+// Reference geometry probes (cpp/RoadGeometry.h:19-67, cpp/LineMask.h:15-18)
+// evaluated on the 750x750 integer pixel grid: out[y*750+x] bit0 = is_on_road,
+// bit1 = hits_yellow_line, bit2 = LineMask::is_line.
+void rh_geometry_grid(int num_lanes, uint8_t* out) {
+    RoadGeometry geom(num_lanes);
+    LineMask lm(num_lanes);
+    for (int y = 0; y < HEIGHT; ++y)
+        for (int x = 0; x < WIDTH; ++x) {
+            uint8_t v = 0;
+            if (geom.is_on_road(float(x), float(y))) v |= 1;
+            if (geom.hits_yellow_line(float(x), float(y))) v |= 2;
+            if (lm.is_line(x, y)) v |= 4;
+            out[y * WIDTH + x] = v;
+        }
+}
+int rh_is_on_road(int num_lanes, float x, float y) { return RoadGeometry(num_lanes).is_on_road(x, y) ? 1 : 0; }
+int rh_hits_yellow_line(int num_lanes, float x, float y) { return RoadGeometry(num_lanes).hits_yellow_line(x, y) ? 1 : 0; }
+
 // Raw LiDAR distances of every ego (n x rays).
 void rh_get_lidar(void* p, float* out) {
     auto* h = static_cast<Harness*>(p);

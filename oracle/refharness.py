@@ -54,6 +54,9 @@ def lib():
         L.rh_add_npc.argtypes = [vp, i, fp, ip]
         L.rh_get_lidar.argtypes = [vp, fp]
         L.rh_route_path.argtypes = [vp, i, fp]
+        L.rh_geometry_grid.argtypes = [i, ctypes.POINTER(ctypes.c_uint8)]
+        L.rh_is_on_road.argtypes = [i, f, f]
+        L.rh_hits_yellow_line.argtypes = [i, f, f]
         L.rh_get_obs.argtypes = [vp, fp]
         L.rh_step.argtypes = [vp, i, fp, fp, f, fp, fp, ip, ip, ip, ip]
         L.rh_bench.restype = ctypes.c_double
@@ -163,6 +166,12 @@ class RefEnv:
         return dict(obs=obs[:n], rew=rew[:n], done=done[:n], status=status[:n],
                     terminated=int(flags[0]), truncated=int(flags[1]), agents_alive=int(flags[2]),
                     step=int(flags[3]), spawned=int(spawned[0]))
+
+
+def geometry_grid(num_lanes: int) -> np.ndarray:
+    out = np.zeros((750, 750), np.uint8)
+    lib().rh_geometry_grid(int(num_lanes), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return out
 
 
 def bench(num_agents: int, rays: int, use_team: bool, traffic: bool, density: float,

@@ -186,7 +186,35 @@ def inject_npcs(kcount: int):
     return _inj
 
 
+def gen_static(lanes: int):
+    """Route table and geometry of the reference for `lanes` lanes: every
+    (start point, end point) pair's 160-point path, intent and spawn heading
+    (cpp/RouteGen.cpp:7-205, cpp/IntersectionEnv.cpp:78-131), plus the road /
+    yellow-line / line-mask predicates on the integer pixel grid and on random
+    real-valued points."""
+    nl = 4 * lanes
+    names = [f"IN_{k}" for k in range(1, nl + 1)] + [f"OUT_{k}" for k in range(1, nl + 1)]
+    pairs = [(s, e) for s in names for e in names]
+    env = R.RefEnv(num_lanes=lanes, traffic=True, density=0.0, routes=pairs)
+    env.reset()
+    paths = np.stack([env.route_path(k) for k in range(len(pairs))])
+    for k, (s_, e_) in enumerate(pairs):
+        assert env.add_car(s_, e_, tag=k) == 0
+    ef, ei = env.cars(0)
+    grid = R.geometry_grid(lanes)
+    rng = np.random.default_rng(lanes)
+    pts = np.concatenate([rng.uniform(-120, 870, (30000, 2)), rng.uniform(150, 600, (30000, 2))]).astype(np.float32)
+    road = np.array([R.lib().rh_is_on_road(lanes, float(x), float(y)) for x, y in pts], np.uint8)
+    yel = np.array([R.lib().rh_hits_yellow_line(lanes, float(x), float(y)) for x, y in pts], np.uint8)
+    env.close()
+    np.savez_compressed(os.path.join(OUT, f"static_lanes{lanes}.npz"), names=np.array(names), paths=paths,
+                        intent=ei[:, 1], spawn=ef[:, [0, 1, 3]], grid=grid, pts=pts, road=road, yellow=yel)
+    print(f"static_lanes{lanes}: {len(pairs)} routes, grid on-road px={int((grid & 1).sum())}")
+
+
 def main():
+    gen_static(3)
+    gen_static(2)
     # Config 1 shape: 1 env x 1 agent, 16 beams.
     run("cfg1_r16_random", n_agents=1, rays=16, steps=400, act="random", seed=0)
     run("cfg1_r16_policy", n_agents=1, rays=16, steps=300, act="policy", seed=1)

@@ -1,0 +1,184 @@
+"""Replay a golden scenario (tests/golden/*.npz, produced from the REAL reference
+by tests/golden/gen_golden.py) through the device path and compare every
+output bit-for-bit.  Test infrastructure; no /root/reference access."""
+from __future__ import annotations
+
+import glob
+import json
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+EGO_F = ["x", "y", "v", "heading", "acc", "steering", "spawn_x", "spawn_y", "spawn_v", "spawn_heading",
+         "prev_dist", "prev_a0", "prev_a1"]
+NPC_F = ["npc_x", "npc_y", "npc_v", "npc_heading", "npc_acc", "npc_steering"]
+
+
+def scenario_names(prefix: str = "") -> List[str]:
+    out = []
+    for p in sorted(glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))):
+        n = os.path.basename(p)[:-4]
+        if n.startswith("static_"):
+            continue
+        if n.startswith(prefix):
+            out.append(n)
+    return out
+
+
+def load(name: str):
+    z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    d["meta"] = json.loads(str(d["meta"]))
+    return d
+
+
+def point_index(name: str, lanes: int) -> int:
+    kind, k = name.split("_")
+    k = int(k)
+    return k - 1 if kind == "IN" else 4 * lanes + k - 1
+
+
+def bits_equal(a, b) -> bool:
+    a = np.ascontiguousarray(a)
+    b = np.ascontiguousarray(b)
+    if a.shape != b.shape:
+        return False
+    if a.dtype == np.float32:
+        return np.array_equal(a.view(np.uint32), b.astype(np.float32).view(np.uint32))
+    return np.array_equal(a, b)
+
+
+@dataclass
+class Report:
+    name: str
+    steps: int = 0
+    mismatches: List[str] = field(default_factory=list)
+    max_obs_diff: float = 0.0
+
+    @property
+    def ok(self) -> bool:
+        return not self.mismatches
+
+    def add(self, msg: str):
+        if len(self.mismatches) < 20:
+            self.mismatches.append(msg)
+
+
+def make_handle(mod, meta, num_envs: int, device: int = 0):
+    R = int(meta["rays"])
+    return mod.Handle(num_envs=num_envs, num_agents=int(meta["n_agents"]), num_lanes=int(meta["num_lanes"]),
+                      lidar_rays=R, obs_dim=127 if R <= 96 else 31 + R, traffic_flow=int(meta["traffic"]),
+                      traffic_density=float(meta["density"]), use_team_reward=int(meta["use_team"]),
+                      respawn_enabled=int(meta["respawn"]), max_steps=int(meta["max_steps"]),
+                      reward=meta["reward"], max_npcs=32, device=device)
+
+
+def replay(mod, names, steps: Optional[int] = None, stop_at_first=True) -> List[Report]:
+    """Run the scenarios `names` (identical configs) as envs 0..B-1 of one handle."""
+    if isinstance(names, str):
+        names = [names]
+    data = [load(n) for n in names]
+    meta = data[0]["meta"]
+    for d in data[1:]:
+        for k in ("num_lanes", "n_agents", "rays", "use_team", "respawn", "max_steps", "traffic", "density", "reward",
+                  "dt", "traffic_routes"):
+            assert d["meta"][k] == meta[k], f"scenario configs differ in {k}"
+    B = len(data)
+    L = int(meta["num_lanes"])
+    h = make_handle(mod, meta, B)
+    troutes = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["traffic_routes"]]
+    h.set_traffic_routes(troutes)
+    n = int(meta["n_agents"])
+    ego_routes = np.zeros((B, n), np.int32)
+    for b, d in enumerate(data):
+        ego_routes[b] = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in d["meta"]["ego_routes"]]
+    h.set_ego_routes(ego_routes)
+    # initial state
+    st = h.get_state()
+    for b, d in enumerate(data):
+        f, i = d["init_ego_f"], d["init_ego_i"]
+        for j, key in enumerate(EGO_F):
+            st[key][b] = f[:, j]
+        st["alive"][b] = i[:, 0]
+        st["intention"][b] = i[:, 1]
+        st["path_index"][b] = i[:, 2]
+        st["route"][b] = ego_routes[b]
+        k = len(d["init_npc_f"])
+        st["npc_count"][b] = k
+        if k:
+            nf, ni = d["init_npc_f"], d["init_npc_i"]
+            for j, key in enumerate(NPC_F):
+                st[key][b, :k] = nf[:, j]
+            st["npc_alive"][b, :k] = ni[:, 0]
+            st["npc_intention"][b, :k] = ni[:, 1]
+            st["npc_path_index"][b, :k] = ni[:, 2]
+            st["npc_route"][b, :k] = [troutes[r] for r in ni[:, 3]]
+        st["step_count"][b] = 0
+    h.set_state(st)
+    reports = [Report(nm) for nm in names]
+    obs0 = h.observations()
+    for b, d in enumerate(data):
+        if not bits_equal(obs0[b, :, :127], d["init_obs"]):
+            reports[b].add("initial obs differ")
+    T = min(int(meta["steps"]), steps or 10 ** 9)
+    out = h.alloc_outputs()
+    for t in range(T):
+        acts = np.stack([d["actions"][t] for d in data])
+        spawn = None
+        if meta["traffic"]:
+            spawn = np.array([d["spawned"][t] for d in data], np.int32)
+        h.step(acts, float(meta["dt"]), out=out, spawn_route=spawn)
+        st = h.get_state()
+        for b, d in enumerate(data):
+            rep = reports[b]
+            if not rep.ok and stop_at_first:
+                continue
+            rep.steps = t + 1
+            g_obs = d["obs"][t]
+            my = out["obs"][b]
+            diff = float(np.max(np.abs(my[:, :127] - g_obs))) if my.size else 0.0
+            rep.max_obs_diff = max(rep.max_obs_diff, diff)
+            if not bits_equal(my[:, :127], g_obs):
+                bad = np.argwhere(my[:, :127].view(np.uint32) != g_obs.view(np.uint32))
+                rep.add(f"step {t + 1}: obs differ at {bad[:4].tolist()} (max |d|={diff:.3g})")
+            if "lidar" in d and meta["rays"] > 96:
+                if not bits_equal(my[:, 31:], d["lidar"][t] * np.float32(1.0 / 250.0)):
+                    rep.add(f"step {t + 1}: full lidar differs")
+            if not bits_equal(out["reward"][b], d["rew"][t]):
+                rep.add(f"step {t + 1}: reward {out['reward'][b].tolist()} vs {d['rew'][t].tolist()}")
+            if not bits_equal(out["done"][b], d["done"][t]):
+                rep.add(f"step {t + 1}: done {out['done'][b].tolist()} vs {d['done'][t].tolist()}")
+            if not bits_equal(out["status"][b], d["status"][t]):
+                rep.add(f"step {t + 1}: status {out['status'][b].tolist()} vs {d['status'][t].tolist()}")
+            fl = d["flags"][t]
+            got = [int(out["terminated"][b]), int(out["truncated"][b]), int(out["agents_alive"][b]),
+                   int(out["step"][b])]
+            if got != [int(x) for x in fl]:
+                rep.add(f"step {t + 1}: flags {got} vs {fl.tolist()}")
+            ef, ei = d["ego_f"][t], d["ego_i"][t]
+            for j, key in enumerate(EGO_F):
+                if not bits_equal(st[key][b], ef[:, j]):
+                    rep.add(f"step {t + 1}: ego {key} {st[key][b][:4]} vs {ef[:4, j]}")
+            if not bits_equal(st["alive"][b], ei[:, 0].astype(np.uint8)) or \
+                    not bits_equal(st["intention"][b], ei[:, 1]) or not bits_equal(st["path_index"][b], ei[:, 2]):
+                rep.add(f"step {t + 1}: ego alive/intention/path_index differ")
+            kc = int(d["npc_count"][t])
+            if int(st["npc_count"][b]) != kc:
+                rep.add(f"step {t + 1}: npc count {int(st['npc_count'][b])} vs {kc}")
+            elif kc:
+                nf, ni = d["npc_f"][t, :kc], d["npc_i"][t, :kc]
+                for j, key in enumerate(NPC_F):
+                    if not bits_equal(st[key][b, :kc], nf[:, j]):
+                        rep.add(f"step {t + 1}: {key} {st[key][b, :kc]} vs {nf[:, j]}")
+                if not bits_equal(st["npc_path_index"][b, :kc], ni[:, 2]):
+                    rep.add(f"step {t + 1}: npc path_index differ")
+                if not bits_equal(st["npc_route"][b, :kc], np.array([troutes[r] for r in ni[:, 3]], np.int32)):
+                    rep.add(f"step {t + 1}: npc route differ")
+        if stop_at_first and all(not r.ok for r in reports):
+            break
+    h.close()
+    return reports

@@ -1,0 +1,33 @@
+"""Bit-exact parity of the gfx950 step against golden vectors from the REAL
+reference simulator (tests/golden/*.npz, see tests/golden/gen_golden.py).
+Every output is compared with exact bit equality — stricter than the 1e-5
+float tolerance BASELINE.json asks for (obs, rewards, ego/NPC state) and the
+bit-exact requirement on crash/success flags."""
+import pytest
+
+import golden_replay as G
+
+pytestmark = pytest.mark.gpu
+
+SINGLE = [n for n in G.scenario_names() if not n.startswith("inject_egos")]
+
+
+@pytest.mark.parametrize("name", SINGLE)
+def test_golden_scenario(mev, name):
+    (rep,) = G.replay(mev, name)
+    assert rep.ok, f"{name}: {rep.mismatches[:5]} (steps checked {rep.steps})"
+
+
+def test_injected_states_batched(mev):
+    # six different injected scenarios as six envs of ONE handle
+    reps = G.replay(mev, G.scenario_names("inject_egos"))
+    bad = [(r.name, r.mismatches[:3]) for r in reps if not r.ok]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["cfg3_team_policy", "traffic_d20"])
+def test_same_scenario_replicated_envs(mev, name):
+    # the same scenario in 37 envs of one handle: every env must match the reference
+    reps = G.replay(mev, [name] * 37)
+    bad = [i for i, r in enumerate(reps) if not r.ok]
+    assert not bad, reps[bad[0]].mismatches[:5]
