@@ -120,8 +120,11 @@ int mev_create(const mev_config* cfg, mev_handle** out);
 int mev_destroy(mev_handle* h);
 int mev_get_config(const mev_handle* h, mev_config* cfg);
 int mev_obs_dim(const mev_handle* h, int32_t* obs_dim);
-/* hipStream_t to order this handle's work on (NULL = the handle's own stream). */
+/* A handle starts on its own non-blocking stream.  mev_set_stream orders all
+ * later work on `stream` (a hipStream_t; NULL = the legacy default stream),
+ * e.g. torch.cuda.current_stream().cuda_stream; mev_use_own_stream reverts. */
 int mev_set_stream(mev_handle* h, void* stream);
+int mev_use_own_stream(mev_handle* h);
 int mev_sync(mev_handle* h);
 
 /* Lane points / routes (reference cpp/RouteGen.cpp). */
@@ -161,6 +164,9 @@ int mev_device_outputs(mev_handle* h, float** obs, float** reward, uint8_t** don
 
 /* Diagnostics: spawns dropped because max_npcs was full (cumulative). */
 int mev_npc_overflow(mev_handle* h, int64_t* count);
+/* Diagnostics: per-env phase timestamps [E][8] of the last step; all zero
+ * unless the library was built with -DMEV_STAMPS (tools/phase_profile.py). */
+int mev_debug_stamps(mev_handle* h, uint64_t* out);
 
 #ifdef __cplusplus
 }

@@ -35,19 +35,28 @@ def _inputs():
     return [f for f in files if os.path.isfile(f)]
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(LIB_PATH):
+VARIANTS = {"": [], "stamps": ["-DMEV_STAMPS"]}
+
+
+def lib_path(variant: str = "") -> str:
+    return LIB_PATH if not variant else os.path.join(PKG_DIR, f"libmarlenv_hip_{variant}.so")
+
+
+def up_to_date(variant: str = "") -> bool:
+    path = lib_path(variant)
+    if not os.path.exists(path):
         return False
-    t = os.path.getmtime(LIB_PATH)
+    t = os.path.getmtime(path)
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return LIB_PATH
-    tmp = LIB_PATH + ".tmp"
+def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
+    path = lib_path(variant)
+    if not force and up_to_date(variant):
+        return path
+    tmp = path + ".tmp"
     cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC]
+           "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC] + VARIANTS[variant]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     cmd += ["-o", tmp]
     if verbose:
@@ -55,9 +64,13 @@ def build(force: bool = False, verbose: bool = False) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stderr[-6000:]}")
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, path)
+    return path
 
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    if "--all" in sys.argv:
+        for v in VARIANTS:
+            if v:
+                print(build(force="--force" in sys.argv, verbose=True, variant=v))

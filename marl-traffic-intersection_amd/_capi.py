@@ -30,7 +30,7 @@ EXPORTED = (
     "mev_get_config", "mev_obs_dim", "mev_set_stream", "mev_sync", "mev_num_points", "mev_point_xy",
     "mev_route_id", "mev_route_info", "mev_path_len", "mev_set_ego_routes", "mev_set_traffic_routes",
     "mev_default_traffic_routes", "mev_reset", "mev_step", "mev_get_outputs", "mev_get_state", "mev_set_state",
-    "mev_device_outputs", "mev_npc_overflow",
+    "mev_device_outputs", "mev_npc_overflow", "mev_use_own_stream", "mev_debug_stamps",
 )
 
 
@@ -75,25 +75,27 @@ class MevState(ctypes.Structure):
     _fields_ = [(name, _vp) for name, _, _ in STATE_FIELDS]
 
 
-_lib = None
+_libs = {}
+VARIANT = os.environ.get("MEV_LIB_VARIANT", "")  # "" = product library; "stamps" = diagnostic build
 
 
 def lib_available() -> bool:
     return os.path.exists(LIB_PATH)
 
 
-def load_library():
+def load_library(variant: str = None):
     """Load libmarlenv_hip.so (building it first when hipcc is present)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not _build.up_to_date():
+    variant = VARIANT if variant is None else variant
+    if variant in _libs:
+        return _libs[variant]
+    path = _build.lib_path(variant)
+    if not _build.up_to_date(variant):
         try:
-            _build.build()
+            _build.build(variant=variant)
         except Exception as exc:  # no hipcc on this machine: use a prebuilt library if it is there
-            if not os.path.exists(LIB_PATH):
-                raise RuntimeError(f"libmarlenv_hip.so is missing and could not be built: {exc}") from exc
-    L = ctypes.CDLL(LIB_PATH)
+            if not os.path.exists(path):
+                raise RuntimeError(f"{os.path.basename(path)} is missing and could not be built: {exc}") from exc
+    L = ctypes.CDLL(path)
     i32p = ctypes.POINTER(ctypes.c_int32)
     f32p = ctypes.POINTER(ctypes.c_float)
     L.mev_last_error.restype = ctypes.c_char_p
@@ -119,7 +121,9 @@ def load_library():
     L.mev_device_outputs.argtypes = [_vp] + [ctypes.POINTER(_vp)] * 6
     L.mev_npc_overflow.argtypes = [_vp, ctypes.POINTER(ctypes.c_int64)]
     L.mev_device_count.argtypes = [i32p]
-    _lib = L
+    L.mev_use_own_stream.argtypes = [_vp]
+    L.mev_debug_stamps.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64)]
+    _libs[variant] = L
     return L
 
 
@@ -133,7 +137,7 @@ class IndexRangeError(MevError, IndexError):
 
 def _check(rc: int):
     if rc != 0:
-        msg = load_library().mev_last_error().decode(errors="replace")
+        msg = load_library().mev_last_error().decode(errors="replace")  # thread-local in the product lib
         if rc == -4:
             raise IndexRangeError(msg)
         raise MevError(f"libmarlenv_hip error {rc}: {msg}")
@@ -207,7 +211,16 @@ class Handle:
         return self._h
 
     def set_stream(self, stream_ptr: Optional[int]):
-        _check(self._lib.mev_set_stream(self._h, stream_ptr))
+        """Order this handle's work on a hipStream_t (int handle; 0/None = legacy default stream)."""
+        _check(self._lib.mev_set_stream(self._h, stream_ptr or None))
+
+    def use_own_stream(self):
+        _check(self._lib.mev_use_own_stream(self._h))
+
+    def debug_stamps(self) -> np.ndarray:
+        out = np.zeros((self.E, 8), np.uint64)
+        _check(self._lib.mev_debug_stamps(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+        return out
 
     def sync(self):
         _check(self._lib.mev_sync(self._h))

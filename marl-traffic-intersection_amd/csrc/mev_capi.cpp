@@ -167,6 +167,14 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
         }
     }
     h->h_traffic = mev::default_traffic_routes(c.num_lanes);
+    // LiDAR probe distances exactly as Lidar.cpp:33 accumulates them
+    std::vector<float> dists;
+    bool dist_mul_exact = true;
+    for (float dist = 0.0f; dist < c.lidar_max_dist; dist += c.lidar_step) {
+        if (dist != float(dists.size()) * c.lidar_step) dist_mul_exact = false;
+        dists.push_back(dist);
+        if (dists.size() > (1u << 20)) return fail(MEV_E_INVALID, "lidar_max_dist / lidar_step too large");
+    }
 
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
@@ -185,7 +193,8 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&p.ego.pidx, EN); A(&p.ego.route, EN); A(&p.ego.intent, EN); A(&p.ego.alive, EN);
     A(&p.npc.x, EK); A(&p.npc.y, EK); A(&p.npc.v, EK); A(&p.npc.h, EK); A(&p.npc.acc, EK); A(&p.npc.steer, EK);
     A(&p.npc.pidx, EK); A(&p.npc.route, EK); A(&p.npc.intent, EK); A(&p.npc.alive, EK); A(&p.npc.count, size_t(E));
-    A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 1);
+    A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 1); A(&p.debug, size_t(E) * 8);
+    A(&p.ob_box, size_t(E) * size_t(N + c.max_npcs)); A(&p.ob_cand, EN * 2);
     // outputs
     A(&h->internal.obs, EN * size_t(D)); A(&h->internal.rew, EN); A(&h->internal.done, EN); A(&h->internal.status, EN);
     A(&h->internal.term, size_t(E)); A(&h->internal.trunc, size_t(E)); A(&h->internal.alive_cnt, size_t(E));
@@ -194,6 +203,8 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&h->d_actions, EN * 2); A(&h->d_spawn, size_t(E)); A(&h->d_mask, size_t(E));
     A(&h->d_paths, h->h_paths.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
     A(&h->d_rel, rel.size()); A(&h->d_traffic, size_t(h->P) * size_t(h->P));
+    float* d_dist = nullptr;
+    if (!dist_mul_exact) A(&d_dist, dists.size());
     if (err != hipSuccess) {
         std::string m = hipGetErrorString(err);
         delete h;
@@ -205,6 +216,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_spawn_tab, h->h_spawn.data(), h->h_spawn.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_intent, h->h_intent.data(), h->h_intent.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_rel, rel.data(), rel.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess && d_dist) err = hipMemcpyAsync(d_dist, dists.data(), dists.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_traffic, h->h_traffic.data(), h->h_traffic.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
     // default ego routes: reference env.py:138-145 (mapping routes, cyclic)
     std::vector<int32_t> ego(EN);
@@ -244,6 +256,9 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     p.lidar_max = c.lidar_max_dist;
     p.lidar_step = c.lidar_step;
     p.lidar_inv = (c.lidar_max_dist > 0.0f) ? (1.0f / c.lidar_max_dist) : 0.0f;  // Lidar.cpp:94
+    p.lidar_steps = int(dists.size());
+    p.ob_stride = N + c.max_npcs;
+    p.dist_tab = d_dist;
     p.spawn_prob = 0.0f;
     p.seed = c.seed;
     p.rt.path = h->d_paths;
@@ -281,7 +296,25 @@ int mev_obs_dim(const mev_handle* h, int32_t* d) {
 
 int mev_set_stream(mev_handle* h, void* stream) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
-    h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // order the switch after outstanding work
+    h->stream = static_cast<hipStream_t>(stream);  // NULL = the legacy default stream
+    return MEV_OK;
+}
+
+int mev_use_own_stream(mev_handle* h) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->stream = h->own_stream;
+    return MEV_OK;
+}
+
+int mev_debug_stamps(mev_handle* h, uint64_t* out) {
+    if (!h || !out) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipMemcpyAsync(out, h->sp.debug, size_t(h->cfg.num_envs) * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
     return MEV_OK;
 }
 

@@ -61,6 +61,8 @@ struct SimParams {
     float k_prog, v_min, k_stuck, k_cv, k_co, k_succ, k_sm, alpha;
     float max_progress;      // hypot(750, 750)
     float lidar_max, lidar_step, lidar_inv;
+    int32_t lidar_steps;      // S = number of march probes (dist < max_dist)
+    const float* dist_tab;    // [S] accumulated probe distances, or null when dist_k == k*step exactly
     float spawn_prob;        // 1 - expf(-density * dt) computed on host with glibc
     uint64_t seed;
     EgoSoA ego;
@@ -72,6 +74,11 @@ struct SimParams {
     int32_t* step_count;      // [E]
     uint8_t* pending_reset;   // [E]
     unsigned long long* overflow;  // [1]
+    unsigned long long* debug;     // diagnostic builds only (MEV_STAMPS): [E*8]
+    // LiDAR hand-off k_cars -> k_lidar (L2-resident, rewritten every step)
+    int4* ob_box;                  // [E][ob_stride] integer pixel AABB (x0, x1, y0, y1)
+    unsigned long long* ob_cand;   // [E*N][2] candidate obstacle bits per agent
+    int32_t ob_stride;             // N + max_npcs
 };
 
 struct StepInputs {

@@ -19,6 +19,18 @@
 namespace mev {
 
 constexpr int WAVE = 64;
+
+// Diagnostic build only (-DMEV_STAMPS): per-env phase timestamps (s_memtime)
+// into SimParams::debug[e*8 + k]; never compiled into the product library.
+#ifdef MEV_STAMPS
+#define STAMP(k)                                                         \
+    do {                                                                 \
+        __syncthreads();                                                 \
+        if (threadIdx.x == 0) p.debug[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
 constexpr int MAXN = 64;
 constexpr int MAXK = 64;
 constexpr int MAXOB = MAXN + MAXK;
@@ -70,6 +82,13 @@ __device__ inline void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint64_t se
 
 __device__ inline float u01(uint32_t r) { return (float)(r >> 8) * 0x1p-24f; }
 
+// dist of march probe k: the reference accumulates `dist += step_size` in
+// float (Lidar.cpp:33); when that sum equals k*step exactly (checked on the
+// host, e.g. step 4) we multiply, otherwise read the host-accumulated table.
+__device__ inline float march_dist(const SimParams& p, int k) {
+    return p.dist_tab ? p.dist_tab[k] : (float)k * p.lidar_step;
+}
+
 // Car::update_path_index (cpp/Car.cpp:47-74): argmin of squared distance over
 // path[idx, idx+50) — one window point per lane, strict '<' => first minimum wins.
 __device__ inline int path_index_update(const float* path, int idx, float x, float y, int lane) {
@@ -110,6 +129,7 @@ struct NpcLDS {
 struct ObsLDS {
     int x0[MAXOB], x1[MAXOB], y0[MAXOB], y1[MAXOB];
     float px[MAXOB], py[MAXOB], ph[MAXOB];
+    unsigned long long cand[MAXN][2];  // per agent: boxes its beams can reach (self/twins excluded)
 };
 
 // --------------------------------------------------- NPC traffic phase ---
@@ -482,9 +502,13 @@ __device__ void write_obs_head(const SimParams& p, int i, const EgoLDS& el, cons
 
 // ------------------------------------------------------------- the step ---
 template <bool TRAFFIC>
-__global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outputs out) {
+__global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outputs out) {
+    // one wave per env: the order-dependent per-env logic (NPCs, kinematics,
+    // status, collisions, respawn, observation head); the LiDAR block of the
+    // observation is filled by k_lidar right after.
     const int e = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int nthr = blockDim.x;
     const int N = p.N;
     __shared__ EgoLDS el;
     __shared__ ObsLDS ob;
@@ -497,7 +521,7 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
     const int prev_step = do_reset ? 0 : p.step_count[e];
     const int prev_npcs = TRAFFIC ? (do_reset ? 0 : p.npc.count[e]) : 0;
     if (do_reset) {
-        for (int i = lane; i < N; i += WAVE) {
+        for (int i = tid; i < N; i += nthr) {
             const int g = e * N + i;
             const int rid = p.ego.route[g];
             p.ego.x[g] = p.rt.spawn[3 * rid];
@@ -512,13 +536,15 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
         __syncthreads();
     }
     const int step_no = prev_step + 1;  // res.step = ++step_count (:137)
-    if (lane == 0) p.step_count[e] = step_no;
+    if (tid == 0) p.step_count[e] = step_no;
 
+    STAMP(0);
     int ncnt = 0;
-    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, lane);
+    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid);
+    STAMP(1);
 
     // ---- ego physics + base reward (:151-163) + status (:165-290); lane = agent
-    for (int i = lane; i < N; i += WAVE) {
+    for (int i = tid; i < N; i += nthr) {
         const int g = e * N + i;
         const int rid = p.ego.route[g];
         const float* path = p.rt.path + (size_t)rid * (2 * PATH_LEN);
@@ -531,18 +557,30 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
         if (alive) {
             const float thr = in.actions[2 * g], st = in.actions[2 * g + 1];
             car_update(k, thr, st, in.dt, &cH, &sH);
-            // update_path_index (serial per lane; 50 points)
+            // update_path_index (Car.cpp:47-74), in order over the 50-point
+            // window; loads issued 10 at a time so they overlap
             {
-                int start_i = pidx < 0 ? 0 : pidx;
-                int end_i = start_i + 50;
-                if (end_i > PATH_LEN) end_i = PATH_LEN;
+                const int start_i = pidx < 0 ? 0 : pidx;
+                const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
+                const float2* P = reinterpret_cast<const float2*>(path);
                 float min_d = __builtin_inff();
                 int best = start_i;
-                for (int q = start_i; q < end_i; ++q) {
-                    const float dx = path[2 * q] - k.x;
-                    const float dy = path[2 * q + 1] - k.y;
-                    const float d = dx * dx + dy * dy;
-                    if (d < min_d) { min_d = d; best = q; }
+                for (int base = 0; base < 50; base += 10) {
+                    float2 pt[10];
+#pragma unroll
+                    for (int j = 0; j < 10; ++j) {
+                        int q = start_i + base + j;
+                        pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 10; ++j) {
+                        if (base + j < cnt) {
+                            const float dx = pt[j].x - k.x;
+                            const float dy = pt[j].y - k.y;
+                            const float d = dx * dx + dy * dy;
+                            if (d < min_d) { min_d = d; best = start_i + base + j; }
+                        }
+                    }
                 }
                 pidx = best;
             }
@@ -624,9 +662,10 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
     }
     __syncthreads();
 
+    STAMP(2);
     // ---- car-car SAT (:292-318): ego pairs (i<j) and ego x NPC, one pair per lane
-    for (int pbase = 0; pbase < N * N; pbase += WAVE) {
-        const int pi = pbase + lane;
+    for (int pbase = 0; pbase < N * N; pbase += nthr) {
+        const int pi = pbase + tid;
         if (pi < N * N) {
             const int a = pi / N, b = pi % N;
             if (a < b && el.alive[a] && el.alive[b] &&
@@ -635,8 +674,8 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
         }
     }
     if constexpr (TRAFFIC) {
-        for (int pbase = 0; pbase < N * ncnt; pbase += WAVE) {
-            const int pi = pbase + lane;
+        for (int pbase = 0; pbase < N * ncnt; pbase += nthr) {
+            const int pi = pbase + tid;
             if (pi < N * ncnt) {
                 const int a = pi / ncnt, b = pi % ncnt;
                 if (el.alive[a] && sat_collide(el.cx[a], el.cy[a], el.c[a], el.s[a], nl->cx[b], nl->cy[b], nl->c[b], nl->s[b]))
@@ -646,9 +685,10 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
     }
     __syncthreads();
 
+    STAMP(3);
     // ---- greedy resolution in (i, j) order, bonuses, team mix, respawn, flags (:292-370)
     // lane 0 owns the order-dependent scan; masks are 64-bit (N <= 64)
-    if (lane == 0) {
+    if (tid == 0) {
         unsigned long long donem = 0ull, crash = 0ull;
         for (int i = 0; i < N; ++i) if (el.done[i] || !el.alive[i]) donem |= 1ull << i;
         for (int i = 0; i < N; ++i) {
@@ -662,7 +702,7 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
             if ((crash >> i) & 1ull) { el.done[i] = 1; el.status[i] = ST_CRASH_CAR; }
     }
     __syncthreads();
-    for (int i = lane; i < N; i += WAVE) {
+    for (int i = tid; i < N; i += nthr) {
         if (el.done[i]) {
             const uint8_t st = el.status[i];
             if (st == ST_CRASH_CAR) el.rew[i] += p.k_cv;
@@ -671,7 +711,7 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
         }
     }
     __syncthreads();
-    if (lane == 0) {
+    if (tid == 0) {
         if (p.use_team && N > 0) {
             float avg = 0.0f;
             for (int i = 0; i < N; ++i) avg += el.rew[i];
@@ -699,7 +739,7 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
     }
     __syncthreads();
     // respawn crashed egos (:339-351); lane = agent
-    for (int i = lane; i < N; i += WAVE) {
+    for (int i = tid; i < N; i += nthr) {
         const int g = e * N + i;
         out.rew[g] = el.rew[i];
         out.done[g] = el.done[i];
@@ -717,93 +757,49 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
     }
     __syncthreads();
 
-    // ---- LiDAR obstacle table (:374-388): every ego (alive or not), then NPCs
+    STAMP(4);
+    // ---- LiDAR obstacle table (:374-388): every ego (alive or not), then NPCs,
+    // published to HBM for k_lidar together with each agent's candidate mask
     const int nob = N + ncnt;
-    for (int o = lane; o < nob; o += WAVE) {
+    const int OB = p.ob_stride;
+    for (int o = tid; o < nob; o += nthr) {
         float x, y, h, c, s;
         if (o < N) { x = el.x[o]; y = el.y[o]; h = el.h[o]; c = el.c[o]; s = el.s[o]; }
         else { const int k = o - N; x = nl->x[k]; y = nl->y[k]; h = nl->h[k]; c = nl->c[k]; s = nl->s[k]; }
-        const PxBox b = aabb_px(x, y, c, s);
-        ob.x0[o] = b.x0; ob.x1[o] = b.x1; ob.y0[o] = b.y0; ob.y1[o] = b.y1;
+        const PxBox bx = aabb_px(x, y, c, s);
+        ob.x0[o] = bx.x0; ob.x1[o] = bx.x1; ob.y0[o] = bx.y0; ob.y1[o] = bx.y1;
         ob.px[o] = x; ob.py[o] = y; ob.ph[o] = h;
+        p.ob_box[e * OB + o] = make_int4(bx.x0, bx.x1, bx.y0, bx.y1);
+    }
+    for (int i = tid; i < N; i += nthr) { ob.cand[i][0] = 0ull; ob.cand[i][1] = 0ull; }
+    __syncthreads();
+    // per-agent candidate boxes: not self, not state-identical to self within
+    // 1e-3 (Lidar.cpp:55-62), and within max_dist + 2 px of the agent (no probe
+    // beyond max_dist exists, truncation moves a probe < 1 px)
+    for (int pbase = 0; pbase < N * nob; pbase += nthr) {
+        const int pi = pbase + tid;
+        if (pi < N * nob) {
+            const int a = pi / nob, o = pi - a * nob;
+            const float cx = el.x[a], cy = el.y[a];
+            if (o != a && el.alive[a] &&
+                !(fabs_f(ob.px[o] - cx) < 1e-3f && fabs_f(ob.py[o] - cy) < 1e-3f && fabs_f(ob.ph[o] - el.h[a]) < 1e-3f)) {
+                const float ddx = fmaxf(fmaxf((float)ob.x0[o] - cx, cx - (float)ob.x1[o]), 0.0f);
+                const float ddy = fmaxf(fmaxf((float)ob.y0[o] - cy, cy - (float)ob.y1[o]), 0.0f);
+                const float reach = p.lidar_max + 2.0f;
+                if (ddx * ddx + ddy * ddy <= reach * reach) atomicOr(&ob.cand[a][o >> 6], 1ull << (o & 63));
+            }
+        }
     }
     __syncthreads();
-
-    // ---- LiDAR march (Lidar::update, cpp/Lidar.cpp:16-90); lane = (agent, beam)
-    const int R = p.R;
-    const int total = N * R;
-    const float maxd = p.lidar_max, stp = p.lidar_step;
-    for (int w0 = 0; w0 < total; w0 += WAVE) {
-        const int w = w0 + lane;
-        if (w >= total) break;
-        const int a = w / R, b = w - a * R;
-        const int g = e * N + a;
-        float* row = out.obs + (size_t)g * p.D;
-        if (!el.alive[a]) {
-            if (b < p.lidar_slots) row[OBS_HEAD + b] = 0.0f;
-            continue;
-        }
-        const float cx = el.x[a], cy = el.y[a], ch = el.h[a];
-        float sn, cs;
-        sincosf(ch + p.rel_angles[b], &sn, &cs);
-        const float dx = cs, dy = -sn;
-        // candidate obstacles: not self, not state-identical to self, and the
-        // ray segment passes within 2 px of the box (march points are truncated
-        // by < 1 px, so this never drops a box the march could enter)
-        unsigned long long cand[2] = {0ull, 0ull};
-        for (int o = 0; o < nob; ++o) {
-            if (o == a) continue;
-            if (fabs_f(ob.px[o] - cx) < 1e-3f && fabs_f(ob.py[o] - cy) < 1e-3f && fabs_f(ob.ph[o] - ch) < 1e-3f) continue;
-            float t0 = 0.0f, t1 = maxd;
-            const float bx0 = (float)ob.x0[o] - 2.0f, bx1 = (float)ob.x1[o] + 2.0f;
-            const float by0 = (float)ob.y0[o] - 2.0f, by1 = (float)ob.y1[o] + 2.0f;
-            bool ok = true;
-            if (fabs_f(dx) < 1e-9f) ok = cx >= bx0 && cx <= bx1;
-            else {
-                const float inv = 1.0f / dx;
-                float ta = (bx0 - cx) * inv, tb = (bx1 - cx) * inv;
-                if (ta > tb) { const float tt = ta; ta = tb; tb = tt; }
-                t0 = ta > t0 ? ta : t0;
-                t1 = tb < t1 ? tb : t1;
-            }
-            if (ok) {
-                if (fabs_f(dy) < 1e-9f) ok = cy >= by0 && cy <= by1;
-                else {
-                    const float inv = 1.0f / dy;
-                    float ta = (by0 - cy) * inv, tb = (by1 - cy) * inv;
-                    if (ta > tb) { const float tt = ta; ta = tb; tb = tt; }
-                    t0 = ta > t0 ? ta : t0;
-                    t1 = tb < t1 ? tb : t1;
-                }
-            }
-            if (ok && t0 <= t1 + 1.0f) cand[o >> 6] |= 1ull << (o & 63);
-        }
-        float final_dist = maxd;
-        for (float dist = 0.0f; dist < maxd; dist += stp) {
-            const int px = (int)(cx + dx * dist);
-            const int py = (int)(cy + dy * dist);
-            if (px < 0 || px >= WIDTH || py < 0 || py >= HEIGHT) break;
-            if (dist > 0.0f) {
-                if (!is_on_road_px(px, py, p.irw)) { final_dist = dist; break; }
-                bool hit = false;
-#pragma unroll
-                for (int wd = 0; wd < 2; ++wd) {
-                    unsigned long long m = cand[wd];
-                    while (m) {
-                        const int o = (wd << 6) + __builtin_ctzll(m);
-                        m &= m - 1ull;
-                        if (px >= ob.x0[o] && px <= ob.x1[o] && py >= ob.y0[o] && py <= ob.y1[o]) { hit = true; break; }
-                    }
-                    if (hit) break;
-                }
-                if (hit) { final_dist = dist; break; }
-            }
-        }
-        if (b < p.lidar_slots) row[OBS_HEAD + b] = final_dist * p.lidar_inv;
+    for (int i = tid; i < N; i += nthr) {
+        const int g = e * N + i;
+        p.ob_cand[2 * g] = ob.cand[i][0];
+        p.ob_cand[2 * g + 1] = ob.cand[i][1];
     }
 
+    STAMP(5);
     // ---- observation head (:418-520); lane = agent
-    for (int i = lane; i < N; i += WAVE) {
+    for (int i = tid; i < N; i += nthr) {
         const int g = e * N + i;
         float* row = out.obs + (size_t)g * p.D;
         if (!el.alive[i]) {
@@ -814,6 +810,121 @@ __global__ __launch_bounds__(WAVE) void k_step(SimParams p, StepInputs in, Outpu
         const float* path = p.rt.path + (size_t)p.ego.route[g] * (2 * PATH_LEN);
         write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row);
     }
+    STAMP(6);
+}
+
+// ------------------------------------------------------------- LiDAR ---
+// Lidar::update (cpp/Lidar.cpp:16-90) for every (env, agent, beam): one thread
+// per beam, reading the poses k_cars left in HBM (after respawn) and the
+// obstacle boxes / candidate masks it published.
+//
+// The reference marches k = 0..S-1 (dist_k = k*step) and stops at the first k
+// whose truncated pixel is off-screen (no hit), off-road (k>0, hit) or inside
+// another car's AABB (k>0, hit).  We find the same k with far fewer probes:
+//  1. road/screen: exact probe at k, then skip ahead by the number of steps
+//     provably safe from the real-valued point (truncation moves a pixel by
+//     < 1 px, margin 1.5 px): every skipped probe is on-screen and strictly
+//     inside a road strip, so it could not have stopped the march;
+//  2. cars: for each candidate box only the k whose real point lies within
+//     1.5 px of the box are probed exactly, and only below the k of step 1.
+// Bit-identical to the sequential march (tests/test_parity_gpu.py).
+__global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out) {
+    const long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int R = p.R;
+    const long long total = (long long)p.E * p.N * R;
+    if (w >= total) return;
+    const int gb = (int)(w / R);  // e*N + a
+    const int b = (int)(w - (long long)gb * R);
+    const int e = gb / p.N;
+    float* row = out.obs + (size_t)gb * p.D;
+    if (!p.ego.alive[gb]) {
+        if (b < p.lidar_slots) row[OBS_HEAD + b] = 0.0f;
+        return;
+    }
+    const float maxd = p.lidar_max, stp = p.lidar_step;
+    const int S = p.lidar_steps;
+    const float rwf = (float)p.irw;
+    const float inv_stp = __builtin_amdgcn_rcpf(stp);
+    const float cx = p.ego.x[gb], cy = p.ego.y[gb], ch = p.ego.h[gb];
+    float sn, cs;
+    sincosf(ch + p.rel_angles[b], &sn, &cs);
+    const float dx = cs, dy = -sn;
+    // 1. road + screen
+    const float adx = fabs_f(dx), ady = fabs_f(dy);
+    const float iadx = __builtin_amdgcn_rcpf(adx), iady = __builtin_amdgcn_rcpf(ady);
+    const float crf = CORNER_RADIUS, ccen = rwf + crf;
+    int kr = S;
+    bool hit = false;
+    for (int k = 0; k < S;) {
+        const float d = march_dist(p, k);
+        const float fx = cx + dx * d;
+        const float fy = cy + dy * d;
+        const int px = (int)fx, py = (int)fy;
+        if (px < 0 || px >= WIDTH || py < 0 || py >= HEIGHT) { kr = k; break; }
+        if (k > 0 && !is_on_road_px(px, py, p.irw)) { kr = k; hit = true; break; }
+        // Distance along the ray that provably keeps every truncated probe on
+        // screen and on the road (margin 1.5 px > the < 1 px truncation shift).
+        const float ax = fabs_f(fx - 375.0f), ay = fabs_f(fy - 375.0f);
+        const float mx = rwf - 1.5f - ax, my = rwf - 1.5f - ay;
+        float road;
+        if (mx > 0.0f || my > 0.0f) {
+            // strictly inside a strip: |x-375| grows at most |dx| per unit length
+            road = fmaxf(mx > 0.0f ? mx * iadx : 0.0f, my > 0.0f ? my * iady : 0.0f);
+        } else if (ax < ccen && ay < ccen) {
+            // corner square: road outside the grass disc centred on its outer corner
+            const float qx = ax - ccen, qy = ay - ccen;
+            road = fminf(__builtin_sqrtf(qx * qx + qy * qy) - crf, fminf(ccen - ax, ccen - ay)) - 1.5f;
+        } else {
+            road = 0.0f;
+        }
+        const float tx = dx > 0.0f ? (748.5f - fx) * iadx : (fx - 0.5f) * iadx;
+        const float ty = dy > 0.0f ? (748.5f - fy) * iady : (fy - 0.5f) * iady;
+        const float safe = fminf(road, fminf(tx, ty));
+        // probes k+1 .. k+j-1 lie within (j-1)*step <= safe of this point
+        k += (safe >= 2.0f * stp) ? (int)(safe * inv_stp) : 1;
+    }
+    // 2. cars among the agent's candidates (every ego alive or not, then NPCs)
+    const float idx_ = __builtin_amdgcn_rcpf(dx), idy_ = __builtin_amdgcn_rcpf(dy);
+    const int4* boxes = p.ob_box + (size_t)e * p.ob_stride;
+#pragma unroll
+    for (int wd = 0; wd < 2; ++wd)
+    for (unsigned long long cm = p.ob_cand[2 * gb + wd]; cm; cm &= cm - 1ull) {
+        const int o = (wd << 6) + __builtin_ctzll(cm);
+        const int4 bx = boxes[o];
+        const int x0 = bx.x, x1 = bx.y, y0 = bx.z, y1 = bx.w;
+        float t0 = 0.0f, t1 = maxd;
+        const float bx0 = (float)x0 - 1.5f, bx1 = (float)x1 + 1.5f;
+        const float by0 = (float)y0 - 1.5f, by1 = (float)y1 + 1.5f;
+        // slab test on the box grown by 1.5 px (approximate reciprocals are
+        // fine: the range only selects which probes are tested exactly)
+        if (fabs_f(dx) < 1e-6f) {
+            if (cx < bx0 || cx > bx1) continue;
+        } else {
+            const float ta = (bx0 - cx) * idx_, tb = (bx1 - cx) * idx_;
+            t0 = fmaxf(t0, fminf(ta, tb));
+            t1 = fminf(t1, fmaxf(ta, tb));
+        }
+        if (fabs_f(dy) < 1e-6f) {
+            if (cy < by0 || cy > by1) continue;
+        } else {
+            const float ta = (by0 - cy) * idy_, tb = (by1 - cy) * idy_;
+            t0 = fmaxf(t0, fminf(ta, tb));
+            t1 = fminf(t1, fmaxf(ta, tb));
+        }
+        if (!(t0 <= t1 + 0.5f)) continue;
+        int k0 = (int)(t0 * inv_stp) - 1;
+        int k1 = (int)(t1 * inv_stp) + 2;
+        k0 = k0 < 1 ? 1 : k0;
+        k1 = k1 > kr - 1 ? kr - 1 : k1;
+        for (int k = k0; k <= k1; ++k) {
+            const float d = march_dist(p, k);
+            const int px = (int)(cx + dx * d);
+            const int py = (int)(cy + dy * d);
+            if (px >= x0 && px <= x1 && py >= y0 && py <= y1) { kr = k; hit = true; break; }
+        }
+    }
+    const float final_dist = hit ? march_dist(p, kr) : maxd;
+    if (b < p.lidar_slots) row[OBS_HEAD + b] = final_dist * p.lidar_inv;
 }
 
 // ------------------------------------------------- reset / re-observe ---
@@ -875,8 +986,13 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
 }
 
 hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s) {
-    if (p.traffic) hipLaunchKernelGGL(k_step<true>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
-    else hipLaunchKernelGGL(k_step<false>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
+    if (p.traffic) hipLaunchKernelGGL(k_cars<true>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
+    else hipLaunchKernelGGL(k_cars<false>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const long long beams = (long long)p.E * p.N * p.R;
+    const unsigned blocks = (unsigned)((beams + 255) / 256);
+    hipLaunchKernelGGL(k_lidar, dim3(blocks), dim3(256), 0, s, p, out);
     return hipGetLastError();
 }
 

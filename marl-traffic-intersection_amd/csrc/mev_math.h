@@ -325,8 +325,14 @@ MEV_HD float hypotf(float x, float y) {
 }
 
 // ----------------------------------------------------------------- fmodf ---
-// Exact IEEE remainder x - trunc(x/y)*y (bit-level, after musl's fmodf).
-MEV_HD float fmodf(float x, float y) {
+// Exact IEEE remainder x - trunc(x/y)*y.  fmod is exact (the result is always
+// representable), so any correct method returns glibc's bits; this one is
+// branch-light for the GPU: estimate the quotient with a multiply, get the
+// remainder exactly with one fma (exact whenever the quotient is right), and
+// correct a one-off estimate.  Falls back to the bit-level loop when the
+// quotient does not fit in 24 bits.  Checked bit-for-bit against glibc
+// (tests/native/devmath_check.cpp).
+MEV_HD float fmodf_bits(float x, float y) {  // musl-style reference loop
     uint32_t ux = f2u(x), uy = f2u(y);
     int ex = (ux >> 23) & 0xff;
     int ey = (uy >> 23) & 0xff;
@@ -373,6 +379,20 @@ MEV_HD float fmodf(float x, float y) {
     }
     ux |= sx;
     return u2f(ux);
+}
+
+MEV_HD float fmodf(float x, float y) {
+    const float ax = fabs_f(x), ay = fabs_f(y);
+    // fast path: finite, normal y, quotient < 2^23
+    if (ay >= 0x1p-100f && ay < 0x1p100f && ax < ay * 0x1p22f) {
+        if (ax < ay) return x;
+        float q = __builtin_truncf(ax * (1.0f / ay));
+        float r = __builtin_fmaf(-q, ay, ax);  // exact when q == trunc(ax/ay)
+        if (r < 0.0f) { q -= 1.0f; r = __builtin_fmaf(-q, ay, ax); }
+        else if (r >= ay) { q += 1.0f; r = __builtin_fmaf(-q, ay, ax); }
+        return u2f(f2u(r) | (f2u(x) & 0x80000000u));  // result carries the sign of x (also for zero)
+    }
+    return fmodf_bits(x, y);
 }
 
 }  // namespace mev

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <cmath>
 #include <random>
 #include <string>
 #include <thread>
@@ -134,8 +135,20 @@ int main(int argc, char** argv) {
         report("fmodf wrap |a|<=64", sweep_abs(64.0f, stride, [&](float a) -> uint64_t {
             return same(mev::fmodf(a + PI_F, 2.0f * PI_F), ::fmodf(a + PI_F, 2.0f * PI_F)) ? 0 : 1;
         }), 2ull * f2u_(64.0f) / stride);
+        report("fmodf |x|<=1e6, y=2pi", sweep_abs(1e6f, stride * 5, [&](float a) -> uint64_t {
+            return same(mev::fmodf(a, 2.0f * PI_F), ::fmodf(a, 2.0f * PI_F)) ? 0 : 1;
+        }), 2ull * f2u_(1e6f) / (stride * 5));
         std::mt19937 rng(7);
         std::uniform_int_distribution<uint32_t> bits;
+        std::uniform_real_distribution<float> mag(-30.0f, 30.0f);
+        uint64_t badp = 0;
+        const int NP = exhaustive ? 200000000 : 5000000;
+        for (int k = 0; k < NP; ++k) {  // random pairs of moderate magnitude (fast path)
+            float x = std::ldexp(1.0f + (bits(rng) & 0xffff) / 65536.0f, int(mag(rng))) * ((bits(rng) & 1) ? -1.f : 1.f);
+            float y = std::ldexp(1.0f + (bits(rng) & 0xffff) / 65536.0f, int(mag(rng))) * ((bits(rng) & 1) ? -1.f : 1.f);
+            badp += same(mev::fmodf(x, y), ::fmodf(x, y)) ? 0 : 1;
+        }
+        report("fmodf random moderate pairs", badp, NP);
         uint64_t bad = 0;
         const int N = exhaustive ? 200000000 : 5000000;
         for (int k = 0; k < N; ++k) {
