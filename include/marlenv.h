@@ -59,7 +59,7 @@ typedef struct {
     int32_t num_envs;        /* E >= 1                                                     */
     int32_t num_agents;      /* N, 1..64 ego cars per env                                   */
     int32_t num_lanes;       /* lanes per direction (reference default 3)                  */
-    int32_t lidar_rays;      /* R >= 1 (reference hard-codes 96, IntersectionEnv.cpp:113)  */
+    int32_t lidar_rays;      /* R in [1, 1024] (reference hard-codes 96, IntersectionEnv.cpp:113) */
     float lidar_fov_deg;     /* 360                                                        */
     float lidar_max_dist;    /* 250 px                                                     */
     float lidar_step;        /* 4 px                                                       */

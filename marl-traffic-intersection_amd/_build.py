@@ -36,6 +36,10 @@ def _inputs():
 
 
 VARIANTS = {"": [], "stamps": ["-DMEV_STAMPS"]}
+# timing-only experiment builds (wrong results by construction; never used by the product)
+EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOCARS"],
+               "exp_none": ["-DMEV_EXP_NOROAD", "-DMEV_EXP_NOCARS"], "exp_iters": ["-DMEV_ITERS"]}
+VARIANTS.update(EXPERIMENTS)
 
 
 def lib_path(variant: str = "") -> str:
@@ -70,7 +74,7 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
-    if "--all" in sys.argv:
+    if "--all" in sys.argv or "--exp" in sys.argv:
         for v in VARIANTS:
-            if v:
+            if v and (v in EXPERIMENTS) == ("--exp" in sys.argv):
                 print(build(force="--force" in sys.argv, verbose=True, variant=v))

@@ -125,7 +125,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     if (c.num_envs < 1) return fail(MEV_E_INVALID, "num_envs must be >= 1");
     if (c.num_agents < 1 || c.num_agents > 64) return fail(MEV_E_INVALID, "num_agents must be in [1, 64]");
     if (c.num_lanes < 1 || c.num_lanes > 8) return fail(MEV_E_INVALID, "num_lanes must be in [1, 8]");
-    if (c.lidar_rays < 1 || c.lidar_rays > 4096) return fail(MEV_E_INVALID, "lidar_rays must be in [1, 4096]");
+    if (c.lidar_rays < 1 || c.lidar_rays > 1024) return fail(MEV_E_INVALID, "lidar_rays must be in [1, 1024]");
     if (!(c.lidar_step > 0.0f) || !(c.lidar_max_dist > 0.0f)) return fail(MEV_E_INVALID, "lidar step/max_dist must be > 0");
     if (c.max_npcs < 0 || c.max_npcs > 64) return fail(MEV_E_INVALID, "max_npcs must be in [0, 64]");
     const int D = c.obs_dim > 0 ? c.obs_dim : mev::OBS_HEAD + c.lidar_rays;

@@ -828,13 +828,60 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 //  2. cars: for each candidate box only the k whose real point lies within
 //     1.5 px of the box are probed exactly, and only below the k of step 1.
 // Bit-identical to the sequential march (tests/test_parity_gpu.py).
-__global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out) {
-    const long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int R = p.R;
-    const long long total = (long long)p.E * p.N * R;
-    if (w >= total) return;
-    const int gb = (int)(w / R);  // e*N + a
-    const int b = (int)(w - (long long)gb * R);
+// Probe coordinate of a beam: c(k) = (int)(c0 + dc * dist_k).  dist_k grows
+// with k and IEEE rounding and truncation are monotone, so c(k) is monotone
+// in k (non-decreasing for dc > 0, non-increasing for dc < 0).  That makes
+// "k with c(k) inside [lo, hi]" an interval whose ends we find from a real
+// estimate corrected by exact probes (usually 0-1 extra probe per end).
+__device__ inline int probe_c(const SimParams& p, float c0, float dc, int k) {
+    return (int)(c0 + dc * march_dist(p, k));
+}
+
+// Interval [*k0, *k1] of probes k in [0, S-1] with lo <= c(k) <= hi (empty: *k0 > *k1).
+__device__ inline void coord_interval(const SimParams& p, float c0, float dc, int lo, int hi, int S, float inv_stp,
+                                      int* k0, int* k1) {
+    if (fabs_f(dc) < 1e-6f) {  // effectively constant over <= max_dist
+        // still evaluate exactly at both ends (c(k) may step by one pixel)
+        int a = 0, b = S - 1;
+        const int ca = probe_c(p, c0, dc, 0), cb = probe_c(p, c0, dc, S - 1);
+        if ((ca < lo || ca > hi) && (cb < lo || cb > hi)) { *k0 = 1; *k1 = 0; return; }
+        while (a <= b) { const int c = probe_c(p, c0, dc, a); if (c >= lo && c <= hi) break; ++a; }
+        while (b >= a) { const int c = probe_c(p, c0, dc, b); if (c >= lo && c <= hi) break; --b; }
+        *k0 = a; *k1 = b;
+        return;
+    }
+    // entry bound E (first k with c(k) past it), exit bound X (last k not past it)
+    const bool inc = dc > 0.0f;
+    const float ent = inc ? (float)lo : (float)hi;  // c(k) >= lo  (inc)  /  c(k) <= hi (dec)
+    const float ext = inc ? (float)hi : (float)lo;  // c(k) <= hi  (inc)  /  c(k) >= lo (dec)
+    const float scale = __builtin_amdgcn_rcpf(dc) * inv_stp;
+    auto entered = [&](int k) { const int c = probe_c(p, c0, dc, k); return inc ? c >= lo : c <= hi; };
+    auto not_exited = [&](int k) { const int c = probe_c(p, c0, dc, k); return inc ? c <= hi : c >= lo; };
+    float fe = (ent - c0) * scale;
+    float fx = (ext + (inc ? 1.0f : -1.0f) - c0) * scale;
+    fe = fminf(fmaxf(fe, 0.0f), (float)(S - 1));
+    fx = fminf(fmaxf(fx, 0.0f), (float)(S - 1));
+    int ke = (int)fe;
+    while (ke > 0 && entered(ke - 1)) --ke;
+    while (ke < S && !entered(ke)) ++ke;
+    if (ke >= S) { *k0 = 1; *k1 = 0; return; }
+    int kx = (int)fx;
+    if (kx < ke) kx = ke;
+    while (kx + 1 < S && not_exited(kx + 1)) ++kx;
+    while (kx >= ke && !not_exited(kx)) --kx;
+    *k0 = ke;
+    *k1 = kx;
+}
+
+template <bool TAB>
+__global__ __launch_bounds__(1024) void k_lidar(SimParams p, Outputs out) {
+    // one (env, agent) per Ta = roundup(R, 64) threads, 256/Ta agents per block:
+    // the pose, liveness and candidate masks are wave-uniform; one thread per beam
+    const int Ta = (p.R + WAVE - 1) / WAVE * WAVE;
+    // Ta is a multiple of 64, so every wave serves exactly one agent
+    const int gb = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / Ta) + threadIdx.x / Ta);  // e*N + a
+    const int b = threadIdx.x % Ta;
+    if (gb >= p.E * p.N || b >= p.R) return;
     const int e = gb / p.N;
     float* row = out.obs + (size_t)gb * p.D;
     if (!p.ego.alive[gb]) {
@@ -849,79 +896,93 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out) {
     float sn, cs;
     sincosf(ch + p.rel_angles[b], &sn, &cs);
     const float dx = cs, dy = -sn;
-    // 1. road + screen
+    // 1. road + screen: exact probes, skipping provably-safe stretches
     const float adx = fabs_f(dx), ady = fabs_f(dy);
     const float iadx = __builtin_amdgcn_rcpf(adx), iady = __builtin_amdgcn_rcpf(ady);
     const float crf = CORNER_RADIUS, ccen = rwf + crf;
+    const float cr2 = crf * crf;
+    const float two_stp = 2.0f * stp;
+    // Lanes step in lockstep with predication instead of per-lane breaks: the
+    // loop exit is wave-uniform, so divergence costs no exec-mask juggling.
     int kr = S;
     bool hit = false;
-    for (int k = 0; k < S;) {
-        const float d = march_dist(p, k);
+    int k = 0;
+#ifdef MEV_EXP_NOROAD
+    bool active = false;
+#else
+    bool active = S > 0;
+#endif
+    const float rw_m = rwf, ccen_m = ccen, cr2p1 = cr2 + 1.0f;
+#ifdef MEV_ITERS
+    int iters = 0;
+#endif
+    while (__builtin_amdgcn_ballot_w64(active) != 0ull) {
+        const int kk = active ? k : 0;
+        const float d = TAB ? p.dist_tab[kk] : (float)kk * stp;
         const float fx = cx + dx * d;
         const float fy = cy + dy * d;
         const int px = (int)fx, py = (int)fy;
-        if (px < 0 || px >= WIDTH || py < 0 || py >= HEIGHT) { kr = k; break; }
-        if (k > 0 && !is_on_road_px(px, py, p.irw)) { kr = k; hit = true; break; }
+        // exact reference predicates at the truncated pixel (Lidar.cpp:36-48):
+        // screen, then (k > 0) road == RoadGeometry::is_on_road at integer pixels:
+        //   on_road <=> dist^2 to the grass-disc centre > cr^2 (integers: >= cr^2+1)
+        //               and (in a strip: min(ax, ay) <= rw  or  in the corner square: max <= rw+cr)
+        const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
+        const bool off_screen = pmax >= (unsigned)WIDTH;
+        const float iax = fabs_f((float)(px - 375)), iay = fabs_f((float)(py - 375));
+        const float qdx = iax - ccen_m, qdy = iay - ccen_m;
+        const float onv = fmaxf(fminf(fminf(iax, iay) - rw_m, fmaxf(iax, iay) - ccen_m), cr2p1 - (qdx * qdx + qdy * qdy));
+        const bool off_road = (kk > 0) & (onv > 0.0f);
+        const bool stop = active & (off_screen | off_road);
+        kr = stop ? kk : kr;
+        hit = stop ? !off_screen : hit;
         // Distance along the ray that provably keeps every truncated probe on
         // screen and on the road (margin 1.5 px > the < 1 px truncation shift).
         const float ax = fabs_f(fx - 375.0f), ay = fabs_f(fy - 375.0f);
         const float mx = rwf - 1.5f - ax, my = rwf - 1.5f - ay;
-        float road;
-        if (mx > 0.0f || my > 0.0f) {
-            // strictly inside a strip: |x-375| grows at most |dx| per unit length
-            road = fmaxf(mx > 0.0f ? mx * iadx : 0.0f, my > 0.0f ? my * iady : 0.0f);
-        } else if (ax < ccen && ay < ccen) {
-            // corner square: road outside the grass disc centred on its outer corner
-            const float qx = ax - ccen, qy = ay - ccen;
-            road = fminf(__builtin_sqrtf(qx * qx + qy * qy) - crf, fminf(ccen - ax, ccen - ay)) - 1.5f;
-        } else {
-            road = 0.0f;
-        }
-        const float tx = dx > 0.0f ? (748.5f - fx) * iadx : (fx - 0.5f) * iadx;
-        const float ty = dy > 0.0f ? (748.5f - fy) * iady : (fy - 0.5f) * iady;
+        // strictly inside a strip: |x-375| grows at most |dx| per unit length
+        const float strip = fmaxf(fmaxf(mx, 0.0f) * iadx, fmaxf(my, 0.0f) * iady);
+        // corner square: road outside the grass disc on its outer corner
+        // (approximate sqrt: bound only, extra 0.05 px margin)
+        const float qx = ax - ccen, qy = ay - ccen;
+        const float corner = fminf(__builtin_amdgcn_sqrtf(qx * qx + qy * qy) - crf, fminf(ccen - ax, ccen - ay)) - 1.55f;
+        const float road = fmaxf(mx, my) > 0.0f ? strip : (fmaxf(ax, ay) < ccen ? corner : 0.0f);
+        const float tx = (dx > 0.0f ? 748.5f - fx : fx - 0.5f) * iadx;
+        const float ty = (dy > 0.0f ? 748.5f - fy : fy - 0.5f) * iady;
         const float safe = fminf(road, fminf(tx, ty));
         // probes k+1 .. k+j-1 lie within (j-1)*step <= safe of this point
-        k += (safe >= 2.0f * stp) ? (int)(safe * inv_stp) : 1;
+        const int jump = (safe >= two_stp) ? (int)(safe * inv_stp) : 1;
+        k = kk + jump;
+        active = active & !stop & (k < S);
+#ifdef MEV_ITERS
+        ++iters;
+#endif
     }
-    // 2. cars among the agent's candidates (every ego alive or not, then NPCs)
-    const float idx_ = __builtin_amdgcn_rcpf(dx), idy_ = __builtin_amdgcn_rcpf(dy);
+#ifdef MEV_ITERS
+    // diagnostic build: wave iteration count and summed per-lane iterations
+    if (b == 0 && gb < p.E * 8) p.debug[gb] = (unsigned long long)iters;
+#endif
+    // 2. cars among the agent's candidates (every ego alive or not, then NPCs):
+    //    the probes inside a box form the intersection of the x- and y-intervals
     const int4* boxes = p.ob_box + (size_t)e * p.ob_stride;
+#ifdef MEV_EXP_NOCARS
+    const unsigned long long cand0 = 0, cand1 = 0;
+#else
+    const unsigned long long cand0 = p.ob_cand[2 * gb], cand1 = p.ob_cand[2 * gb + 1];
+#endif
 #pragma unroll
     for (int wd = 0; wd < 2; ++wd)
-    for (unsigned long long cm = p.ob_cand[2 * gb + wd]; cm; cm &= cm - 1ull) {
+    for (unsigned long long cm = wd ? cand1 : cand0; cm; cm &= cm - 1ull) {
         const int o = (wd << 6) + __builtin_ctzll(cm);
         const int4 bx = boxes[o];
-        const int x0 = bx.x, x1 = bx.y, y0 = bx.z, y1 = bx.w;
-        float t0 = 0.0f, t1 = maxd;
-        const float bx0 = (float)x0 - 1.5f, bx1 = (float)x1 + 1.5f;
-        const float by0 = (float)y0 - 1.5f, by1 = (float)y1 + 1.5f;
-        // slab test on the box grown by 1.5 px (approximate reciprocals are
-        // fine: the range only selects which probes are tested exactly)
-        if (fabs_f(dx) < 1e-6f) {
-            if (cx < bx0 || cx > bx1) continue;
-        } else {
-            const float ta = (bx0 - cx) * idx_, tb = (bx1 - cx) * idx_;
-            t0 = fmaxf(t0, fminf(ta, tb));
-            t1 = fminf(t1, fmaxf(ta, tb));
-        }
-        if (fabs_f(dy) < 1e-6f) {
-            if (cy < by0 || cy > by1) continue;
-        } else {
-            const float ta = (by0 - cy) * idy_, tb = (by1 - cy) * idy_;
-            t0 = fmaxf(t0, fminf(ta, tb));
-            t1 = fminf(t1, fmaxf(ta, tb));
-        }
-        if (!(t0 <= t1 + 0.5f)) continue;
-        int k0 = (int)(t0 * inv_stp) - 1;
-        int k1 = (int)(t1 * inv_stp) + 2;
-        k0 = k0 < 1 ? 1 : k0;
-        k1 = k1 > kr - 1 ? kr - 1 : k1;
-        for (int k = k0; k <= k1; ++k) {
-            const float d = march_dist(p, k);
-            const int px = (int)(cx + dx * d);
-            const int py = (int)(cy + dy * d);
-            if (px >= x0 && px <= x1 && py >= y0 && py <= y1) { kr = k; hit = true; break; }
-        }
+        if (kr <= 1) break;
+        int ax0, ax1, ay0, ay1;
+        coord_interval(p, cx, dx, bx.x, bx.y, kr, inv_stp, &ax0, &ax1);
+        if (ax0 > ax1) continue;
+        coord_interval(p, cy, dy, bx.z, bx.w, kr, inv_stp, &ay0, &ay1);
+        int k0 = ax0 > ay0 ? ax0 : ay0;
+        const int k1 = ax1 < ay1 ? ax1 : ay1;
+        k0 = k0 < 1 ? 1 : k0;  // no car test at dist == 0
+        if (k0 <= k1) { kr = k0; hit = true; }  // k1 <= kr-1 by construction
     }
     const float final_dist = hit ? march_dist(p, kr) : maxd;
     if (b < p.lidar_slots) row[OBS_HEAD + b] = final_dist * p.lidar_inv;
@@ -990,9 +1051,11 @@ hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& 
     else hipLaunchKernelGGL(k_cars<false>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const long long beams = (long long)p.E * p.N * p.R;
-    const unsigned blocks = (unsigned)((beams + 255) / 256);
-    hipLaunchKernelGGL(k_lidar, dim3(blocks), dim3(256), 0, s, p, out);
+    const int Ta = (p.R + WAVE - 1) / WAVE * WAVE;
+    const int per = Ta >= 256 ? 1 : 256 / Ta;
+    const unsigned blocks = (unsigned)((p.E * p.N + per - 1) / per);
+    if (p.dist_tab) hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(per * Ta), 0, s, p, out);
+    else hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(per * Ta), 0, s, p, out);
     return hipGetLastError();
 }
 
