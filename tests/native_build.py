@@ -1,0 +1,22 @@
+"""Build helpers for the host-side native checks (tests/native/*.cpp)."""
+import os
+import subprocess
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(ROOT, "marl-traffic-intersection_amd", "csrc")
+OUT = os.path.join(tempfile.gettempdir(), "mev_native_tests")
+
+
+def build(name: str) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    src = os.path.join(HERE, "native", name + ".cpp")
+    exe = os.path.join(OUT, name)
+    deps = [src] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    if os.path.exists(exe) and all(os.path.getmtime(d) <= os.path.getmtime(exe) for d in deps):
+        return exe
+    # same rounding discipline as the device build: no contraction, plain x86-64
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread", "-I", CSRC, src, "-o", exe, "-lm"],
+                   check=True, capture_output=True)
+    return exe

@@ -1,0 +1,70 @@
+"""Replay golden scenarios through the C restatement (oracle/marl_oracle.c)."""
+import os
+import sys
+
+import numpy as np
+
+import golden_replay as G
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import oracle as O  # noqa: E402
+
+
+def state_from_records(f, i, routes):
+    cars = np.zeros(len(f), O.CAR_DTYPE)
+    names = ["x", "y", "v", "h", "acc", "steer", "sx", "sy", "sv", "sh", "prev_dist", "pa0", "pa1"]
+    for j, nm in enumerate(names):
+        cars[nm] = f[:, j]
+    cars["alive"] = i[:, 0]
+    cars["intention"] = i[:, 1]
+    cars["path_index"] = i[:, 2]
+    cars["route"] = routes
+    return cars
+
+
+def make_oracle(meta):
+    R = int(meta["rays"])
+    return O.OracleEnv(num_lanes=int(meta["num_lanes"]), n_agents=int(meta["n_agents"]), rays=R,
+                       obs_dim=127 if R <= 96 else 31 + R, use_team=bool(meta["use_team"]),
+                       respawn=bool(meta["respawn"]), max_steps=int(meta["max_steps"]), traffic=bool(meta["traffic"]),
+                       density=float(meta["density"]), reward=meta["reward"], max_npcs=64)
+
+
+def replay(name):
+    d = G.load(name)
+    meta = d["meta"]
+    L = int(meta["num_lanes"])
+    env = make_oracle(meta)
+    tr = [env.route_id(G.point_index(s, L), G.point_index(e, L)) for s, e in meta["traffic_routes"]]
+    env.set_traffic_routes(tr)
+    ego_routes = [env.route_id(G.point_index(s, L), G.point_index(e, L)) for s, e in meta["ego_routes"]]
+    egos = state_from_records(d["init_ego_f"], d["init_ego_i"], ego_routes)
+    k = len(d["init_npc_f"])
+    npcs = state_from_records(d["init_npc_f"], d["init_npc_i"], [tr[r] for r in d["init_npc_i"][:, 3]]) if k else []
+    env.set_state(egos, npcs, 0)
+    errs = []
+    if not G.bits_equal(env.observe()[:, :127], d["init_obs"]):
+        errs.append("initial obs")
+    for t in range(int(meta["steps"])):
+        r = env.step(d["actions"][t], float(meta["dt"]), int(d["spawned"][t]) if meta["traffic"] else -1)
+        if not G.bits_equal(r["obs"][:, :127], d["obs"][t]):
+            errs.append(f"step {t + 1}: obs")
+        if not G.bits_equal(r["rew"], d["rew"][t]):
+            errs.append(f"step {t + 1}: reward")
+        if not G.bits_equal(r["status"], d["status"][t]) or not G.bits_equal(r["done"], d["done"][t]):
+            errs.append(f"step {t + 1}: status/done")
+        if [r["terminated"], r["truncated"], r["agents_alive"], r["step"]] != [int(x) for x in d["flags"][t]]:
+            errs.append(f"step {t + 1}: flags")
+        if "lidar" in d and not G.bits_equal(r["obs"][:, 31:], d["lidar"][t] * np.float32(1.0 / 250.0)):
+            errs.append(f"step {t + 1}: full lidar")
+        egos, npcs, sc = env.get_state()
+        ef = d["ego_f"][t]
+        for j, nm in enumerate(["x", "y", "v", "h", "acc", "steer", "sx", "sy", "sv", "sh", "prev_dist", "pa0", "pa1"]):
+            if not G.bits_equal(egos[nm], ef[:, j]):
+                errs.append(f"step {t + 1}: ego {nm}")
+        if len(npcs) != int(d["npc_count"][t]):
+            errs.append(f"step {t + 1}: npc count")
+        if errs:
+            break
+    env.close()
+    return errs

@@ -1,0 +1,170 @@
+"""Device path vs the C restatement (oracle/marl_oracle.c, itself pinned to the
+reference by tests/test_oracle.py) on randomized inputs the golden set does not
+cover: random poses/speeds/controls/path indices for every ego, random NPC
+fleets placed on their routes, random (partly unclipped) actions and random
+spawn decisions, many envs per handle.  Bit-exact on every output and on the
+full state after every step."""
+import numpy as np
+import pytest
+
+import golden_replay as G
+import oracle_replay as R
+
+pytestmark = pytest.mark.gpu
+
+ROUTES3 = [(1, 4), (2, 8), (3, 12), (4, 7), (5, 11), (6, 3), (7, 10), (8, 2), (9, 6), (10, 1), (11, 5), (12, 9)]
+ROUTES2 = [(1, 3), (2, 6), (3, 5), (4, 8), (6, 2), (7, 1), (8, 4)]
+
+CONFIGS = [
+    dict(name="n8_r64_team", n=8, rays=64, use_team=True),
+    dict(name="n1_r64", n=1, rays=64),
+    dict(name="n3_r16_norespawn", n=3, rays=16, respawn=False, max_steps=40),
+    dict(name="n12_r96_obs127", n=12, rays=96),
+    dict(name="n8_r128", n=8, rays=128, use_team=True),
+    dict(name="lanes2_n7", n=7, rays=64, lanes=2),
+    dict(name="n5_r33_custom", n=5, rays=33, reward=[3.0, 0.5, -0.1, -2.0, -1.0, 4.0, -0.3, 0.7], dt=1 / 30),
+    dict(name="traffic_n1", n=1, rays=64, traffic=True, density=0.5, spawn_p=0.15, npcs=6),
+    dict(name="traffic_n3", n=3, rays=48, traffic=True, density=2.0, spawn_p=0.3, npcs=9),
+]
+
+
+def _random_state(rng, h, n, npcs, lanes, routes_table):
+    E = h.E
+    st = h.get_state()
+    P = 8 * lanes
+    nr = len(routes_table)
+    ego_routes = np.zeros((E, n), np.int32)
+    for e in range(E):
+        for i in range(n):
+            s, t = routes_table[rng.integers(0, nr)]
+            ego_routes[e, i] = h.route_id(s - 1, 4 * lanes + t - 1)
+    h.set_ego_routes(ego_routes)
+    st["route"][:] = ego_routes
+    rw = 42 * lanes
+    for e in range(E):
+        for i in range(n):
+            path, intent, spawn = h.route_info(int(ego_routes[e, i]))
+            if rng.uniform() < 0.7:  # near its route
+                j = int(rng.integers(0, 150))
+                x, y = path[j] + rng.normal(0, 4, 2)
+                hd = np.arctan2(-(path[j + 1, 1] - path[j, 1]), path[j + 1, 0] - path[j, 0]) + rng.normal(0, 0.2)
+                pidx = max(0, j - int(rng.integers(0, 5)))
+            else:  # anywhere in the cross
+                x, y = rng.uniform(375 - rw, 375 + rw), rng.uniform(0, 750)
+                if rng.uniform() < 0.5:
+                    x, y = y, x
+                hd = rng.uniform(-np.pi, np.pi)
+                pidx = int(rng.integers(0, 150))
+            st["x"][e, i], st["y"][e, i] = x, y
+            st["heading"][e, i] = hd
+            st["v"][e, i] = rng.uniform(0, 8)
+            st["acc"][e, i] = rng.uniform(-15, 15)
+            st["steering"][e, i] = rng.uniform(-0.6, 0.6)
+            st["prev_dist"][e, i] = rng.uniform(0, 700) if rng.uniform() < 0.8 else 0.0
+            st["prev_a0"][e, i], st["prev_a1"][e, i] = rng.uniform(-1, 1, 2)
+            st["spawn_x"][e, i], st["spawn_y"][e, i], st["spawn_heading"][e, i] = spawn
+            st["spawn_v"][e, i] = 0.0
+            st["path_index"][e, i] = pidx
+            st["intention"][e, i] = intent
+            st["alive"][e, i] = 0 if rng.uniform() < 0.05 else 1
+    troutes = [h.route_id(s - 1, 4 * lanes + t - 1) for s, t in routes_table]
+    for e in range(E):
+        k = int(rng.integers(0, npcs + 1)) if npcs else 0
+        placed = []
+        cnt = 0
+        for _ in range(k * 10):
+            if cnt >= k:
+                break
+            ri = int(rng.integers(0, len(troutes)))
+            path, intent, spawn = h.route_info(troutes[ri])
+            j = int(rng.integers(0, 150))
+            x, y = path[j]
+            if any((x - a) ** 2 + (y - b) ** 2 < 60 ** 2 for a, b in placed):
+                continue
+            placed.append((x, y))
+            st["npc_x"][e, cnt], st["npc_y"][e, cnt] = x + rng.normal(0, 1), y + rng.normal(0, 1)
+            st["npc_heading"][e, cnt] = np.arctan2(-(path[j + 1, 1] - path[j, 1]), path[j + 1, 0] - path[j, 0])
+            st["npc_v"][e, cnt] = rng.uniform(0, 5)
+            st["npc_acc"][e, cnt] = 0.0
+            st["npc_steering"][e, cnt] = rng.uniform(-0.2, 0.2)
+            st["npc_path_index"][e, cnt] = max(0, j - 1)
+            st["npc_route"][e, cnt] = troutes[ri]
+            st["npc_intention"][e, cnt] = intent
+            st["npc_alive"][e, cnt] = 1
+            cnt += 1
+        st["npc_count"][e] = cnt
+    st["step_count"][:] = rng.integers(0, 5, E)
+    h.set_state(st)
+    return st, troutes
+
+
+def _oracle_from_state(cfg, st, e, troutes):
+    n = cfg["n"]
+    meta = dict(rays=cfg["rays"], num_lanes=cfg.get("lanes", 3), n_agents=n, use_team=cfg.get("use_team", False),
+                respawn=cfg.get("respawn", True), max_steps=cfg.get("max_steps", 2000),
+                traffic=cfg.get("traffic", False), density=cfg.get("density", 0.5),
+                reward=cfg.get("reward", [10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2]))
+    o = R.make_oracle(meta)
+    o.set_traffic_routes(troutes)
+    cars = np.zeros(n, R.O.CAR_DTYPE)
+    m = {"x": "x", "y": "y", "v": "v", "h": "heading", "acc": "acc", "steer": "steering", "sx": "spawn_x",
+         "sy": "spawn_y", "sv": "spawn_v", "sh": "spawn_heading", "prev_dist": "prev_dist", "pa0": "prev_a0",
+         "pa1": "prev_a1", "path_index": "path_index", "route": "route", "intention": "intention", "alive": "alive"}
+    for a, b in m.items():
+        cars[a] = st[b][e]
+    k = int(st["npc_count"][e])
+    npcs = np.zeros(k, R.O.CAR_DTYPE)
+    mn = {"x": "npc_x", "y": "npc_y", "v": "npc_v", "h": "npc_heading", "acc": "npc_acc", "steer": "npc_steering",
+          "path_index": "npc_path_index", "route": "npc_route", "intention": "npc_intention", "alive": "npc_alive"}
+    for a, b in mn.items():
+        npcs[a] = st[b][e, :k]
+    o.set_state(cars, npcs, int(st["step_count"][e]))
+    return o
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[c["name"] for c in CONFIGS])
+def test_random_states_match_oracle(mev, cfg):
+    rng = np.random.default_rng(abs(hash(cfg["name"])) % 2 ** 32)
+    E, T = 24, 50
+    n, lanes = cfg["n"], cfg.get("lanes", 3)
+    R_ = cfg["rays"]
+    D = 127 if R_ <= 96 else 31 + R_
+    h = mev.Handle(num_envs=E, num_agents=n, num_lanes=lanes, lidar_rays=R_, obs_dim=D,
+                   traffic_flow=int(cfg.get("traffic", False)), traffic_density=cfg.get("density", 0.5),
+                   use_team_reward=int(cfg.get("use_team", False)), respawn_enabled=int(cfg.get("respawn", True)),
+                   max_steps=cfg.get("max_steps", 2000), max_npcs=64,
+                   reward=cfg.get("reward", [10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2]))
+    table = ROUTES2 if lanes == 2 else ROUTES3
+    st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table)
+    h.set_traffic_routes(troutes)
+    oracles = [_oracle_from_state(cfg, st, e, troutes) for e in range(E)]
+    obs0 = h.observations()
+    for e in range(E):
+        assert G.bits_equal(obs0[e], oracles[e].observe()), f"env {e}: observation after set_state"
+    dt = cfg.get("dt", 1 / 60)
+    out = h.alloc_outputs()
+    for t in range(T):
+        acts = rng.uniform(-1, 1, (E, n, 2)).astype(np.float32)
+        acts[rng.uniform(size=(E, n)) < 0.1] *= 2.5  # unclipped inputs
+        acts[..., 0][rng.uniform(size=(E, n)) < 0.1] = 0.0  # exact-zero throttle (friction branch)
+        spawn = None
+        if cfg.get("traffic"):
+            spawn = np.where(rng.uniform(size=E) < cfg["spawn_p"], rng.integers(0, len(troutes), E), -1).astype(np.int32)
+        h.step(acts, dt, out=out, spawn_route=spawn)
+        gst = h.get_state()
+        for e in range(E):
+            r = oracles[e].step(acts[e], dt, int(spawn[e]) if spawn is not None else -1)
+            tag = f"{cfg['name']} env {e} step {t + 1}"
+            assert G.bits_equal(out["obs"][e], r["obs"]), tag + ": obs"
+            assert G.bits_equal(out["reward"][e], r["rew"]), tag + ": reward"
+            assert G.bits_equal(out["status"][e], r["status"]) and G.bits_equal(out["done"][e], r["done"]), tag
+            got = [int(out["terminated"][e]), int(out["truncated"][e]), int(out["agents_alive"][e]), int(out["step"][e])]
+            assert got == [r["terminated"], r["truncated"], r["agents_alive"], r["step"]], tag + ": flags"
+            egos, npcs, sc = oracles[e].get_state()
+            assert G.bits_equal(gst["x"][e], egos["x"]) and G.bits_equal(gst["heading"][e], egos["h"]), tag + ": pose"
+            assert G.bits_equal(gst["path_index"][e], egos["path_index"]), tag + ": path_index"
+            assert int(gst["npc_count"][e]) == len(npcs), tag + ": npc count"
+            k = len(npcs)
+            if k:
+                assert G.bits_equal(gst["npc_x"][e, :k], npcs["x"]) and G.bits_equal(gst["npc_v"][e, :k], npcs["v"]), tag
+    h.close()

@@ -1,0 +1,136 @@
+"""Full-size (BASELINE config 3: 4096 envs x 8 agents x 64 beams) properties of
+the device path that do not need an oracle: determinism, env independence
+(a permutation of envs permutes every output), batched == single-env,
+auto-reset/truncation semantics and output invariants."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+E, N, R = 4096, 8, 64
+
+
+def _handle(mev, **kw):
+    cfg = dict(num_envs=E, num_agents=N, lidar_rays=R, use_team_reward=1)
+    cfg.update(kw)
+    return mev.Handle(**cfg)
+
+
+def _warm_state(mev, steps=60, seed=0):
+    """A diverse state: run random actions from reset."""
+    h = _handle(mev)
+    rng = np.random.default_rng(seed)
+    for _ in range(steps):
+        h.step(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32))
+    st = h.get_state()
+    h.close()
+    return st
+
+
+def test_determinism_full_size(mev):
+    st = _warm_state(mev)
+    rng = np.random.default_rng(1)
+    acts = rng.uniform(-1, 1, (10, E, N, 2)).astype(np.float32)
+    outs = []
+    for _ in range(2):
+        h = _handle(mev)
+        h.set_state(st)
+        o = [h.step(a) for a in acts]
+        outs.append((o, h.get_state()))
+        h.close()
+    for a, b in zip(outs[0][0], outs[1][0]):
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
+    for k in outs[0][1]:
+        assert np.array_equal(outs[0][1][k], outs[1][1][k]), k
+
+
+def test_env_permutation_equivariance(mev):
+    st = _warm_state(mev, seed=2)
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(E)
+    acts = rng.uniform(-1, 1, (8, E, N, 2)).astype(np.float32)
+    h1, h2 = _handle(mev), _handle(mev)
+    h1.set_state(st)
+    h2.set_state({k: v[perm] for k, v in st.items()})
+    for a in acts:
+        o1 = h1.step(a)
+        o2 = h2.step(a[perm])
+        for k in o1:
+            assert np.array_equal(o1[k][perm], o2[k]), k
+    h1.close()
+    h2.close()
+
+
+def test_batched_equals_single_env(mev):
+    st = _warm_state(mev, seed=4)
+    rng = np.random.default_rng(5)
+    acts = rng.uniform(-1, 1, (6, E, N, 2)).astype(np.float32)
+    hb = _handle(mev)
+    hb.set_state(st)
+    picks = [0, 1, 777, 4095]
+    singles = []
+    for e in picks:
+        hs = mev.Handle(num_envs=1, num_agents=N, lidar_rays=R, use_team_reward=1)
+        hs.set_state({k: v[e:e + 1] for k, v in st.items()})
+        singles.append(hs)
+    for a in acts:
+        ob = hb.step(a)
+        for e, hs in zip(picks, singles):
+            os_ = hs.step(a[e:e + 1])
+            for k in ob:
+                assert np.array_equal(ob[k][e:e + 1], os_[k]), (e, k)
+    for hs in singles:
+        hs.close()
+    hb.close()
+
+
+def test_truncation_and_auto_reset(mev):
+    h = _handle(mev, max_steps=30)
+    rng = np.random.default_rng(6)
+    st0 = h.get_state()
+    for t in range(30):
+        o = h.step(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32), auto_reset=True)
+    assert o["truncated"].all() and (o["step"] == 30).all()
+    o = h.step(np.zeros((E, N, 2), np.float32), auto_reset=True)
+    assert (o["step"] == 1).all() and not o["truncated"].any()
+    st = h.get_state()
+    # the step after an auto-reset starts from the spawn poses
+    assert np.array_equal(st["spawn_x"], st0["spawn_x"])
+    h.close()
+
+
+def test_output_invariants(mev):
+    h = _handle(mev)
+    rng = np.random.default_rng(7)
+    for t in range(120):
+        o = h.step(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32), auto_reset=True)
+    obs = o["obs"]
+    assert np.isfinite(obs).all()
+    lid = obs[..., 31:]
+    assert (lid >= 0).all() and (lid <= 1.0000001).all()
+    # LiDAR distances are multiples of the 4 px step (or max_dist)
+    d = np.rint(lid * 250.0)
+    assert (np.isclose(lid * 250.0, d, atol=1e-3)).all()
+    assert ((d % 4 == 0) | (d == 250)).all()
+    assert set(np.unique(o["status"]).tolist()) <= {0, 2, 3, 4, 5}
+    assert np.array_equal(o["done"] == 1, o["status"] != 0)
+    assert (o["agents_alive"] == N).all()
+    h.close()
+
+
+def test_traffic_full_size_philox_spawns(mev):
+    h = mev.Handle(num_envs=E, num_agents=1, lidar_rays=R, traffic_flow=1, traffic_density=0.5, max_npcs=32)
+    rng = np.random.default_rng(8)
+    counts = []
+    for t in range(240):
+        h.step(rng.uniform(-1, 1, (E, 1, 2)).astype(np.float32), auto_reset=True)
+        if t % 40 == 39:
+            counts.append(h.get_state()["npc_count"].copy())
+    c = np.stack(counts)
+    assert c.max() <= 32 and c.mean() > 0.3
+    # spawn attempts follow p = 1 - exp(-0.5/60) per env-step: after 240 steps about
+    # 240 * 0.00830 ~ 2 attempts per env, most of them accepted
+    assert 0.5 < c[-1].mean() < 3.0
+    assert h.npc_overflow() == 0
+    h.close()
