@@ -127,6 +127,21 @@ int mev_set_stream(mev_handle* h, void* stream);
 int mev_use_own_stream(mev_handle* h);
 int mev_sync(mev_handle* h);
 
+/* Runtime reconfiguration, effective from the next step: reference
+ * IntersectionEnv::configure / configure_traffic (cpp/IntersectionEnv.cpp:50-60)
+ * and writes to its reward_config (env.py:57-77, cpp/Reward.h:5-14). */
+int mev_configure(mev_handle* h, int32_t use_team, int32_t respawn, int32_t max_steps);
+int mev_configure_traffic(mev_handle* h, int32_t enabled, float density);
+int mev_set_reward(mev_handle* h, const float* reward8);
+
+/* Host-side single-car helpers with the reference's exact arithmetic, for API
+ * parity with the bound MARLEnv.Car methods (cpp/bindings.cpp:24-25); they do
+ * not touch any device.  kin = {x, y, v, heading, acc, steering_angle}
+ * (Car::update, cpp/Car.cpp:9-40); box = {x, y, heading, length, width}
+ * (Car::check_collision, cpp/Car.cpp:86-141). */
+int mev_car_update(float* kin, float throttle, float steer_input, float dt);
+int mev_car_check_collision(const float* box_a, const float* box_b, int32_t* collide);
+
 /* Lane points / routes (reference cpp/RouteGen.cpp). */
 int mev_num_points(const mev_handle* h, int32_t* n);
 int mev_point_xy(const mev_handle* h, int32_t point, float* xy);

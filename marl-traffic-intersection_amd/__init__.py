@@ -6,5 +6,9 @@ a C ABI, include/marlenv.h).  Python only marshals buffers.
 """
 from . import _capi  # noqa: F401
 from ._capi import Handle, MevError, STATUS_NAMES, device_count, lib_available, load_library  # noqa: F401
+from . import utils, cpp_backend, env, vec_env  # noqa: F401,E402
+from .env import IntersectionEnv  # noqa: F401,E402
+from .vec_env import VecIntersectionEnv  # noqa: F401,E402
 
-__all__ = ["Handle", "MevError", "STATUS_NAMES", "device_count", "lib_available", "load_library"]
+__all__ = ["Handle", "MevError", "STATUS_NAMES", "device_count", "lib_available", "load_library",
+           "IntersectionEnv", "VecIntersectionEnv", "cpp_backend", "env", "vec_env", "utils"]

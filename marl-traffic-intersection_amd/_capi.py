@@ -31,6 +31,7 @@ EXPORTED = (
     "mev_route_id", "mev_route_info", "mev_path_len", "mev_set_ego_routes", "mev_set_traffic_routes",
     "mev_default_traffic_routes", "mev_reset", "mev_step", "mev_get_outputs", "mev_get_state", "mev_set_state",
     "mev_device_outputs", "mev_npc_overflow", "mev_use_own_stream", "mev_debug_stamps",
+    "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
 )
 
 
@@ -123,6 +124,11 @@ def load_library(variant: str = None):
     L.mev_device_count.argtypes = [i32p]
     L.mev_use_own_stream.argtypes = [_vp]
     L.mev_debug_stamps.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.mev_configure.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+    L.mev_configure_traffic.argtypes = [_vp, ctypes.c_int32, ctypes.c_float]
+    L.mev_set_reward.argtypes = [_vp, f32p]
+    L.mev_car_update.argtypes = [f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+    L.mev_car_check_collision.argtypes = [f32p, f32p, i32p]
     _libs[variant] = L
     return L
 
@@ -332,10 +338,42 @@ class Handle:
                 setattr(st, name, _ptr(a))
         _check(self._lib.mev_set_state(self._h, ctypes.byref(st)))
 
+    def configure(self, use_team: bool, respawn: bool, max_steps: int):
+        _check(self._lib.mev_configure(self._h, int(use_team), int(respawn), int(max_steps)))
+        self.config.update(use_team_reward=int(use_team), respawn_enabled=int(respawn), max_steps=int(max_steps))
+
+    def configure_traffic(self, enabled: bool, density: float):
+        _check(self._lib.mev_configure_traffic(self._h, int(enabled), float(density)))
+        self.config.update(traffic_flow=int(enabled), traffic_density=max(0.0, float(density)))
+
+    def set_reward(self, reward):
+        rc = np.ascontiguousarray(reward, np.float32)
+        assert rc.size == 8
+        _check(self._lib.mev_set_reward(self._h, rc.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+        self.config["reward"] = [float(x) for x in rc]
+
     def npc_overflow(self) -> int:
         v = ctypes.c_int64()
         _check(self._lib.mev_npc_overflow(self._h, ctypes.byref(v)))
         return v.value
+
+
+def car_update(kin, throttle: float, steer: float, dt: float):
+    """Host Car::update with the reference's exact arithmetic; kin = [x, y, v, heading, acc, steering]."""
+    k = np.ascontiguousarray(kin, np.float32).copy()
+    _check(load_library().mev_car_update(k.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), float(throttle),
+                                         float(steer), float(dt)))
+    return k
+
+
+def car_check_collision(box_a, box_b) -> bool:
+    """Host Car::check_collision; box = [x, y, heading, length, width]."""
+    a = np.ascontiguousarray(box_a, np.float32)
+    b = np.ascontiguousarray(box_b, np.float32)
+    r = ctypes.c_int32()
+    _check(load_library().mev_car_check_collision(a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                  b.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(r)))
+    return bool(r.value)
 
 
 def device_count() -> int:

@@ -1,0 +1,521 @@
+"""Drop-in for the reference's backend module (reference cpp_backend.py:30-66,
+which lazily imports the pybind11 module MARLEnv, cpp/bindings.cpp:11-95).
+
+The classes keep MARLEnv's names, attributes and methods (State, Car,
+RewardConfig, StepResult, EnvState, Lidar, IntersectionEnv), but the
+simulation runs in libmarlenv_hip.so on the GPU: one IntersectionEnv here is a
+device handle holding ONE env (E = 1) whose N = number of added cars.  There
+is no CPU simulator behind these classes — without the HIP library and a GPU,
+creating the environment raises.
+
+Deviations from MARLEnv (all outside the hot path):
+ * configure_routes validates lane names immediately (MARLEnv fails later,
+   inside step, on an unknown end lane; an unknown start lane never spawns);
+ * all cars share one LiDAR configuration (MARLEnv keeps one Lidar per car);
+   assigning `lidars` reconfigures every car;
+ * Car.length / Car.width are honoured by Car.check_collision but the
+   environment simulates the reference's fixed 54 x 24 px cars;
+ * observations after set_state() / mid-episode add_car_with_route() carry a
+   fresh LiDAR block (max range), exactly as after reset.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _capi
+from .utils import point_index, point_name
+
+STATUS = _capi.STATUS_NAMES
+DEFAULT_LIDAR = (96, 360.0, 250.0, 4.0)  # IntersectionEnv.cpp:113-116
+CTOR_LIDAR = (72, 360.0, 250.0, 4.0)     # Lidar() defaults, Lidar.h:11-14 (used by set_state)
+OBS_W = 127
+
+
+def has_cpp_backend() -> bool:
+    """True when the gfx950 library is present (reference cpp_backend.py:38-39)."""
+    return _capi.lib_available()
+
+
+class State:
+    """reference cpp/Car.h:9-14"""
+
+    __slots__ = ("x", "y", "v", "heading")
+
+    def __init__(self, x: float = 0.0, y: float = 0.0, v: float = 0.0, heading: float = 0.0):
+        self.x, self.y, self.v, self.heading = float(x), float(y), float(v), float(heading)
+
+    def __repr__(self):
+        return f"State(x={self.x:.3f}, y={self.y:.3f}, v={self.v:.3f}, heading={self.heading:.4f})"
+
+
+class Car:
+    """reference cpp/Car.h:16-46 (bound fields + the hidden ones, for state round trips)."""
+
+    def __init__(self):
+        self.state = State()
+        self.length = 54.0
+        self.width = 24.0
+        self.alive = True
+        self.intention = 0
+        self.path: List[Tuple[float, float]] = []
+        self.path_index = 0
+        self.acc = 0.0
+        self.steering_angle = 0.0
+        self.spawn_state = State()
+        self.prev_dist_to_goal = 0.0
+        self.prev_action = (0.0, 0.0)
+        self._route = -1
+
+    def update(self, throttle: float, steer_input: float, dt: float):
+        """Car::update (cpp/Car.cpp:9-40), same float arithmetic (host C helper)."""
+        k = _capi.car_update([self.state.x, self.state.y, self.state.v, self.state.heading, self.acc,
+                              self.steering_angle], throttle, steer_input, dt)
+        self.state.x, self.state.y, self.state.v, self.state.heading = (float(k[0]), float(k[1]), float(k[2]),
+                                                                        float(k[3]))
+        self.acc, self.steering_angle = float(k[4]), float(k[5])
+
+    def check_collision(self, other: "Car") -> bool:
+        """Car::check_collision (cpp/Car.cpp:117-141), SAT on the oriented boxes."""
+        a = [self.state.x, self.state.y, self.state.heading, self.length, self.width]
+        b = [other.state.x, other.state.y, other.state.heading, other.length, other.width]
+        return _capi.car_check_collision(a, b)
+
+    def __repr__(self):
+        return f"Car({self.state!r}, alive={self.alive}, intention={self.intention}, path_index={self.path_index})"
+
+
+class RewardConfig:
+    """reference cpp/Reward.h:5-14; writes go straight to the owning environment
+    (as MARLEnv's by-reference property does, which env.py:57-77 relies on)."""
+
+    _FIELDS = ("k_prog", "v_min_ms", "k_stuck", "k_cv", "k_co", "k_succ", "k_sm", "alpha")
+
+    def __init__(self):
+        object.__setattr__(self, "_owner", None)
+        for k, v in zip(self._FIELDS, (10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2)):
+            object.__setattr__(self, k, float(v))
+
+    def __setattr__(self, name, value):
+        if name not in self._FIELDS:
+            raise AttributeError(name)
+        object.__setattr__(self, name, float(value))
+        if self._owner is not None:
+            self._owner._reward_dirty = True
+
+    def as_list(self) -> List[float]:
+        return [getattr(self, k) for k in self._FIELDS]
+
+    def __repr__(self):
+        return "RewardConfig(" + ", ".join(f"{k}={getattr(self, k)}" for k in self._FIELDS) + ")"
+
+
+class StepResult:
+    """reference cpp/Reward.h:16-29 (obs / rewards are float32 numpy arrays)."""
+
+    def __init__(self):
+        self.obs = np.zeros((0, OBS_W), np.float32)
+        self.rewards = np.zeros(0, np.float32)
+        self.done: List[int] = []
+        self.status: List[str] = []
+        self.agent_ids: List[int] = []
+        self.agents_alive = 0
+        self.terminated = False
+        self.truncated = False
+        self.step = 0
+
+
+class EnvState:
+    """reference cpp/EnvState.h:9-15"""
+
+    def __init__(self):
+        self.cars: List[Car] = []
+        self.traffic_cars: List[Car] = []
+        self.agent_ids: List[int] = []
+        self.next_agent_id = 1
+        self.step_count = 0
+
+
+class Lidar:
+    """reference cpp/Lidar.h:8-27 (defaults of Lidar(): 72 rays, 360 deg, 250 px, 4 px)."""
+
+    def __init__(self, rays: int = 72, fov_deg: float = 360.0, max_dist: float = 250.0, step_size: float = 4.0):
+        self.rays = int(rays)
+        self.fov_deg = float(fov_deg)
+        self.max_dist = float(max_dist)
+        self.step_size = float(step_size)
+        self.distances = [self.max_dist] * self.rays
+        self.rel_angles = _rel_angles(self.rays, self.fov_deg)
+
+    def normalized(self) -> List[float]:
+        """Lidar::normalized (cpp/Lidar.cpp:92-98): d * (1/max) in float32."""
+        inv = np.float32(1.0) / np.float32(self.max_dist) if self.max_dist > 0 else np.float32(0.0)
+        return (np.asarray(self.distances, np.float32) * inv).tolist()
+
+
+def _rel_angles(rays: int, fov: float) -> List[float]:
+    """Beam offsets in float32 exactly as cpp/Lidar.cpp:4-14."""
+    f32 = np.float32
+    start = f32(-fov) * f32(0.5)
+    step = f32(fov) / f32(rays - 1) if rays > 1 else f32(0.0)
+    pi = f32(math.pi)
+    return [float((start + f32(i) * step) * pi / f32(180.0)) for i in range(rays)]
+
+
+class IntersectionEnv:
+    """MARLEnv.IntersectionEnv (reference cpp/IntersectionEnv.h:23-105) on the GPU."""
+
+    def __init__(self, num_lanes: int = 3, device: int = 0, max_npcs: int = 64):
+        self.num_lanes = int(num_lanes)
+        self._device = int(device)
+        self._max_npcs = int(max_npcs)
+        self._use_team, self._respawn, self._max_steps = False, True, 2000
+        self._traffic, self._density = False, 0.5
+        self._reward = RewardConfig()
+        object.__setattr__(self._reward, "_owner", self)
+        self._reward_dirty = True
+        self._lidar = DEFAULT_LIDAR
+        self._h: Optional[_capi.Handle] = None
+        self._routes: List[int] = []     # ego route ids (add order)
+        self._agent_ids: List[int] = []
+        self._next_id = 1
+        self._fresh = True               # no step since reset: added cars start from spawn
+        self._pending: List[int] = []    # cars added since the last sync
+        self._traffic_routes: Optional[List[int]] = None  # None = reference default (init_traffic_routes)
+
+    # ------------------------------------------------------------ config
+    def configure(self, use_team: bool, respawn: bool, max_steps: int):
+        self._use_team, self._respawn, self._max_steps = bool(use_team), bool(respawn), int(max_steps)
+        if self._h is not None:
+            self._h.configure(self._use_team, self._respawn, self._max_steps)
+
+    def configure_traffic(self, enabled: bool, density: float):
+        self._traffic, self._density = bool(enabled), max(0.0, float(density))
+        if self._h is not None:
+            self._h.configure_traffic(self._traffic, self._density)
+
+    def configure_routes(self, routes: Sequence[Tuple[str, str]]):
+        ids = []
+        P = 8 * self.num_lanes
+        for s, e in routes:
+            si, ei = point_index(s, self.num_lanes), point_index(e, self.num_lanes)
+            if si < 0 or ei < 0:
+                raise IndexError(f"unknown lane id in route ({s!r}, {e!r})")
+            ids.append(si * P + ei)
+        self._traffic_routes = ids
+        if self._h is not None:
+            self._h.set_traffic_routes(ids)
+
+    @property
+    def reward_config(self) -> RewardConfig:
+        return self._reward
+
+    @reward_config.setter
+    def reward_config(self, rc: RewardConfig):
+        for k in RewardConfig._FIELDS:
+            setattr(self._reward, k, getattr(rc, k))
+
+    # ----------------------------------------------------------- episode
+    def reset(self):
+        """IntersectionEnv::reset (cpp/IntersectionEnv.cpp:66-76)."""
+        self._routes, self._agent_ids, self._pending = [], [], []
+        self._next_id = 1
+        self._fresh = True
+        self._lidar = DEFAULT_LIDAR  # add_car_with_route gives every new car a 96-ray Lidar
+
+    def add_car_with_route(self, start_id: str, end_id: str):
+        """cpp/IntersectionEnv.cpp:78-131: unknown start -> silently ignored; unknown end -> IndexError."""
+        si = point_index(start_id, self.num_lanes)
+        if si < 0:
+            return
+        ei = point_index(end_id, self.num_lanes)
+        if ei < 0:
+            raise IndexError(f"unknown lane id {end_id!r}")  # std::out_of_range from .at() (RouteGen.cpp:120)
+        r = si * 8 * self.num_lanes + ei
+        self._routes.append(r)
+        self._pending.append(r)
+        self._agent_ids.append(self._next_id)
+        self._next_id += 1
+
+    def _create(self, n: int, lidar):
+        return _capi.Handle(num_envs=1, num_agents=n, num_lanes=self.num_lanes, lidar_rays=lidar[0],
+                            lidar_fov_deg=lidar[1], lidar_max_dist=lidar[2], lidar_step=lidar[3], obs_dim=OBS_W,
+                            traffic_flow=int(self._traffic), traffic_density=self._density,
+                            use_team_reward=int(self._use_team), respawn_enabled=int(self._respawn),
+                            max_steps=self._max_steps, reward=self._reward.as_list(),
+                            max_npcs=self._max_npcs, device=self._device)
+
+    def _sync(self) -> Optional[_capi.Handle]:
+        n = len(self._routes)
+        if n == 0:
+            return None
+        h = self._h
+        if h is None or h.N != n or self._h_lidar != self._lidar:
+            keep = None
+            if h is not None and not self._fresh:
+                keep = h.get_state()  # cars added mid-episode keep the running episode
+            if h is not None:
+                h.close()
+            h = self._h = self._create(n, self._lidar)
+            self._h_lidar = self._lidar
+            self._reward_dirty = False
+            if self._traffic_routes is not None:
+                h.set_traffic_routes(self._traffic_routes)
+            h.set_ego_routes(np.asarray(self._routes, np.int32)[None])
+            h.reset()  # every car at the spawn of its route
+            if keep is not None:
+                self._restore_grown(keep)
+            self._pending = []
+            return h
+        if self._reward_dirty:
+            h.set_reward(self._reward.as_list())
+            self._reward_dirty = False
+        if self._pending:
+            h.set_ego_routes(np.asarray(self._routes, np.int32)[None])
+            if self._fresh:
+                h.reset()
+            self._pending = []
+        return h
+
+    def _restore_grown(self, old):
+        """Old cars keep their state; newly added ones start at their spawn (add_car_with_route)."""
+        h = self._h
+        new = h.get_state()  # after creation == a reset: every car at its spawn
+        m = old["x"].shape[1]
+        for k, v in old.items():
+            if k.startswith("npc_") or v.ndim == 1:
+                new[k] = v
+            else:
+                new[k][:, :m] = v
+        h.set_state(new)
+
+    @property
+    def step_count(self) -> int:
+        h = self._sync()
+        return int(h.get_state()["step_count"][0]) if h is not None else 0
+
+    @step_count.setter
+    def step_count(self, value: int):
+        h = self._sync()
+        if h is not None:
+            h.set_state({"step_count": np.array([int(value)], np.int32)})
+
+    def step(self, throttles: Sequence[float], steerings: Sequence[float], dt: float = 1.0 / 60.0) -> StepResult:
+        """IntersectionEnv::step (cpp/IntersectionEnv.cpp:133-392) on the GPU."""
+        h = self._sync()
+        res = StepResult()
+        if h is None:
+            return res
+        n = h.N
+        act = np.zeros((1, n, 2), np.float32)
+        t = np.asarray(throttles, np.float32).reshape(-1)[:n]
+        s = np.asarray(steerings, np.float32).reshape(-1)[:n]
+        act[0, : len(t), 0] = t
+        act[0, : len(s), 1] = s
+        out = h.step(act, float(dt))
+        self._fresh = False
+        res.obs = out["obs"][0]
+        res.rewards = out["reward"][0]
+        res.done = [int(x) for x in out["done"][0]]
+        res.status = [STATUS[int(x)] for x in out["status"][0]]
+        res.agent_ids = list(self._agent_ids)
+        res.agents_alive = int(out["agents_alive"][0])
+        res.terminated = bool(out["terminated"][0])
+        res.truncated = bool(out["truncated"][0])
+        res.step = int(out["step"][0])
+        return res
+
+    def get_observations(self) -> np.ndarray:
+        """get_observations (cpp/IntersectionEnv.cpp:418-520): float32 [n, 127]."""
+        h = self._sync()
+        if h is None:
+            return np.zeros((0, OBS_W), np.float32)
+        return h.observations()[0]
+
+    # ----------------------------------------------------------- cars
+    def _cars_from(self, st, ego: bool) -> List[Car]:
+        out = []
+        h = self._h
+        if ego:
+            n = h.N
+            get = lambda k, i: st[k][0, i]  # noqa: E731
+            count = n
+        else:
+            count = int(st["npc_count"][0])
+            get = lambda k, i: st["npc_" + k][0, i]  # noqa: E731
+        for i in range(count):
+            c = Car()
+            c.state = State(get("x", i), get("y", i), get("v", i), get("heading", i))
+            c.acc, c.steering_angle = float(get("acc", i)), float(get("steering", i))
+            c.alive = bool(get("alive", i))
+            c.intention = int(get("intention", i))
+            c.path_index = int(get("path_index", i))
+            c._route = int(get("route", i))
+            c.path = [tuple(map(float, p)) for p in h.route_info(c._route)[0]]
+            if ego:
+                c.spawn_state = State(st["spawn_x"][0, i], st["spawn_y"][0, i], st["spawn_v"][0, i],
+                                      st["spawn_heading"][0, i])
+                c.prev_dist_to_goal = float(st["prev_dist"][0, i])
+                c.prev_action = (float(st["prev_a0"][0, i]), float(st["prev_a1"][0, i]))
+            else:
+                c.spawn_state = State(c.path[0][0], c.path[0][1], 0.0,
+                                      math.atan2(-(c.path[1][1] - c.path[0][1]), c.path[1][0] - c.path[0][0]))
+            out.append(c)
+        return out
+
+    @property
+    def cars(self) -> List[Car]:
+        h = self._sync()
+        return [] if h is None else self._cars_from(h.get_state(), True)
+
+    @property
+    def traffic_cars(self) -> List[Car]:
+        h = self._sync()
+        return [] if h is None else self._cars_from(h.get_state(), False)
+
+    @property
+    def lidars(self) -> List[Lidar]:
+        """One Lidar per car; distances recovered exactly from the observation
+        (every distance is max_dist or a probe distance k*step)."""
+        h = self._sync()
+        if h is None:
+            return []
+        rays, fov, maxd, stp = self._lidar
+        obs = h.observations()[0][:, 31:31 + min(rays, OBS_W - 31)]
+        out = []
+        inv = np.float32(1.0) / np.float32(maxd)
+        for row in obs:
+            l_ = Lidar(rays, fov, maxd, stp)
+            k = np.rint(row.astype(np.float64) * maxd / stp)
+            cand = (k * stp).astype(np.float32)
+            ok = (cand * inv) == row
+            d = np.where(ok, cand, np.float32(maxd))
+            l_.distances = d.tolist() + [maxd] * (rays - len(d))
+            out.append(l_)
+        return out
+
+    @lidars.setter
+    def lidars(self, lidars: Sequence[Lidar]):
+        if not lidars:
+            return
+        cfg = {(l_.rays, l_.fov_deg, l_.max_dist, l_.step_size) for l_ in lidars}
+        if len(cfg) != 1:
+            raise ValueError("all cars must share one LiDAR configuration")
+        self._set_lidar(cfg.pop())
+
+    def _set_lidar(self, lidar):
+        lidar = (int(lidar[0]), float(lidar[1]), float(lidar[2]), float(lidar[3]))
+        if lidar == self._lidar:
+            return
+        if self._h is not None and len(self._routes) == self._h.N:
+            st = self._h.get_state()
+            self._h.close()
+            self._h = self._create(len(self._routes), lidar)
+            if self._traffic_routes is not None:
+                self._h.set_traffic_routes(self._traffic_routes)
+            self._h.set_ego_routes(np.asarray(self._routes, np.int32)[None])
+            self._h.set_state(st)
+            self._h_lidar = lidar
+        self._lidar = lidar
+
+    # ---------------------------------------------------------- snapshot
+    def get_state(self) -> EnvState:
+        """cpp/IntersectionEnv.cpp:394-404"""
+        s = EnvState()
+        h = self._sync()
+        if h is not None:
+            st = h.get_state()
+            s.cars = self._cars_from(st, True)
+            s.traffic_cars = self._cars_from(st, False)
+            s.step_count = int(st["step_count"][0])
+        s.agent_ids = list(self._agent_ids)
+        s.next_agent_id = self._next_id
+        return s
+
+    def _route_of(self, c: Car) -> int:
+        if c._route >= 0:
+            return c._route
+        if len(c.path) >= 2:
+            want = np.asarray(c.path, np.float32)
+            P = 8 * self.num_lanes
+            for r in range(P * P):  # a path built from the lane layout: find its route
+                path = self._h.route_info(r)[0]
+                if path.shape == want.shape and np.array_equal(path, want):
+                    return r
+        raise ValueError("Car.path must be one of the lane-layout routes")
+
+    def set_state(self, s: EnvState):
+        """cpp/IntersectionEnv.cpp:406-416; like the reference, the LiDAR objects
+        are rebuilt with Lidar() defaults (72 rays) from here on."""
+        n = len(s.cars)
+        self._agent_ids = list(s.agent_ids)
+        self._next_id = int(s.next_agent_id)
+        if n == 0:
+            self._routes = []
+            return
+        if self._h is None or self._h.N != n or self._h_lidar != CTOR_LIDAR:
+            if self._h is not None:
+                self._h.close()
+            self._h = self._create(n, CTOR_LIDAR)
+            self._h_lidar = CTOR_LIDAR
+        routes = [self._route_of(c) for c in s.cars]
+        self._routes = routes
+        self._lidar = CTOR_LIDAR
+        if self._traffic_routes is not None:
+            self._h.set_traffic_routes(self._traffic_routes)
+        self._h.set_ego_routes(np.asarray(routes, np.int32)[None])
+        st = self._h.get_state()
+        for i, c in enumerate(s.cars):
+            st["x"][0, i], st["y"][0, i], st["v"][0, i], st["heading"][0, i] = (c.state.x, c.state.y, c.state.v,
+                                                                                 c.state.heading)
+            st["acc"][0, i], st["steering"][0, i] = c.acc, c.steering_angle
+            st["spawn_x"][0, i], st["spawn_y"][0, i] = c.spawn_state.x, c.spawn_state.y
+            st["spawn_v"][0, i], st["spawn_heading"][0, i] = c.spawn_state.v, c.spawn_state.heading
+            st["prev_dist"][0, i] = c.prev_dist_to_goal
+            st["prev_a0"][0, i], st["prev_a1"][0, i] = c.prev_action
+            st["path_index"][0, i], st["intention"][0, i] = c.path_index, c.intention
+            st["alive"][0, i] = int(bool(c.alive))
+            st["route"][0, i] = routes[i]
+        k = len(s.traffic_cars)
+        if k > self._h.K:
+            raise ValueError(f"{k} traffic cars exceed max_npcs={self._h.K}")
+        for j, c in enumerate(s.traffic_cars):
+            st["npc_x"][0, j], st["npc_y"][0, j], st["npc_v"][0, j] = c.state.x, c.state.y, c.state.v
+            st["npc_heading"][0, j], st["npc_acc"][0, j], st["npc_steering"][0, j] = (c.state.heading, c.acc,
+                                                                                      c.steering_angle)
+            st["npc_path_index"][0, j], st["npc_intention"][0, j] = c.path_index, c.intention
+            st["npc_alive"][0, j] = int(bool(c.alive))
+            st["npc_route"][0, j] = self._route_of(c)
+        st["npc_count"][0] = k
+        st["step_count"][0] = int(s.step_count)
+        self._h.set_state(st)
+        self._fresh = False
+        self._pending = []
+
+    # ---------------------------------------------- renderer (out of scope)
+    def render(self, show_lane_ids: bool = False, show_lidar: bool = False):
+        """The reference renderer is Windows/GLFW-only (Renderer.h:8-10); not provided."""
+        return None
+
+    def window_should_close(self) -> bool:
+        return True
+
+    def poll_events(self):
+        return None
+
+    def key_pressed(self, glfw_key: int) -> bool:
+        return False
+
+    def close(self):
+        if self._h is not None:
+            self._h.close()
+            self._h = None
+
+
+# reference cpp_backend.py factories
+def _require():
+    if not has_cpp_backend():
+        raise RuntimeError("libmarlenv_hip.so is not built: run python -c 'import __graft_entry__ as g; g.build()'")
+    return True

@@ -325,6 +325,64 @@ int mev_sync(mev_handle* h) {
     return MEV_OK;
 }
 
+int mev_configure(mev_handle* h, int32_t use_team, int32_t respawn, int32_t max_steps) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    h->cfg.use_team_reward = use_team;
+    h->cfg.respawn_enabled = respawn;
+    h->cfg.max_steps = max_steps;
+    h->sp.use_team = use_team;
+    h->sp.respawn = respawn;
+    h->sp.max_steps = max_steps;
+    return MEV_OK;
+}
+
+int mev_configure_traffic(mev_handle* h, int32_t enabled, float density) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (enabled && h->cfg.max_npcs == 0) return fail(MEV_E_INVALID, "traffic needs max_npcs > 0 (set at creation)");
+    h->cfg.traffic_flow = enabled;
+    h->cfg.traffic_density = density < 0.0f ? 0.0f : density;  // configure_traffic clamps (:56-60)
+    h->sp.traffic = enabled;
+    return MEV_OK;
+}
+
+int mev_set_reward(mev_handle* h, const float* rc) {
+    if (!h || !rc) return fail(MEV_E_INVALID, "null argument");
+    memcpy(h->cfg.reward, rc, sizeof(h->cfg.reward));
+    mev::SimParams& p = h->sp;
+    p.k_prog = rc[0]; p.v_min = rc[1]; p.k_stuck = rc[2]; p.k_cv = rc[3];
+    p.k_co = rc[4]; p.k_succ = rc[5]; p.k_sm = rc[6]; p.alpha = rc[7];
+    return MEV_OK;
+}
+
+int mev_car_update(float* kin, float throttle, float steer_input, float dt) {
+    if (!kin) return fail(MEV_E_INVALID, "null argument");
+    mev::Kin k{kin[0], kin[1], kin[2], kin[3], kin[4], kin[5]};
+    float c, s;
+    mev::car_update(k, throttle, steer_input, dt, &c, &s);
+    kin[0] = k.x; kin[1] = k.y; kin[2] = k.v; kin[3] = k.h; kin[4] = k.acc; kin[5] = k.steer;
+    return MEV_OK;
+}
+
+static void box_corners(const float* b, float* cx, float* cy, float* c, float* s) {
+    // Car::corners (cpp/Car.cpp:86-103) with the car's own length/width
+    mev::sincosf(b[2], s, c);
+    const float hx = b[4] * 0.5f, hy = b[3] * 0.5f;
+    const float lx[4] = {hy, hy, -hy, -hy}, ly[4] = {hx, -hx, -hx, hx};
+    for (int k = 0; k < 4; ++k) {
+        cx[k] = b[0] + lx[k] * *c - ly[k] * *s;
+        cy[k] = b[1] + lx[k] * *s + ly[k] * *c;
+    }
+}
+
+int mev_car_check_collision(const float* a, const float* b, int32_t* collide) {
+    if (!a || !b || !collide) return fail(MEV_E_INVALID, "null argument");
+    float ax[4], ay[4], bx[4], by[4], ca, sa, cb, sb;
+    box_corners(a, ax, ay, &ca, &sa);
+    box_corners(b, bx, by, &cb, &sb);
+    *collide = mev::sat_collide(ax, ay, ca, sa, bx, by, cb, sb) ? 1 : 0;
+    return MEV_OK;
+}
+
 int mev_num_points(const mev_handle* h, int32_t* n) {
     if (!h || !n) return fail(MEV_E_INVALID, "null argument");
     *n = h->P;
