@@ -2,17 +2,23 @@
 
 Workload (BASELINE.json metric, config 3): per GPU 4096 envs x 8 ego agents,
 64-beam LiDAR, team reward, respawn on, max_steps 2000, per-env auto-reset.
-One "step" = one fused gfx950 step kernel over the GPU's 4096 envs with the
-actions already resident in HBM (pre-generated uniform [-1, 1) f32), writing
-obs [E, 8, 95] / reward / done / status / terminated / truncated to HBM.
-With --gpus N > 1 (one process per GPU, torchrun) every rank steps its own
-4096 envs (weak scaling: envs are independent, no data-path collective inside
-a step) and the stacked outputs of each step are gathered to rank 0 with one
-RCCL gather over xGMI, overlapped with the next step (double-buffered).
+One "step" = IntersectionEnv::step + get_observations for all of the GPU's
+4096 envs: the k_cars kernel (one wave per env: physics, status, collisions,
+rewards, respawn, observation head) followed by k_lidar (one wave per agent:
+the 64-beam march), with the actions already resident in HBM (pre-generated
+uniform [-1, 1) f32) and obs [E, 8, 95] / reward / done / status /
+terminated / truncated written to HBM.
 
-Prints ONE JSON line on rank 0 (contract in the task statement), including
-"roofline" (dominant kernel, HBM-bound accounting) and "cpu_baseline" (the
-reference C++ simulator timed on this host's cores).
+--gpus N > 1 (one process per GPU, torchrun): every rank steps its own 4096
+envs (weak scaling: envs are independent, no data-path collective inside a
+step) and each step's packed outputs are gathered to rank 0 with one RCCL
+gather over xGMI (sharding.py), overlapped with the next step (double
+buffered).
+
+Prints ONE JSON line on rank 0, including "roofline" for the dominant kernel
+(k_lidar; device durations from HIP events the library records on its stream
+around each kernel during the timed region) and "cpu_baseline" (the
+reference's own C++ simulator, compiled from its sources, on this host).
 """
 from __future__ import annotations
 
@@ -34,13 +40,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
 def algorithmic_bytes_per_agent_step(rays: int) -> int:
-    # actions 8 + ego hot state r/w 80 + obs 4*(31+R) + reward 4 + done/status 2
+    """actions 8 + ego hot state r/w 80 + obs 4*(31+R) + reward 4 + done/status 2."""
     return 8 + 80 + 4 * (31 + rays) + 4 + 2
 
 
+def lidar_bytes_per_agent_step(rays: int) -> int:
+    """k_lidar's share: reads the ego pose x, y, heading (12 B) and alive (1 B), writes obs[31:31+R] (4R B)."""
+    return 13 + 4 * rays
+
+
+def cars_bytes_per_agent_step(rays: int) -> int:
+    """k_cars's share: actions 8 + hot state r/w 80 + obs head 4*31 + reward 4 + done/status 2."""
+    return 8 + 80 + 4 * 31 + 4 + 2
+
+
 def cpu_baseline(seconds_budget: float = 20.0):
-    """Reference C++ (oracle/_ref, built from the reference's own sources) on
-    this host: `threads` workers x 1 env x `steps` steps of the same workload."""
+    """The reference's C++ simulator (oracle/_ref: its unmodified sources compiled
+    with g++ -O2 by oracle/build_ref.sh) on this host's cores; falls back to the
+    C restatement (oracle/marl_oracle.c, single thread) when _ref is absent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import refharness
@@ -54,7 +71,12 @@ def cpu_baseline(seconds_budget: float = 20.0):
         return {"value": round(v, 1), "unit": "agent-steps/s", "cores": threads, "kind": "reference",
                 "sample": f"reference cpp/ simulator (unmodified sources, g++ -O2), {threads} threads x 1 env x "
                           f"{steps} steps, 8 agents, 64 beams, team reward, uniform random actions, auto-reset"}
-    return None
+    import oracle
+    steps = int(seconds_budget / 1.2e-3)
+    v = oracle.bench(N_AGENTS, RAYS, True, steps, 0)
+    return {"value": round(v, 1), "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"C restatement (oracle/marl_oracle.c, gcc -O2), 1 thread x 1 env x {steps} steps, 8 agents, "
+                      f"64 beams, team reward, uniform random actions, auto-reset"}
 
 
 def main():
@@ -64,6 +86,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--envs", type=int, default=E_PER_GPU, help="envs per GPU")
     ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL gather to rank 0")
+    ap.add_argument("--no-kernel-events", action="store_true", help="do not record per-kernel HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -71,26 +94,25 @@ def main():
     import pkgload
 
     mev = pkgload.load()
+    from marl_traffic_intersection_amd import sharding
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
+    torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     E, N, D = args.envs, N_AGENTS, OBS_DIM
     K, W = args.steps, args.warmup
 
     env = mev.Handle(num_envs=E, num_agents=N, lidar_rays=RAYS, use_team_reward=1, respawn_enabled=1,
                      max_steps=2000, seed=rank, device=local_rank)
-    stream = torch.cuda.Stream(dev)  # the env kernel, the events and the gather are all ordered on it
+    stream = torch.cuda.Stream(dev)  # the env kernels, the events and the gather are all ordered on it
     torch.cuda.set_stream(stream)
     env.set_stream(stream.cuda_stream)
 
@@ -98,49 +120,37 @@ def main():
     g.manual_seed(1234 + rank)
     actions = torch.rand((W + K, E, N, 2), device=dev, generator=g, dtype=torch.float32) * 2.0 - 1.0
 
-    # packed per-step output buffer: obs f32 | reward f32 | done u8 | status u8 | term u8 | trunc u8
-    n_obs, n_rew = E * N * D * 4, E * N * 4
-    n_flags = 2 * E * N + 2 * E
-    nbytes = (n_obs + n_rew + n_flags + 255) // 256 * 256
-    bufs = [torch.zeros(nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-
-    def views(b):
-        base = b.data_ptr()
-        return dict(obs=base, reward=base + n_obs, done=base + n_obs + n_rew, status=base + n_obs + n_rew + E * N,
-                    terminated=base + n_obs + n_rew + 2 * E * N, truncated=base + n_obs + n_rew + 2 * E * N + E)
-
-    views_ = [views(b) for b in bufs]
+    layout = sharding.PackedOutputs(E, N, D)  # every rank steps E envs: the gather needs no padding
+    bufs = [torch.zeros(layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+    ptrs = [layout.pointers(b.data_ptr()) for b in bufs]
     gather_on = world > 1 and not args.no_gather
-    stacked = None
-    if gather_on and rank == 0:
-        stacked = torch.empty((world, nbytes), dtype=torch.uint8, device=dev)
+    stacked = torch.empty((world, layout.nbytes), dtype=torch.uint8, device=dev) if gather_on and rank == 0 else None
     works = [None, None]
     env.reset(device=True)
 
-    def step(t, timed_events=None):
+    def step(t):
         slot = t & 1
         if works[slot] is not None:
             works[slot].wait()  # stream-ordered: the gather reading this buffer is done
             works[slot] = None
-        if timed_events is not None:
-            timed_events[0].record(stream)
-        env.step(actions[t].data_ptr(), 1.0 / 60.0, out=views_[slot], auto_reset=True, device=True)
-        if timed_events is not None:
-            timed_events[1].record(stream)
+        env.step(actions[t].data_ptr(), 1.0 / 60.0, out=ptrs[slot], auto_reset=True, device=True)
         if gather_on:
-            gl = list(stacked.unbind(0)) if rank == 0 else None
-            works[slot] = dist.gather(bufs[slot], gather_list=gl, dst=0, async_op=True)
+            works[slot] = sharding.gather_to_root(bufs[slot], stacked, async_op=True)
 
     for t in range(W):
         step(t)
     torch.cuda.synchronize(dev)
+    if not args.no_kernel_events:
+        env.kernel_timing(True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for k in range(K):
-        step(W + k, evs[k])
+        step(W + k)
+    ev1.record(stream)
     for w in works:
         if w is not None:
             w.wait()
@@ -149,34 +159,51 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / K
+    stream_ms = ev0.elapsed_time(ev1) / K
+    cars_ms = lidar_ms = None
+    if not args.no_kernel_events:
+        c_sum, l_sum, n_steps = env.kernel_times()
+        assert n_steps == K, (n_steps, K)
+        cars_ms, lidar_ms = c_sum / K, l_sum / K
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        kk = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(kk, op=dist.ReduceOp.MAX)
-        kern_ms = float(kk.item())
+        vals = torch.tensor([elapsed, cars_ms or 0.0, lidar_ms or 0.0, stream_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        elapsed, c_, l_, stream_ms = (float(x) for x in vals.tolist())
+        if cars_ms is not None:
+            cars_ms, lidar_ms = c_, l_
 
     # sanity: outputs are finite and the sim advanced
-    o = bufs[(W + K - 1) & 1][: n_obs].view(torch.float32)
-    assert torch.isfinite(o).all().item(), "non-finite observations"
+    last = layout.unpack(bufs[(W + K - 1) & 1])
+    assert torch.isfinite(last["obs"]).all().item(), "non-finite observations"
 
     if rank == 0:
         total_agent_steps = world * E * N * K
         value = total_agent_steps / elapsed
-        bpa = algorithmic_bytes_per_agent_step(RAYS)
-        bytes_per_launch = E * N * bpa
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic = None
-        pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_file):
-            try:
-                pm = json.load(open(pmc_file))
-                if pm.get("envs") == E and pm.get("agents") == N and pm.get("rays") == RAYS:
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        roofline = None
+        if lidar_ms is not None:
+            lb = lidar_bytes_per_agent_step(RAYS) * E * N
+            pb = algorithmic_bytes_per_agent_step(RAYS) * E * N
+            achieved = lb / (lidar_ms * 1e-3) / 1e9
+            traffic = None
+            pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc_file):
+                try:
+                    pm = json.load(open(pmc_file))
+                    if pm.get("envs") == E and pm.get("agents") == N and pm.get("rays") == RAYS:
+                        traffic = pm.get("k_lidar", {}).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roofline = {
+                "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                "kernel": "k_lidar<true>", "kernel_ms": round(lidar_ms, 5),
+                "algorithmic_bytes_per_agent_step": lidar_bytes_per_agent_step(RAYS), "bytes_per_launch": lb,
+                "other_kernels": {"k_cars<false>": {"kernel_ms": round(cars_ms, 5),
+                                                    "algorithmic_bytes_per_agent_step": cars_bytes_per_agent_step(RAYS)}},
+                "step_pipeline": {"kernels_ms": round(cars_ms + lidar_ms, 5), "stream_ms_per_step": round(stream_ms, 5),
+                                  "algorithmic_bytes_per_agent_step": algorithmic_bytes_per_agent_step(RAYS),
+                                  "achieved_GBs": round(pb / ((cars_ms + lidar_ms) * 1e-3) / 1e9, 3)},
+            }
         res = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -194,10 +221,7 @@ def main():
                                    f"respawn on, max_steps 2000, per-env auto-reset",
                        "envs_per_gpu": E, "agents": N, "rays": RAYS, "obs_dim": D,
                        "parallelism": f"env-sharded x{world}" + (" + RCCL gather to rank 0 per step" if gather_on else "")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "kernel": "k_step<false>", "kernel_ms": round(kern_ms, 5),
-                         "algorithmic_bytes_per_agent_step": bpa, "bytes_per_launch": bytes_per_launch},
+            "roofline": roofline,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

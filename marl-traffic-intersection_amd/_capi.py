@@ -32,6 +32,7 @@ EXPORTED = (
     "mev_default_traffic_routes", "mev_reset", "mev_step", "mev_get_outputs", "mev_get_state", "mev_set_state",
     "mev_device_outputs", "mev_npc_overflow", "mev_use_own_stream", "mev_debug_stamps",
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
+    "mev_kernel_timing", "mev_kernel_times",
 )
 
 
@@ -124,6 +125,9 @@ def load_library(variant: str = None):
     L.mev_device_count.argtypes = [i32p]
     L.mev_use_own_stream.argtypes = [_vp]
     L.mev_debug_stamps.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.mev_kernel_timing.argtypes = [_vp, ctypes.c_int32]
+    L.mev_kernel_times.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_int64)]
     L.mev_configure.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.mev_configure_traffic.argtypes = [_vp, ctypes.c_int32, ctypes.c_float]
     L.mev_set_reward.argtypes = [_vp, f32p]
@@ -160,6 +164,34 @@ def _ptr(a) -> Optional[int]:
     return int(a)
 
 
+_torch_first_done = False
+
+
+def _torch_runtime_first():
+    """PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so, no
+    soname), distinct from the /opt/rocm libamdhip64.so.7 this library links.
+    Both coexist in one process (same KFD process, one GPU address space, so
+    torch tensors are valid kernel arguments here) only when torch's runtime
+    initialises first; ours initialising first makes torch report "No HIP
+    GPUs".  So before our first HIP call, let torch initialise if it is
+    installed.  Set MEV_TORCH_FIRST=0 for torch-free processes."""
+    global _torch_first_done
+    if _torch_first_done:
+        return
+    _torch_first_done = True
+    if os.environ.get("MEV_TORCH_FIRST", "1") == "0":
+        return
+    try:
+        import torch
+    except ImportError:
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+
+
 def default_config() -> Dict:
     c = MevConfig()
     _check(load_library().mev_config_default(ctypes.byref(c)))
@@ -172,6 +204,7 @@ class Handle:
     """One device-resident batch of E intersection envs (owner of a mev_handle)."""
 
     def __init__(self, **cfg):
+        _torch_runtime_first()
         L = load_library()
         c = MevConfig()
         _check(L.mev_config_default(ctypes.byref(c)))
@@ -352,6 +385,15 @@ class Handle:
         _check(self._lib.mev_set_reward(self._h, rc.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
         self.config["reward"] = [float(x) for x in rc]
 
+    def kernel_timing(self, enable: bool = True):
+        _check(self._lib.mev_kernel_timing(self._h, int(bool(enable))))
+
+    def kernel_times(self):
+        """(k_cars ms summed, k_lidar ms summed, steps) since the previous call."""
+        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        _check(self._lib.mev_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
+        return a.value, b.value, n.value
+
     def npc_overflow(self) -> int:
         v = ctypes.c_int64()
         _check(self._lib.mev_npc_overflow(self._h, ctypes.byref(v)))
@@ -377,6 +419,7 @@ def car_check_collision(box_a, box_b) -> bool:
 
 
 def device_count() -> int:
+    _torch_runtime_first()
     n = ctypes.c_int32()
     load_library().mev_device_count(ctypes.byref(n))
     return n.value

@@ -65,6 +65,11 @@ struct mev_handle {
     float* d_rel = nullptr;
     int32_t* d_traffic = nullptr;
     uint64_t rng_counter = 0;
+    // per-kernel timing (mev_kernel_timing): 3 events per step, folded into sums when the ring fills
+    std::vector<hipEvent_t> tev;
+    int tn = 0;
+    double t_cars_ms = 0.0, t_lidar_ms = 0.0;
+    int64_t t_steps = 0;
 
     template <class T>
     hipError_t alloc(T** p, size_t n) {
@@ -75,7 +80,28 @@ struct mev_handle {
         }
         return e;
     }
+    hipError_t fold_timing() {
+        if (tn == 0) return hipSuccess;
+        hipError_t e = hipEventSynchronize(tev[size_t(3 * tn - 1)]);
+        if (e != hipSuccess) return e;
+        for (int i = 0; i < tn; ++i) {
+            float a = 0.f, b = 0.f;
+            if ((e = hipEventElapsedTime(&a, tev[size_t(3 * i)], tev[size_t(3 * i + 1)])) != hipSuccess) return e;
+            if ((e = hipEventElapsedTime(&b, tev[size_t(3 * i + 1)], tev[size_t(3 * i + 2)])) != hipSuccess) return e;
+            t_cars_ms += a;
+            t_lidar_ms += b;
+        }
+        t_steps += tn;
+        tn = 0;
+        return hipSuccess;
+    }
+    void free_timing() {
+        for (hipEvent_t ev : tev) (void)hipEventDestroy(ev);
+        tev.clear();
+        tn = 0;
+    }
     ~mev_handle() {
+        free_timing();
         for (void* p : allocs) (void)hipFree(p);
         if (own_stream) (void)hipStreamDestroy(own_stream);
     }
@@ -529,7 +555,13 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     h->sp.spawn_prob = 1.0f - expf(-h->cfg.traffic_density * a->dt);
     const mev::Outputs o = resolve_outputs(h, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated,
                                            a->agents_alive, a->step, dev);
-    HIP_TRY(mev::launch_step(h->sp, in, o, h->stream));
+    const hipEvent_t* ev = nullptr;
+    if (!h->tev.empty()) {
+        if (size_t(3 * (h->tn + 1)) > h->tev.size()) HIP_TRY(h->fold_timing());
+        ev = &h->tev[size_t(3 * h->tn)];
+        ++h->tn;
+    }
+    HIP_TRY(mev::launch_step(h->sp, in, o, h->stream, ev));
     h->last = o;
     if (!dev) {
         int r = copy_out(h, o, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated, a->agents_alive,
@@ -612,6 +644,38 @@ int mev_device_outputs(mev_handle* h, float** obs, float** rew, uint8_t** done, 
     if (status) *status = h->internal.status;
     if (term) *term = h->internal.term;
     if (trunc) *trunc = h->internal.trunc;
+    return MEV_OK;
+}
+
+int mev_kernel_timing(mev_handle* h, int32_t enable) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (!enable) {
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        h->free_timing();
+        return MEV_OK;
+    }
+    if (h->tev.empty()) {
+        const int ring = 4096;  // steps between host folds
+        h->tev.resize(size_t(3 * ring), nullptr);
+        for (auto& ev : h->tev) HIP_TRY(hipEventCreate(&ev));
+    }
+    h->tn = 0;
+    h->t_cars_ms = h->t_lidar_ms = 0.0;
+    h->t_steps = 0;
+    return MEV_OK;
+}
+
+int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* steps) {
+    if (!h || !cars_ms || !lidar_ms || !steps) return fail(MEV_E_INVALID, "null argument");
+    if (h->tev.empty()) return fail(MEV_E_INVALID, "kernel timing is not enabled");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(h->fold_timing());
+    *cars_ms = h->t_cars_ms;
+    *lidar_ms = h->t_lidar_ms;
+    *steps = h->t_steps;
+    h->t_cars_ms = h->t_lidar_ms = 0.0;
+    h->t_steps = 0;
     return MEV_OK;
 }
 

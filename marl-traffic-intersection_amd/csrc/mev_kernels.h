@@ -89,7 +89,9 @@ struct StepInputs {
     uint64_t rng_counter;      // handle-wide step counter (Philox counter for NPC spawns)
 };
 
-hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s);
+// ev (nullable): three events recorded before k_cars, between k_cars and k_lidar, after k_lidar
+hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
+                       const hipEvent_t* ev = nullptr);
 hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s);
 // recompute the observation rows from the current state with LiDAR = max (after set_state)
 hipError_t launch_observe_reset_lidar(const SimParams& p, const Outputs& out, hipStream_t s);

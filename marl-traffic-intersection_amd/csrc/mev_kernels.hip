@@ -1046,17 +1046,22 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
     }
 }
 
-hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s) {
+hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
+                       const hipEvent_t* ev) {
+    if (ev) (void)hipEventRecord(ev[0], s);
     if (p.traffic) hipLaunchKernelGGL(k_cars<true>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
     else hipLaunchKernelGGL(k_cars<false>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (ev) (void)hipEventRecord(ev[1], s);
     const int Ta = (p.R + WAVE - 1) / WAVE * WAVE;
     const int per = Ta >= 256 ? 1 : 256 / Ta;
     const unsigned blocks = (unsigned)((p.E * p.N + per - 1) / per);
     if (p.dist_tab) hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(per * Ta), 0, s, p, out);
     else hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(per * Ta), 0, s, p, out);
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (ev && e == hipSuccess) (void)hipEventRecord(ev[2], s);
+    return e;
 }
 
 hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s) {

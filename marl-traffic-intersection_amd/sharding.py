@@ -1,0 +1,101 @@
+"""Env sharding over GPUs.
+
+Envs never interact, so a batch of E envs is split into contiguous blocks,
+env e -> rank floor(e * G / E), one process and one device handle per GPU,
+with no communication inside a step.  The only collective is one gather per
+step of the per-rank outputs to rank 0 (RCCL over xGMI on MI355X; gloo in
+the CPU tests), issued on the step's stream right after the step so it
+overlaps the next step's launch on the other ranks.
+
+The outputs of one step are packed into ONE flat byte buffer per rank so the
+gather is a single message per peer:
+
+    obs f32 [C, N, D] | reward f32 [C, N] | done u8 [C, N] | status u8 [C, N]
+    | terminated u8 [C] | truncated u8 [C]        (padded to 256 B)
+
+with C = ceil(E / G) slots per rank (ranks with fewer envs leave the tail of
+their slots unused).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+
+def shard_bounds(total_envs: int, world: int, rank: int) -> Tuple[int, int]:
+    """(first env, env count) of `rank`: env e belongs to rank floor(e*world/total)."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    start = -(-rank * total_envs // world)          # ceil(rank*E/G): smallest e with e*G/E >= rank
+    stop = -(-(rank + 1) * total_envs // world)
+    return start, stop - start
+
+
+def env_owner(env: int, total_envs: int, world: int) -> int:
+    return env * world // total_envs
+
+
+class PackedOutputs:
+    """Byte layout of one rank's step outputs (see module docstring)."""
+
+    FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated")
+
+    def __init__(self, slots: int, agents: int, obs_dim: int):
+        self.C, self.N, self.D = int(slots), int(agents), int(obs_dim)
+        C, N, D = self.C, self.N, self.D
+        sizes = [C * N * D * 4, C * N * 4, C * N, C * N, C, C]
+        self.offsets: Dict[str, int] = {}
+        off = 0
+        for name, sz in zip(self.FIELDS, sizes):
+            self.offsets[name] = off
+            off += sz
+        self.used = off
+        self.nbytes = (off + 255) // 256 * 256
+
+    def pointers(self, base: int) -> Dict[str, int]:
+        """Field pointers (for mev_step's output arguments) inside a buffer at `base`."""
+        return {k: base + v for k, v in self.offsets.items()}
+
+    def _shapes(self):
+        C, N, D = self.C, self.N, self.D
+        return {"obs": ((C, N, D), 4), "reward": ((C, N), 4), "done": ((C, N), 1), "status": ((C, N), 1),
+                "terminated": ((C,), 1), "truncated": ((C,), 1)}
+
+    def unpack(self, buf) -> Dict[str, object]:
+        """Typed views of one packed buffer (torch uint8 tensor or numpy uint8 array)."""
+        out = {}
+        is_torch = hasattr(buf, "view") and hasattr(buf, "data_ptr")
+        for name, (shape, isz) in self._shapes().items():
+            off = self.offsets[name]
+            n = 1
+            for s in shape:
+                n *= s
+            raw = buf[off: off + n * isz]
+            if is_torch:
+                import torch
+                t = raw.view(torch.float32) if isz == 4 else raw
+                out[name] = t.view(*shape)
+            else:
+                import numpy as np
+                a = raw.view(np.float32) if isz == 4 else raw
+                out[name] = a.reshape(shape)
+        return out
+
+    def unpack_gathered(self, stacked, total_envs: int, world: int) -> Dict[str, object]:
+        """[world, nbytes] gathered buffers -> outputs of all `total_envs` envs in env order."""
+        parts: List[Dict[str, object]] = []
+        for r in range(world):
+            _, cnt = shard_bounds(total_envs, world, r)
+            v = self.unpack(stacked[r])
+            parts.append({k: x[:cnt] for k, x in v.items()})
+        if hasattr(stacked, "data_ptr"):
+            import torch
+            return {k: torch.cat([p[k] for p in parts]) for k in self.FIELDS}
+        import numpy as np
+        return {k: np.concatenate([p[k] for p in parts]) for k in self.FIELDS}
+
+
+def gather_to_root(buf, stacked: Optional[object], group=None, async_op: bool = True):
+    """One gather of every rank's packed buffer into `stacked` ([world, nbytes]) on rank 0."""
+    import torch.distributed as dist
+    gl = list(stacked.unbind(0)) if stacked is not None else None
+    return dist.gather(buf, gather_list=gl, dst=0, group=group, async_op=async_op)

@@ -1,0 +1,137 @@
+"""Env sharding + the per-step gather, world_size 2 over gloo on the CPU.
+
+Each rank steps ITS shard of the envs (with the C restatement oracle standing
+in for the per-GPU device handle — test infrastructure), packs the step
+outputs with sharding.PackedOutputs exactly as bench.py does for the device
+buffers, and gathers them to rank 0, which must see the same outputs as one
+process stepping all envs."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+import pkgload  # noqa: E402
+
+pkgload.load()
+from marl_traffic_intersection_amd import sharding  # noqa: E402
+
+N, R, D, T = 3, 16, 127, 6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_envs(env_ids):
+    import oracle_replay as OR
+    O = OR.O
+    envs = []
+    for e in env_ids:
+        o = O.OracleEnv(n_agents=N, rays=R, obs_dim=D, use_team=True, max_npcs=64)
+        routes = [o.route_id(((e + i) % 12), 12 + [3, 7, 11, 6, 10, 2, 9, 1, 5, 0, 4, 8][(e + i) % 12]) for i in range(N)]
+        o.reset(routes)
+        envs.append(o)
+    return envs
+
+
+def _actions(total_envs, t):
+    rng = np.random.default_rng(100 + t)
+    return rng.uniform(-1, 1, (total_envs, N, 2)).astype(np.float32)
+
+
+def _step_packed(envs, first, count, layout, t, total_envs):
+    buf = np.zeros(layout.nbytes, np.uint8)
+    v = layout.unpack(buf)
+    acts = _actions(total_envs, t)
+    for j in range(count):
+        r = envs[j].step(acts[first + j])
+        v["obs"][j] = r["obs"]
+        v["reward"][j] = r["rew"]
+        v["done"][j] = r["done"]
+        v["status"][j] = r["status"]
+        v["terminated"][j] = r["terminated"]
+        v["truncated"][j] = r["truncated"]
+    return buf
+
+
+def _worker(rank, world, port, total_envs, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        first, count = sharding.shard_bounds(total_envs, world, rank)
+        slots = -(-total_envs // world)
+        layout = sharding.PackedOutputs(slots, N, D)
+        envs = _oracle_envs(range(first, first + count))
+        results = []
+        for t in range(T):
+            buf = torch.from_numpy(_step_packed(envs, first, count, layout, t, total_envs))
+            stacked = torch.zeros((world, layout.nbytes), dtype=torch.uint8) if rank == 0 else None
+            w = sharding.gather_to_root(buf, stacked, async_op=True)
+            w.wait()
+            if rank == 0:
+                got = layout.unpack_gathered(stacked, total_envs, world)
+                results.append({k: v.numpy().copy() for k, v in got.items()})
+        if rank == 0:
+            q.put(results)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_bounds_partition():
+    for E in (1, 7, 8, 4096, 32768, 12345):
+        for G in (1, 2, 3, 4, 8):
+            if E < G:
+                continue
+            cover = []
+            for r in range(G):
+                s, c = sharding.shard_bounds(E, G, r)
+                assert c in (E // G, -(-E // G))
+                cover.extend(range(s, s + c))
+                for e in (s, s + c - 1):
+                    assert sharding.env_owner(e, E, G) == r
+            assert cover == list(range(E))
+
+
+def test_packed_layout_offsets():
+    lay = sharding.PackedOutputs(4096, 8, 95)
+    assert lay.offsets["reward"] == 4096 * 8 * 95 * 4
+    assert lay.offsets["truncated"] == lay.used - 4096
+    assert lay.nbytes % 256 == 0 and lay.nbytes >= lay.used
+
+
+@pytest.mark.parametrize("total_envs", [6, 5])
+def test_gather_matches_single_process(total_envs):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total_envs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    envs = _oracle_envs(range(total_envs))
+    for t in range(T):
+        acts = _actions(total_envs, t)
+        for e in range(total_envs):
+            r = envs[e].step(acts[e])
+            assert np.array_equal(results[t]["obs"][e].view(np.uint32), r["obs"].view(np.uint32)), (t, e)
+            assert np.array_equal(results[t]["reward"][e], r["rew"]), (t, e)
+            assert np.array_equal(results[t]["status"][e], r["status"]), (t, e)
+            assert int(results[t]["terminated"][e]) == r["terminated"]
