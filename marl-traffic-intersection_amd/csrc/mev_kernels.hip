@@ -13,6 +13,8 @@
 // cpp/Lidar.cpp:16-90 (ray march).  Compiled with -ffp-contract=off.
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "mev_kernels.h"
 #include "mev_world.h"
 
@@ -814,9 +816,9 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 }
 
 // ------------------------------------------------------------- LiDAR ---
-// Lidar::update (cpp/Lidar.cpp:16-90) for every (env, agent, beam): one thread
-// per beam, reading the poses k_cars left in HBM (after respawn) and the
-// obstacle boxes / candidate masks it published.
+// Lidar::update (cpp/Lidar.cpp:16-90) for every (env, agent, beam), reading
+// the poses k_cars left in HBM (after respawn) and the obstacle boxes /
+// candidate masks it published.
 //
 // The reference marches k = 0..S-1 (dist_k = k*step) and stops at the first k
 // whose truncated pixel is off-screen (no hit), off-road (k>0, hit) or inside
@@ -824,168 +826,262 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 //  1. road/screen: exact probe at k, then skip ahead by the number of steps
 //     provably safe from the real-valued point (truncation moves a pixel by
 //     < 1 px, margin 1.5 px): every skipped probe is on-screen and strictly
-//     inside a road strip, so it could not have stopped the march;
-//  2. cars: for each candidate box only the k whose real point lies within
-//     1.5 px of the box are probed exactly, and only below the k of step 1.
-// Bit-identical to the sequential march (tests/test_parity_gpu.py).
-// Probe coordinate of a beam: c(k) = (int)(c0 + dc * dist_k).  dist_k grows
-// with k and IEEE rounding and truncation are monotone, so c(k) is monotone
-// in k (non-decreasing for dc > 0, non-increasing for dc < 0).  That makes
-// "k with c(k) inside [lo, hi]" an interval whose ends we find from a real
-// estimate corrected by exact probes (usually 0-1 extra probe per end).
-__device__ inline int probe_c(const SimParams& p, float c0, float dc, int k) {
-    return (int)(c0 + dc * march_dist(p, k));
-}
+//     inside a road strip or the corner square, so it could not have stopped
+//     the march;
+//  2. cars: for each candidate box, the probes whose real point lies in the
+//     box's slab widened by >= 0.5 px form a superset range of k; those (and
+//     only below the k of step 1) are probed exactly, in march order.
+// Bit-identical to the sequential march (tests/test_parity_gpu.py,
+// tests/test_gpu_vs_oracle.py).
+// A probe pixel (int)f lies in [x0, x1] only if f lies in (x0 - 1, x1 + 1);
+// the slab used is [x0 - 1.5, x1 + 2.5], so float rounding of the probe
+// position, of the reciprocal and of the accumulated distances can never
+// drop a real hit from the range.
 
-// Interval [*k0, *k1] of probes k in [0, S-1] with lo <= c(k) <= hi (empty: *k0 > *k1).
-__device__ inline void coord_interval(const SimParams& p, float c0, float dc, int lo, int hi, int S, float inv_stp,
-                                      int* k0, int* k1) {
-    if (fabs_f(dc) < 1e-6f) {  // effectively constant over <= max_dist
-        // still evaluate exactly at both ends (c(k) may step by one pixel)
-        int a = 0, b = S - 1;
-        const int ca = probe_c(p, c0, dc, 0), cb = probe_c(p, c0, dc, S - 1);
-        if ((ca < lo || ca > hi) && (cb < lo || cb > hi)) { *k0 = 1; *k1 = 0; return; }
-        while (a <= b) { const int c = probe_c(p, c0, dc, a); if (c >= lo && c <= hi) break; ++a; }
-        while (b >= a) { const int c = probe_c(p, c0, dc, b); if (c >= lo && c <= hi) break; --b; }
-        *k0 = a; *k1 = b;
+// Clip [lo, hi] (distances along the ray) to where coordinate c0 + dc*t lies in [a, b].
+__device__ inline void slab_clip(float c0, float dc, float idc, float a, float b, float& lo, float& hi) {
+    if (fabs_f(dc) < 1e-6f) {  // constant to < 2.5e-4 px over the ray
+        if (c0 < a || c0 > b) { lo = 1.0f; hi = 0.0f; }
         return;
     }
-    // entry bound E (first k with c(k) past it), exit bound X (last k not past it)
-    const bool inc = dc > 0.0f;
-    const float ent = inc ? (float)lo : (float)hi;  // c(k) >= lo  (inc)  /  c(k) <= hi (dec)
-    const float ext = inc ? (float)hi : (float)lo;  // c(k) <= hi  (inc)  /  c(k) >= lo (dec)
-    const float scale = __builtin_amdgcn_rcpf(dc) * inv_stp;
-    auto entered = [&](int k) { const int c = probe_c(p, c0, dc, k); return inc ? c >= lo : c <= hi; };
-    auto not_exited = [&](int k) { const int c = probe_c(p, c0, dc, k); return inc ? c <= hi : c >= lo; };
-    float fe = (ent - c0) * scale;
-    float fx = (ext + (inc ? 1.0f : -1.0f) - c0) * scale;
-    fe = fminf(fmaxf(fe, 0.0f), (float)(S - 1));
-    fx = fminf(fmaxf(fx, 0.0f), (float)(S - 1));
-    int ke = (int)fe;
-    while (ke > 0 && entered(ke - 1)) --ke;
-    while (ke < S && !entered(ke)) ++ke;
-    if (ke >= S) { *k0 = 1; *k1 = 0; return; }
-    int kx = (int)fx;
-    if (kx < ke) kx = ke;
-    while (kx + 1 < S && not_exited(kx + 1)) ++kx;
-    while (kx >= ke && !not_exited(kx)) --kx;
-    *k0 = ke;
-    *k1 = kx;
+    const float t1 = (a - c0) * idc, t2 = (b - c0) * idc;
+    lo = fmaxf(lo, fminf(t1, t2));
+    hi = fminf(hi, fmaxf(t1, t2));
+}
+
+__device__ inline int lane_rank(unsigned long long mask) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+// LDS visibility between the lanes of one wave (no block barrier: waves are independent)
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Per-wave LDS of k_lidar: ag float4[G] (x, y, heading, agent id) of the
+// group's alive agents, dir float2[G*R] beam directions, res int[G*R] road
+// results (kr << 1 | hit).
+size_t lidar_wave_lds_bytes(int G, int R) { return (size_t)G * 16 + (size_t)G * R * 12; }
+
+int lidar_group(int R) {
+    // ~256 beams per wave pool: G = 4 agents at R = 64 (measured best of 1..16, tools/kernel_time.py)
+    int g = 256 / (R > 0 ? R : 1);
+    return g < 1 ? 1 : (g > 64 ? 64 : g);
 }
 
 template <bool TAB>
-__global__ __launch_bounds__(1024) void k_lidar(SimParams p, Outputs out) {
-    // one (env, agent) per Ta = roundup(R, 64) threads, 256/Ta agents per block:
-    // the pose, liveness and candidate masks are wave-uniform; one thread per beam
-    const int Ta = (p.R + WAVE - 1) / WAVE * WAVE;
-    // Ta is a multiple of 64, so every wave serves exactly one agent
-    const int gb = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x / Ta) + threadIdx.x / Ta);  // e*N + a
-    const int b = threadIdx.x % Ta;
-    if (gb >= p.E * p.N || b >= p.R) return;
-    const int e = gb / p.N;
-    float* row = out.obs + (size_t)gb * p.D;
-    if (!p.ego.alive[gb]) {
-        if (b < p.lidar_slots) row[OBS_HEAD + b] = 0.0f;
-        return;
+__global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G, int wave_lds) {
+    // Each wave owns a group of G agents (G*R <= max(256, R) beams).  Phase 1
+    // computes the beam directions in lockstep; phase 2 marches the road with
+    // the group's beams fed to the 64 lanes from a queue, so a lane that
+    // finishes a short beam takes the next one instead of idling until the
+    // longest beam of its agent is done (lockstep cost = max over the agent's
+    // beams, pooled cost ~ their mean); phase 3 resolves the cars per agent
+    // (lane = beam, candidate boxes wave-uniform) and writes the observation.
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wv = threadIdx.x / WAVE;
+    const int R = p.R;
+    const int EN = p.E * p.N;
+    const int a0 = __builtin_amdgcn_readfirstlane((blockIdx.x * (blockDim.x / WAVE) + wv) * G);
+    if (a0 >= EN) return;  // wave-uniform exit: the kernel has no block-level barrier
+    const int na = EN - a0 < G ? EN - a0 : G;
+    unsigned char* base = lds_raw + (size_t)wv * (size_t)wave_lds;
+    float4* ag = reinterpret_cast<float4*>(base);
+    float2* dir = reinterpret_cast<float2*>(base + (size_t)G * 16);
+    int* res = reinterpret_cast<int*>(base + (size_t)G * 16 + (size_t)G * R * 8);
+
+    // ---- phase 1: alive agents of the group (compacted), beam directions
+    bool alv = false;
+    if (lane < na) alv = p.ego.alive[a0 + lane] != 0;
+    const unsigned long long am = ballot(alv);
+    const int nal = __popcll(am);
+    if (alv) {
+        const int g = a0 + lane;
+        ag[lane_rank(am)] = make_float4(p.ego.x[g], p.ego.y[g], p.ego.h[g], __int_as_float(g));
     }
-    const float maxd = p.lidar_max, stp = p.lidar_step;
+    if (__popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
+        for (int j = 0; j < na; ++j) {
+            if ((am >> j) & 1ull) continue;
+            float* row = out.obs + (size_t)(a0 + j) * p.D + OBS_HEAD;
+            for (int b = lane; b < p.lidar_slots; b += WAVE) row[b] = 0.0f;
+        }
+    }
+    wave_lds_sync();
+    for (int j = 0; j < nal; ++j) {
+        const float h = ag[j].z;
+        for (int b = lane; b < R; b += WAVE) {
+            float sn, cs;
+            sincosf(h + p.rel_angles[b], &sn, &cs);  // Lidar.cpp:24-26
+            dir[j * R + b] = make_float2(cs, -sn);
+        }
+    }
+    wave_lds_sync();
+
+    // ---- phase 2: pooled road + screen march (Lidar.cpp:31-48, first stop wins)
+    const int total = nal * R;
+    const float stp = p.lidar_step;
     const int S = p.lidar_steps;
     const float rwf = (float)p.irw;
     const float inv_stp = __builtin_amdgcn_rcpf(stp);
-    const float cx = p.ego.x[gb], cy = p.ego.y[gb], ch = p.ego.h[gb];
-    float sn, cs;
-    sincosf(ch + p.rel_angles[b], &sn, &cs);
-    const float dx = cs, dy = -sn;
-    // 1. road + screen: exact probes, skipping provably-safe stretches
-    const float adx = fabs_f(dx), ady = fabs_f(dy);
-    const float iadx = __builtin_amdgcn_rcpf(adx), iady = __builtin_amdgcn_rcpf(ady);
-    const float crf = CORNER_RADIUS, ccen = rwf + crf;
-    const float cr2 = crf * crf;
     const float two_stp = 2.0f * stp;
-    // Lanes step in lockstep with predication instead of per-lane breaks: the
-    // loop exit is wave-uniform, so divergence costs no exec-mask juggling.
-    int kr = S;
-    bool hit = false;
+    const float crf = CORNER_RADIUS, ccen = rwf + crf;
+    const float cr2p1 = crf * crf + 1.0f;
+    const float rwm = rwf - 1.5f;
+    const float invR = 1.0f / (float)R;
+    int next = total < WAVE ? total : WAVE;
+    int q = lane < total ? lane : -1;
+    float cx = 0.0f, cy = 0.0f, dx = 0.0f, dy = 0.0f, idx = 0.0f, idy = 0.0f, iadx = 0.0f, iady = 0.0f;
     int k = 0;
-#ifdef MEV_EXP_NOROAD
-    bool active = false;
-#else
-    bool active = S > 0;
-#endif
-    const float rw_m = rwf, ccen_m = ccen, cr2p1 = cr2 + 1.0f;
+    auto load_beam = [&](int qq) {
+        int j = (int)((float)qq * invR);
+        j = (j + 1) * R <= qq ? j + 1 : (j * R > qq ? j - 1 : j);
+        const float4 a = ag[j];
+        const float2 d = dir[qq];
+        cx = a.x; cy = a.y; dx = d.x; dy = d.y;
+        idx = __builtin_amdgcn_rcpf(dx);
+        idy = __builtin_amdgcn_rcpf(dy);
+        iadx = fabs_f(idx);
+        iady = fabs_f(idy);
+        k = 0;
+    };
+    if (q >= 0) load_beam(q);
 #ifdef MEV_ITERS
     int iters = 0;
 #endif
-    while (__builtin_amdgcn_ballot_w64(active) != 0ull) {
-        const int kk = active ? k : 0;
-        const float d = TAB ? p.dist_tab[kk] : (float)kk * stp;
-        const float fx = cx + dx * d;
-        const float fy = cy + dy * d;
-        const int px = (int)fx, py = (int)fy;
-        // exact reference predicates at the truncated pixel (Lidar.cpp:36-48):
-        // screen, then (k > 0) road == RoadGeometry::is_on_road at integer pixels:
-        //   on_road <=> dist^2 to the grass-disc centre > cr^2 (integers: >= cr^2+1)
-        //               and (in a strip: min(ax, ay) <= rw  or  in the corner square: max <= rw+cr)
-        const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
-        const bool off_screen = pmax >= (unsigned)WIDTH;
-        const float iax = fabs_f((float)(px - 375)), iay = fabs_f((float)(py - 375));
-        const float qdx = iax - ccen_m, qdy = iay - ccen_m;
-        const float onv = fmaxf(fminf(fminf(iax, iay) - rw_m, fmaxf(iax, iay) - ccen_m), cr2p1 - (qdx * qdx + qdy * qdy));
-        const bool off_road = (kk > 0) & (onv > 0.0f);
-        const bool stop = active & (off_screen | off_road);
-        kr = stop ? kk : kr;
-        hit = stop ? !off_screen : hit;
-        // Distance along the ray that provably keeps every truncated probe on
-        // screen and on the road (margin 1.5 px > the < 1 px truncation shift).
-        const float ax = fabs_f(fx - 375.0f), ay = fabs_f(fy - 375.0f);
-        const float mx = rwf - 1.5f - ax, my = rwf - 1.5f - ay;
-        // strictly inside a strip: |x-375| grows at most |dx| per unit length
-        const float strip = fmaxf(fmaxf(mx, 0.0f) * iadx, fmaxf(my, 0.0f) * iady);
-        // corner square: road outside the grass disc on its outer corner
-        // (approximate sqrt: bound only, extra 0.05 px margin)
-        const float qx = ax - ccen, qy = ay - ccen;
-        const float corner = fminf(__builtin_amdgcn_sqrtf(qx * qx + qy * qy) - crf, fminf(ccen - ax, ccen - ay)) - 1.55f;
-        const float road = fmaxf(mx, my) > 0.0f ? strip : (fmaxf(ax, ay) < ccen ? corner : 0.0f);
-        const float tx = (dx > 0.0f ? 748.5f - fx : fx - 0.5f) * iadx;
-        const float ty = (dy > 0.0f ? 748.5f - fy : fy - 0.5f) * iady;
-        const float safe = fminf(road, fminf(tx, ty));
-        // probes k+1 .. k+j-1 lie within (j-1)*step <= safe of this point
-        const int jump = (safe >= two_stp) ? (int)(safe * inv_stp) : 1;
-        k = kk + jump;
-        active = active & !stop & (k < S);
+#ifdef MEV_EXP_NOROAD
+    for (int qq = lane; qq < total; qq += WAVE) res[qq] = S << 1;
+    q = -1;
+#endif
+    while (ballot(q >= 0) != 0ull) {
+        bool fin = false;
+        if (q >= 0) {
+            const float d = TAB ? p.dist_tab[k] : (float)k * stp;
+            const float fx = cx + dx * d;
+            const float fy = cy + dy * d;
+            const int px = (int)fx, py = (int)fy;
+            // exact reference predicates at the truncated pixel: screen, then
+            // (k > 0) road == RoadGeometry::is_on_road at integer pixels:
+            //   on_road <=> dist^2 to the grass-disc centre >= cr^2 + 1
+            //               and (in a strip: min(ax, ay) <= rw  or  corner square: max <= rw + cr)
+            const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
+            const bool off_screen = pmax >= (unsigned)WIDTH;
+            const float iax = fabs_f((float)(px - 375)), iay = fabs_f((float)(py - 375));
+            const float qdx = iax - ccen, qdy = iay - ccen;
+            const float onv = fmaxf(fminf(fminf(iax, iay) - rwf, fmaxf(iax, iay) - ccen), cr2p1 - (qdx * qdx + qdy * qdy));
+            const bool off_road = (k > 0) & (onv > 0.0f);
+            if (off_screen | off_road) {
+                res[q] = (k << 1) | (off_screen ? 0 : 1);
+                fin = true;
+            } else {
+                // distance along the ray that provably keeps every truncated
+                // probe on screen and on the road (margin 1.5 px > the < 1 px
+                // truncation shift): inside a strip the bound is directional
+                // (the distance to the strip edge the ray is heading for)
+                const float rx = fx - 375.0f, ry = fy - 375.0f;
+                const float ax = fabs_f(rx), ay = fabs_f(ry);
+                const bool in_x = ax < rwm, in_y = ay < rwm;
+                const float sx = in_x ? rwm * iadx - rx * idx : 0.0f;
+                const float sy = in_y ? rwm * iady - ry * idy : 0.0f;
+                // corner square: road outside the grass disc on its outer corner
+                // (approximate sqrt: bound only, extra 0.05 px margin)
+                const float qx = ax - ccen, qy = ay - ccen;
+                const float corner = fminf(__builtin_amdgcn_sqrtf(qx * qx + qy * qy) - crf, fminf(ccen - ax, ccen - ay)) - 1.55f;
+                const float road = (in_x | in_y) ? fmaxf(sx, sy) : (fmaxf(ax, ay) < ccen ? corner : 0.0f);
+                const float tx = (dx > 0.0f ? 748.5f - fx : fx - 0.5f) * iadx;
+                const float ty = (dy > 0.0f ? 748.5f - fy : fy - 0.5f) * iady;
+                const float safe = fminf(road, fminf(tx, ty));
+                // probes k+1 .. k+j-1 lie within (j-1)*step <= safe of this point
+                k += (safe >= two_stp) ? (int)(safe * inv_stp) : 1;
+                if (k >= S) {
+                    res[q] = S << 1;
+                    fin = true;
+                }
+            }
+        }
 #ifdef MEV_ITERS
         ++iters;
 #endif
+        const unsigned long long fm = ballot(fin);
+        if (fm != 0ull) {
+            if (fin) {
+                const int nq = next + lane_rank(fm);
+                q = nq < total ? nq : -1;
+                if (q >= 0) load_beam(q);
+            }
+            next += __popcll(fm);
+        }
     }
 #ifdef MEV_ITERS
-    // diagnostic build: wave iteration count and summed per-lane iterations
-    if (b == 0 && gb < p.E * 8) p.debug[gb] = (unsigned long long)iters;
+    if (lane == 0 && a0 / G < p.E * 8) p.debug[a0 / G] = (unsigned long long)iters;
 #endif
-    // 2. cars among the agent's candidates (every ego alive or not, then NPCs):
-    //    the probes inside a box form the intersection of the x- and y-intervals
-    const int4* boxes = p.ob_box + (size_t)e * p.ob_stride;
+    wave_lds_sync();
+
+    // ---- phase 3: cars (Lidar.cpp:50-80) per alive agent, lane = beam.  The
+    // env's obstacle boxes are loaded once into VGPRs (lane o holds box o) and
+    // broadcast with readlane, so the candidate loop issues no dependent loads.
+    const float d1 = march_dist(p, 1);
+    const int OB = p.ob_stride;  // <= 128
+    int cur_env = -1;
+    int4 vb0 = make_int4(0, 0, 0, 0), vb1 = make_int4(0, 0, 0, 0);
+    for (int j = 0; j < nal; ++j) {
+        const float4 a = ag[j];
+        const int g = __builtin_amdgcn_readfirstlane(__float_as_int(a.w));
+        const int e = g / p.N;
+        if (e != cur_env) {
+            const int4* boxes = p.ob_box + (size_t)e * OB;
+            if (lane < OB) vb0 = boxes[lane];
+            if (lane + WAVE < OB) vb1 = boxes[lane + WAVE];
+            cur_env = e;
+        }
 #ifdef MEV_EXP_NOCARS
-    const unsigned long long cand0 = 0, cand1 = 0;
+        const unsigned long long cand0 = 0, cand1 = 0;
 #else
-    const unsigned long long cand0 = p.ob_cand[2 * gb], cand1 = p.ob_cand[2 * gb + 1];
+        const unsigned long long cand0 = p.ob_cand[2 * g], cand1 = p.ob_cand[2 * g + 1];
 #endif
+        float* row = out.obs + (size_t)g * p.D + OBS_HEAD;
+        for (int b = lane; b < R; b += WAVE) {
+            const int r = res[j * R + b];
+            int kr = r >> 1;
+            bool hit = (r & 1) != 0;
+            const float2 dd = dir[j * R + b];
+            const float bdx = dd.x, bdy = dd.y;
+            const float bidx = __builtin_amdgcn_rcpf(bdx), bidy = __builtin_amdgcn_rcpf(bdy);
+            // the probes inside a box form the intersection of the x- and y-intervals
 #pragma unroll
-    for (int wd = 0; wd < 2; ++wd)
-    for (unsigned long long cm = wd ? cand1 : cand0; cm; cm &= cm - 1ull) {
-        const int o = (wd << 6) + __builtin_ctzll(cm);
-        const int4 bx = boxes[o];
-        if (kr <= 1) break;
-        int ax0, ax1, ay0, ay1;
-        coord_interval(p, cx, dx, bx.x, bx.y, kr, inv_stp, &ax0, &ax1);
-        if (ax0 > ax1) continue;
-        coord_interval(p, cy, dy, bx.z, bx.w, kr, inv_stp, &ay0, &ay1);
-        int k0 = ax0 > ay0 ? ax0 : ay0;
-        const int k1 = ax1 < ay1 ? ax1 : ay1;
-        k0 = k0 < 1 ? 1 : k0;  // no car test at dist == 0
-        if (k0 <= k1) { kr = k0; hit = true; }  // k1 <= kr-1 by construction
+            for (int wd = 0; wd < 2; ++wd)
+            for (unsigned long long cm = wd ? cand1 : cand0; cm; cm &= cm - 1ull) {
+                const int o = __builtin_ctzll(cm);
+                const int4 vb = wd ? vb1 : vb0;
+                const int4 bx = make_int4(__builtin_amdgcn_readlane(vb.x, o), __builtin_amdgcn_readlane(vb.y, o),
+                                          __builtin_amdgcn_readlane(vb.z, o), __builtin_amdgcn_readlane(vb.w, o));
+                if (kr <= 1) break;
+                // probes that can land in the box: the real slab interval of the
+                // ray, widened by >= 0.5 px, as a superset range of k ...
+                float lo = 0.0f, hi = 1.0e6f;
+                slab_clip(a.x, bdx, bidx, (float)bx.x - 1.5f, (float)bx.y + 2.5f, lo, hi);
+                slab_clip(a.y, bdy, bidy, (float)bx.z - 1.5f, (float)bx.w + 2.5f, lo, hi);
+                if (lo > hi) continue;
+                int ka = (int)(lo * inv_stp) - 1, kb = (int)(hi * inv_stp) + 1;
+                ka = ka < 1 ? 1 : ka;  // no car test at dist == 0
+                kb = kb < kr - 1 ? kb : kr - 1;
+                // ... resolved by exact probes in march order (Lidar.cpp:50-80)
+                for (int kk = ka; kk <= kb; ++kk) {
+                    const float d = march_dist(p, kk);
+                    const int px = (int)(a.x + bdx * d), py = (int)(a.y + bdy * d);
+                    if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) {
+                        kr = kk;
+                        hit = true;
+                        break;
+                    }
+                }
+            }
+            const float final_dist = hit ? march_dist(p, kr) : p.lidar_max;
+            if (b < p.lidar_slots) row[b] = final_dist * p.lidar_inv;  // Lidar::normalized (:92-98)
+        }
     }
-    const float final_dist = hit ? march_dist(p, kr) : maxd;
-    if (b < p.lidar_slots) row[OBS_HEAD + b] = final_dist * p.lidar_inv;
 }
 
 // ------------------------------------------------- reset / re-observe ---
@@ -1054,11 +1150,17 @@ hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], s);
-    const int Ta = (p.R + WAVE - 1) / WAVE * WAVE;
-    const int per = Ta >= 256 ? 1 : 256 / Ta;
-    const unsigned blocks = (unsigned)((p.E * p.N + per - 1) / per);
-    if (p.dist_tab) hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(per * Ta), 0, s, p, out);
-    else hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(per * Ta), 0, s, p, out);
+    int G = lidar_group(p.R);
+    static const int g_env = [] { const char* v = getenv("MEV_LIDAR_G"); return v ? atoi(v) : 0; }();
+    if (g_env > 0 && g_env <= 64 && (size_t)g_env * p.R <= 1024) G = g_env;  // experiments (tools/kernel_time.py)
+    const int wave_lds = (int)((lidar_wave_lds_bytes(G, p.R) + 15) / 16 * 16);
+    constexpr int WPB = 4;  // waves per block
+    const int groups = (p.E * p.N + G - 1) / G;
+    const unsigned blocks = (unsigned)((groups + WPB - 1) / WPB);
+    if (p.dist_tab)
+        hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(WPB * WAVE), WPB * wave_lds, s, p, out, G, wave_lds);
+    else
+        hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(WPB * WAVE), WPB * wave_lds, s, p, out, G, wave_lds);
     e = hipGetLastError();
     if (ev && e == hipSuccess) (void)hipEventRecord(ev[2], s);
     return e;
