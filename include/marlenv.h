@@ -182,12 +182,13 @@ int mev_npc_overflow(mev_handle* h, int64_t* count);
 /* Diagnostics: per-env phase timestamps [E][8] of the last step; all zero
  * unless the library was built with -DMEV_STAMPS (tools/phase_profile.py). */
 int mev_debug_stamps(mev_handle* h, uint64_t* out);
-/* Measurement: with timing enabled, every mev_step records HIP events on the
- * handle's stream before k_cars, between k_cars and k_lidar, and after
- * k_lidar.  mev_kernel_times returns the summed device durations (ms) of the
- * two kernels and the number of steps since the previous call (or since
- * enabling), then clears them; it waits for the recorded steps to finish. */
-int mev_kernel_timing(mev_handle* h, int32_t enable);
+/* Measurement: with timing enabled (every = n > 0), every n-th mev_step
+ * records HIP events on the handle's stream before k_cars, between k_cars and
+ * k_lidar, and after k_lidar (every = 0 disables).  mev_kernel_times returns
+ * the summed device durations (ms) of the two kernels over the timed steps
+ * and their count since the previous call (or since enabling), then clears
+ * them; it waits for the recorded steps to finish. */
+int mev_kernel_timing(mev_handle* h, int32_t every);
 int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* steps);
 
 #ifdef __cplusplus

@@ -385,11 +385,12 @@ class Handle:
         _check(self._lib.mev_set_reward(self._h, rc.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
         self.config["reward"] = [float(x) for x in rc]
 
-    def kernel_timing(self, enable: bool = True):
-        _check(self._lib.mev_kernel_timing(self._h, int(bool(enable))))
+    def kernel_timing(self, every: int = 1):
+        """Record per-kernel HIP events on every `every`-th step (0/False: off)."""
+        _check(self._lib.mev_kernel_timing(self._h, int(every)))
 
     def kernel_times(self):
-        """(k_cars ms summed, k_lidar ms summed, steps) since the previous call."""
+        """(k_cars ms summed, k_lidar ms summed, timed steps) since the previous call."""
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
         _check(self._lib.mev_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
         return a.value, b.value, n.value

@@ -68,6 +68,8 @@ struct mev_handle {
     // per-kernel timing (mev_kernel_timing): 3 events per step, folded into sums when the ring fills
     std::vector<hipEvent_t> tev;
     int tn = 0;
+    int t_every = 1;       // record events on every t_every-th step
+    int64_t t_phase = 0;   // steps since timing was enabled
     double t_cars_ms = 0.0, t_lidar_ms = 0.0;
     int64_t t_steps = 0;
 
@@ -556,7 +558,7 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     const mev::Outputs o = resolve_outputs(h, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated,
                                            a->agents_alive, a->step, dev);
     const hipEvent_t* ev = nullptr;
-    if (!h->tev.empty()) {
+    if (!h->tev.empty() && (h->t_phase++ % h->t_every) == 0) {
         if (size_t(3 * (h->tn + 1)) > h->tev.size()) HIP_TRY(h->fold_timing());
         ev = &h->tev[size_t(3 * h->tn)];
         ++h->tn;
@@ -649,6 +651,7 @@ int mev_device_outputs(mev_handle* h, float** obs, float** rew, uint8_t** done, 
 
 int mev_kernel_timing(mev_handle* h, int32_t enable) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (enable < 0) return fail(MEV_E_INVALID, "enable must be >= 0");
     HIP_TRY(hipSetDevice(h->cfg.device));
     if (!enable) {
         HIP_TRY(hipStreamSynchronize(h->stream));
@@ -661,6 +664,8 @@ int mev_kernel_timing(mev_handle* h, int32_t enable) {
         for (auto& ev : h->tev) HIP_TRY(hipEventCreate(&ev));
     }
     h->tn = 0;
+    h->t_every = enable;
+    h->t_phase = 0;
     h->t_cars_ms = h->t_lidar_ms = 0.0;
     h->t_steps = 0;
     return MEV_OK;
