@@ -128,16 +128,12 @@ struct NpcLDS {
     uint8_t pair_ok[MAXK], yield_far[MAXK];
 };
 
-struct ObsLDS {
-    int x0[MAXOB], x1[MAXOB], y0[MAXOB], y1[MAXOB];
-    float px[MAXOB], py[MAXOB], ph[MAXOB];
-    unsigned long long cand[MAXN][2];  // per agent: boxes its beams can reach (self/twins excluded)
-};
 
 // --------------------------------------------------- NPC traffic phase ---
-// update_traffic_flow, cpp/TrafficFlow.cpp:317-367, for env e.  Egos are read
-// (spawn blocking) but not moved.  On return NpcLDS holds the compacted NPCs.
-__device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NpcLDS& nl, int lane) {
+// update_traffic_flow, cpp/TrafficFlow.cpp:317-367, for env e.  Egos (positions
+// in LDS) are read for spawn blocking but not moved.  On return NpcLDS holds the compacted NPCs.
+__device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NpcLDS& nl, int lane,
+                          const float* ego_x, const float* ego_y) {
     const int K = p.K;
     // load
     if (lane < cnt) {
@@ -176,8 +172,8 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const int i = base + lane;
             bool b = false;
             if (i < p.N) {
-                const float dx = p.ego.x[e * p.N + i] - sx;
-                const float dy = p.ego.y[e * p.N + i] - sy;
+                const float dx = ego_x[i] - sx;
+                const float dy = ego_y[i] - sy;
                 b = dx * dx + dy * dy < min_d2;
             }
             blk |= ballot(b) != 0ull;
@@ -440,18 +436,16 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
 // get_observations (cpp/IntersectionEnv.cpp:418-520) minus the LiDAR block:
 // ego features, path look-ahead, 5 nearest alive neighbours (egos first, then
 // NPCs; stable by distance == libstdc++ insertion sort for <= 16 candidates).
-template <bool TRAFFIC>
-__device__ void write_obs_head(const SimParams& p, int i, const EgoLDS& el, const NpcLDS* nl, int ncnt,
-                               const float* path, int pidx, float* row) {
+template <bool TRAFFIC, class EL>
+__device__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const NpcLDS* nl, int ncnt, float tx,
+                                  float ty, float* row) {
     const float x = el.x[i], y = el.y[i], v = el.v[i], h = el.h[i];
     row[0] = x / float(WIDTH);
     row[1] = y / float(HEIGHT);
     row[2] = v / PHYSICS_MAX_SPEED;
     row[3] = h / PI_F;
-    int tidx = pidx + 10;
-    if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
-    const float dxd = path[2 * tidx] - x;
-    const float dyd = path[2 * tidx + 1] - y;
+    const float dxd = tx - x;  // path[min(path_index + 10, 159)] (:444-452)
+    const float dyd = ty - y;
     row[4] = __builtin_sqrtf(dxd * dxd + dyd * dyd) / float(WIDTH);
     row[5] = wrap_angle(atan2f(-dyd, dxd) - h) / PI_F;
     // top-5 insertion (stable)
@@ -502,185 +496,268 @@ __device__ void write_obs_head(const SimParams& p, int i, const EgoLDS& el, cons
     for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
 }
 
+template <bool TRAFFIC, class EL>
+__device__ void write_obs_head(const SimParams& p, int i, const EL& el, const NpcLDS* nl, int ncnt,
+                               const float* path, int pidx, float* row) {
+    int tidx = pidx + 10;
+    if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
+    write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, path[2 * tidx], path[2 * tidx + 1], row);
+}
+
 // ------------------------------------------------------------- the step ---
+// Dynamic LDS of k_cars, carved for the handle's N egos and K NPC slots.
+struct CarsLDS {
+    float *x, *y, *v, *h, *c, *s, *acc, *steer, *prev_dist, *pa0, *pa1;
+    float *sx, *sy, *sv, *sh, *rew, *a0, *a1, *tgx, *tgy, *t10x, *t10y;
+    float4 *cx, *cy;  // corners (Car::corners order)
+    int32_t *pidx, *intent, *route;
+    uint8_t *alive, *done, *status, *colnpc;
+    unsigned long long* col;
+    int4* box;  // obstacle AABBs, integer pixels
+    float *px, *py, *ph;
+    unsigned long long* cand;  // [N][2]: boxes each agent's beams can reach
+};
+
+__host__ __device__ inline size_t lds_al(size_t b) { return (b + 15) & ~size_t(15); }
+
+size_t cars_lds_bytes(int N, int K) {
+    const size_t n = (size_t)N, ob = (size_t)(N + K);
+    return 22 * lds_al(n * 4) + 2 * lds_al(n * 16) + 3 * lds_al(n * 4) + 4 * lds_al(n) + lds_al(n * 8) +
+           lds_al(ob * 16) + 3 * lds_al(ob * 4) + lds_al(n * 16);
+}
+
+__device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
+    const size_t n = (size_t)N, ob = (size_t)(N + K);
+    CarsLDS L;
+    unsigned char* q = base;
+    auto take = [&](size_t bytes) { unsigned char* r = q; q += lds_al(bytes); return r; };
+    float** f[22] = {&L.x, &L.y, &L.v, &L.h, &L.c, &L.s, &L.acc, &L.steer, &L.prev_dist, &L.pa0, &L.pa1,
+                     &L.sx, &L.sy, &L.sv, &L.sh, &L.rew, &L.a0, &L.a1, &L.tgx, &L.tgy, &L.t10x, &L.t10y};
+#pragma unroll
+    for (int k = 0; k < 22; ++k) *f[k] = reinterpret_cast<float*>(take(n * 4));
+    L.cx = reinterpret_cast<float4*>(take(n * 16));
+    L.cy = reinterpret_cast<float4*>(take(n * 16));
+    L.pidx = reinterpret_cast<int32_t*>(take(n * 4));
+    L.intent = reinterpret_cast<int32_t*>(take(n * 4));
+    L.route = reinterpret_cast<int32_t*>(take(n * 4));
+    L.alive = take(n);
+    L.done = take(n);
+    L.status = take(n);
+    L.colnpc = take(n);
+    L.col = reinterpret_cast<unsigned long long*>(take(n * 8));
+    L.box = reinterpret_cast<int4*>(take(ob * 16));
+    L.px = reinterpret_cast<float*>(take(ob * 4));
+    L.py = reinterpret_cast<float*>(take(ob * 4));
+    L.ph = reinterpret_cast<float*>(take(ob * 4));
+    L.cand = reinterpret_cast<unsigned long long*>(take(n * 16));
+    return L;
+}
+
 template <bool TRAFFIC>
 __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outputs out) {
-    // one wave per env: the order-dependent per-env logic (NPCs, kinematics,
+    // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
     // status, collisions, respawn, observation head); the LiDAR block of the
-    // observation is filled by k_lidar right after.
+    // observation is filled by k_lidar right after.  Per-agent phases run on
+    // groups of 8 lanes per agent (8 agents per pass) so the window search,
+    // the corner tests and the neighbour ranking are lane-parallel; global
+    // memory is touched in two dependent rounds (state, then route table) and
+    // written once at the end.
+    extern __shared__ __align__(16) unsigned char cars_lds[];
     const int e = blockIdx.x;
     const int tid = threadIdx.x;
-    const int nthr = blockDim.x;
     const int N = p.N;
-    __shared__ EgoLDS el;
-    __shared__ ObsLDS ob;
+    CarsLDS el = carve_cars_lds(cars_lds, N, p.K);
     __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
     NpcLDS* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
 
-    // vector auto-reset of an env whose previous step ended
+    // ---- phase 0: ego state -> LDS (lane = agent).  An env whose previous
+    // step ended starts from its spawns (vector auto-reset; reset +
+    // add_car_with_route, :66-131).
     const bool do_reset = in.auto_reset && p.pending_reset[e];
     const int prev_step = do_reset ? 0 : p.step_count[e];
     const int prev_npcs = TRAFFIC ? (do_reset ? 0 : p.npc.count[e]) : 0;
-    if (do_reset) {
-        for (int i = tid; i < N; i += nthr) {
-            const int g = e * N + i;
-            const int rid = p.ego.route[g];
-            p.ego.x[g] = p.rt.spawn[3 * rid];
-            p.ego.y[g] = p.rt.spawn[3 * rid + 1];
-            p.ego.v[g] = 0.0f;
-            p.ego.h[g] = p.rt.spawn[3 * rid + 2];
-            p.ego.sx[g] = p.ego.x[g]; p.ego.sy[g] = p.ego.y[g]; p.ego.sv[g] = 0.0f; p.ego.sh[g] = p.ego.h[g];
-            p.ego.acc[g] = 0.0f; p.ego.steer[g] = 0.0f; p.ego.prev_dist[g] = 0.0f;
-            p.ego.pa0[g] = 0.0f; p.ego.pa1[g] = 0.0f; p.ego.pidx[g] = 0;
-            p.ego.intent[g] = p.rt.intent[rid]; p.ego.alive[g] = 1;
+    for (int i = tid; i < N; i += WAVE) {
+        const int g = e * N + i;
+        const int rid = p.ego.route[g];
+        el.route[i] = rid;
+        el.a0[i] = in.actions[2 * g];
+        el.a1[i] = in.actions[2 * g + 1];
+        if (do_reset) {
+            const float sx = p.rt.spawn[3 * rid], sy = p.rt.spawn[3 * rid + 1], sh = p.rt.spawn[3 * rid + 2];
+            el.x[i] = sx; el.y[i] = sy; el.v[i] = 0.0f; el.h[i] = sh;
+            el.acc[i] = 0.0f; el.steer[i] = 0.0f; el.prev_dist[i] = 0.0f; el.pa0[i] = 0.0f; el.pa1[i] = 0.0f;
+            el.sx[i] = sx; el.sy[i] = sy; el.sv[i] = 0.0f; el.sh[i] = sh;
+            el.pidx[i] = 0; el.intent[i] = p.rt.intent[rid]; el.alive[i] = 1;
+        } else {
+            el.x[i] = p.ego.x[g]; el.y[i] = p.ego.y[g]; el.v[i] = p.ego.v[g]; el.h[i] = p.ego.h[g];
+            el.acc[i] = p.ego.acc[g]; el.steer[i] = p.ego.steer[g]; el.prev_dist[i] = p.ego.prev_dist[g];
+            el.pa0[i] = p.ego.pa0[g]; el.pa1[i] = p.ego.pa1[g];
+            el.sx[i] = p.ego.sx[g]; el.sy[i] = p.ego.sy[g]; el.sv[i] = p.ego.sv[g]; el.sh[i] = p.ego.sh[g];
+            el.pidx[i] = p.ego.pidx[g]; el.intent[i] = p.ego.intent[g]; el.alive[i] = p.ego.alive[g];
         }
-        __syncthreads();
     }
     const int step_no = prev_step + 1;  // res.step = ++step_count (:137)
     if (tid == 0) p.step_count[e] = step_no;
+    __syncthreads();
 
     STAMP(0);
     int ncnt = 0;
-    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid);
+    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y);
     STAMP(1);
 
-    // ---- ego physics + base reward (:151-163) + status (:165-290); lane = agent
-    for (int i = tid; i < N; i += nthr) {
-        const int g = e * N + i;
-        const int rid = p.ego.route[g];
-        const float* path = p.rt.path + (size_t)rid * (2 * PATH_LEN);
-        Kin k{p.ego.x[g], p.ego.y[g], p.ego.v[g], p.ego.h[g], p.ego.acc[g], p.ego.steer[g]};
-        const bool alive = p.ego.alive[g] != 0;
+    // ---- phase 1: kinematics (:151-163), path index, base reward (:15-46),
+    // status (:165-290).  Lane (grp, sub): agent i0 + grp, sub-task sub.
+    const int grp = tid >> 3, sub = tid & 7;
+    const unsigned long long gmask = 0xFFull << (grp * 8);
+    for (int i0 = 0; i0 < N; i0 += 8) {
+        const int i = i0 + grp;
+        const bool act = i < N;
+        const int ii = act ? i : 0;  // idle groups mirror agent 0 so every lane reaches the ballots
+        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)el.route[ii] * (2 * PATH_LEN));
+        const int pidx0 = el.pidx[ii];
+        const int start_i = pidx0 < 0 ? 0 : pidx0;
+        const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
+        // the 50-point window and the look-ahead target lie in [start_i, start_i + 64): 8 points per lane
+        float2 pt[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int q = start_i + sub * 8 + j;
+            pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+        }
+        const float2 pend = P[PATH_LEN - 1], pprev = P[PATH_LEN - 2], p10 = P[10];
+        Kin k{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
+        const bool alive = act && el.alive[ii] != 0;
         float cH, sH;
-        float rew = 0.0f;
-        uint8_t done = 0, status = ST_ALIVE;
-        int pidx = p.ego.pidx[g];
-        if (alive) {
-            const float thr = in.actions[2 * g], st = in.actions[2 * g + 1];
-            car_update(k, thr, st, in.dt, &cH, &sH);
-            // update_path_index (Car.cpp:47-74), in order over the 50-point
-            // window; loads issued 10 at a time so they overlap
-            {
-                const int start_i = pidx < 0 ? 0 : pidx;
-                const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
-                const float2* P = reinterpret_cast<const float2*>(path);
-                float min_d = __builtin_inff();
-                int best = start_i;
-                for (int base = 0; base < 50; base += 10) {
-                    float2 pt[10];
+        if (alive) car_update(k, el.a0[ii], el.a1[ii], in.dt, &cH, &sH);
+        else sincosf(k.h, &sH, &cH);
+        // Car::update_path_index (Car.cpp:47-74): first minimum over the window, in order
+        float bd = __builtin_inff();
+        int bi = 0x7fffffff;
 #pragma unroll
-                    for (int j = 0; j < 10; ++j) {
-                        int q = start_i + base + j;
-                        pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
-                    }
-#pragma unroll
-                    for (int j = 0; j < 10; ++j) {
-                        if (base + j < cnt) {
-                            const float dx = pt[j].x - k.x;
-                            const float dy = pt[j].y - k.y;
-                            const float d = dx * dx + dy * dy;
-                            if (d < min_d) { min_d = d; best = start_i + base + j; }
-                        }
-                    }
-                }
-                pidx = best;
+        for (int j = 0; j < 8; ++j) {
+            const int off = sub * 8 + j;
+            if (off < cnt) {
+                const float dx = pt[j].x - k.x, dy = pt[j].y - k.y;
+                const float d = dx * dx + dy * dy;
+                if (d < bd) { bd = d; bi = start_i + off; }
             }
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            const float od = __shfl_xor(bd, o);
+            const int oi = __shfl_xor(bi, o);
+            if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+        }
+        const int pidx = alive ? (bi == 0x7fffffff ? start_i : bi) : pidx0;
+        // look-ahead point of the observation (:444-452), picked from the window
+        {
+            const int tidx = pidx + 10 < PATH_LEN - 1 ? pidx + 10 : PATH_LEN - 1;
+            const int toff = tidx - start_i;
+            if (act && toff >= 0 && toff < 64 && sub == (toff >> 3)) {
+                float2 t = pt[0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j) t = ((toff & 7) == j) ? pt[j] : t;
+                el.tgx[i] = t.x;
+                el.tgy[i] = t.y;
+            } else if (act && (toff < 0 || toff >= 64) && sub == 0) {
+                el.tgx[i] = P[tidx].x;
+                el.tgy[i] = P[tidx].y;
+            }
+        }
+        float rew = 0.0f, cur = 0.0f, an = 0.0f, sn = 0.0f;
+        bool succ = false;
+        float ccx[4], ccy[4];
+        car_corners(k.x, k.y, cH, sH, ccx, ccy);
+        if (alive) {
             // compute_progress / compute_stuck / compute_smooth (:15-46)
-            const float gx = path[2 * (PATH_LEN - 1)], gy = path[2 * (PATH_LEN - 1) + 1];
-            const float cur = hypotf(k.x - gx, k.y - gy);
-            const float prev = p.ego.prev_dist[g];
+            cur = hypotf(k.x - pend.x, k.y - pend.y);
+            const float prev = el.prev_dist[ii];
             float r_prog = 0.0f;
             if (prev > 0.0f) {
                 const float progress = prev - cur;
                 const float normalized = (p.max_progress > 0.0f) ? (progress / p.max_progress) : 0.0f;
                 r_prog = p.k_prog * normalized;
             }
-            p.ego.prev_dist[g] = cur;
             const float speed_ms = (k.v * FPS) / SCALE;
             const float r_stuck = (speed_ms < p.v_min) ? p.k_stuck : 0.0f;
-            const float an = k.acc / MAX_ACC;
-            const float sn = k.steer / MAX_STEERING_ANGLE;
-            const float d0 = an - p.ego.pa0[g];
-            const float d1 = sn - p.ego.pa1[g];
-            const float diff2 = d0 * d0 + d1 * d1;
-            const float r_smooth = p.k_sm * diff2;
-            p.ego.pa0[g] = an;
-            p.ego.pa1[g] = sn;
+            an = k.acc / MAX_ACC;
+            sn = k.steer / MAX_STEERING_ANGLE;
+            const float d0 = an - el.pa0[ii];
+            const float d1 = sn - el.pa1[ii];
+            const float r_smooth = p.k_sm * (d0 * d0 + d1 * d1);
             rew = r_prog + r_stuck + r_smooth;
-
-            // status: SUCCESS by the last path segment's axis
-            const float ex = path[2 * (PATH_LEN - 1)], ey = path[2 * (PATH_LEN - 1) + 1];
-            const float px = path[2 * (PATH_LEN - 2)], py = path[2 * (PATH_LEN - 2) + 1];
-            const float dxr = ex - px, dyr = ey - py;
-            bool succ;
-            if (fabs_f(dxr) > fabs_f(dyr)) succ = fabs_f(k.y - ey) < 15.0f && fabs_f(k.x - ex) < 40.0f;
-            else succ = fabs_f(k.x - ex) < 15.0f && fabs_f(k.y - ey) < 40.0f;
-            float ccx[4], ccy[4];
-            car_corners(k.x, k.y, cH, sH, ccx, ccy);
-            if (succ) {
-                done = 1; status = ST_SUCCESS;
-            } else {
-                const float M = 100.0f;
-                bool oos = false, off = false, line = false;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    oos |= ccx[q] < -M || ccx[q] > float(WIDTH) + M || ccy[q] < -M || ccy[q] > float(HEIGHT) + M;
-                if (oos) { done = 1; status = ST_CRASH_WALL; }
-                else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) off |= !is_on_road(ccx[q], ccy[q], p.rw);
-                    if (off) { done = 1; status = ST_CRASH_WALL; }
-                    else {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) line |= hits_yellow_line(ccx[q], ccy[q], p.rw);
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const int q2 = (q + 1) & 3;
-                            const float mx = 0.5f * (ccx[q] + ccx[q2]);
-                            const float my = 0.5f * (ccy[q] + ccy[q2]);
-                            line |= is_line_px((int)mx, (int)my, p.line_stop);
-                        }
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) line |= is_line_px((int)ccx[q], (int)ccy[q], p.line_stop);
-                        if (line) { done = 1; status = ST_CRASH_LINE; }
-                    }
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { el.cx[i][q] = ccx[q]; el.cy[i][q] = ccy[q]; }
-        } else {
-            done = 1;
-            status = ST_DEAD;
-            sincosf(k.h, &sH, &cH);
+            // SUCCESS by the last path segment's axis
+            const float dxr = pend.x - pprev.x, dyr = pend.y - pprev.y;
+            if (fabs_f(dxr) > fabs_f(dyr)) succ = fabs_f(k.y - pend.y) < 15.0f && fabs_f(k.x - pend.x) < 40.0f;
+            else succ = fabs_f(k.x - pend.x) < 15.0f && fabs_f(k.y - pend.y) < 40.0f;
         }
-        el.x[i] = k.x; el.y[i] = k.y; el.v[i] = k.v; el.h[i] = k.h; el.c[i] = cH; el.s[i] = sH;
-        el.pidx[i] = pidx; el.intent[i] = p.ego.intent[g];
-        el.alive[i] = alive; el.done[i] = done; el.status[i] = status; el.rew[i] = rew;
-        el.col[i] = 0ull; el.colnpc[i] = 0;
-        // write back kinematics (respawn may overwrite below)
-        p.ego.x[g] = k.x; p.ego.y[g] = k.y; p.ego.v[g] = k.v; p.ego.h[g] = k.h;
-        p.ego.acc[g] = k.acc; p.ego.steer[g] = k.steer; p.ego.pidx[g] = pidx;
+        // corner tests, one per lane: sub 0-3 corner q (screen margin, road, yellow line,
+        // line mask), sub 4-7 edge midpoint q (line mask)
+        bool oos_q = false, off_q = false, line_q = false;
+        if (alive) {
+            const int q = sub & 3;
+            float qx = ccx[0], qy = ccy[0], rx = ccx[1], ry = ccy[1];
+#pragma unroll
+            for (int u = 1; u < 4; ++u) {
+                if (q == u) { qx = ccx[u]; qy = ccy[u]; rx = ccx[(u + 1) & 3]; ry = ccy[(u + 1) & 3]; }
+            }
+            if (sub < 4) {
+                const float M = 100.0f;
+                oos_q = qx < -M || qx > float(WIDTH) + M || qy < -M || qy > float(HEIGHT) + M;
+                off_q = !is_on_road(qx, qy, p.rw);
+                line_q = hits_yellow_line(qx, qy, p.rw) || is_line_px((int)qx, (int)qy, p.line_stop);
+            } else {
+                const float mx = 0.5f * (qx + rx), my = 0.5f * (qy + ry);
+                line_q = is_line_px((int)mx, (int)my, p.line_stop);
+            }
+        }
+        const bool any_oos = (ballot(oos_q) & gmask) != 0ull;
+        const bool any_off = (ballot(off_q) & gmask) != 0ull;
+        const bool any_line = (ballot(line_q) & gmask) != 0ull;
+        if (act) {
+            if (sub < 4) {
+                reinterpret_cast<float*>(&el.cx[i])[sub] = ccx[sub];
+                reinterpret_cast<float*>(&el.cy[i])[sub] = ccy[sub];
+            }
+            if (sub == 0) {
+                uint8_t done = 0, status = ST_ALIVE;
+                if (!alive) { done = 1; status = ST_DEAD; }
+                else if (succ) { done = 1; status = ST_SUCCESS; }
+                else if (any_oos || any_off) { done = 1; status = ST_CRASH_WALL; }
+                else if (any_line) { done = 1; status = ST_CRASH_LINE; }
+                el.x[i] = k.x; el.y[i] = k.y; el.v[i] = k.v; el.h[i] = k.h; el.c[i] = cH; el.s[i] = sH;
+                el.acc[i] = k.acc; el.steer[i] = k.steer; el.pidx[i] = pidx;
+                if (alive) { el.prev_dist[i] = cur; el.pa0[i] = an; el.pa1[i] = sn; }
+                el.t10x[i] = p10.x; el.t10y[i] = p10.y;
+                el.done[i] = done; el.status[i] = status; el.rew[i] = rew;
+                el.col[i] = 0ull; el.colnpc[i] = 0;
+            }
+        }
     }
     __syncthreads();
 
     STAMP(2);
     // ---- car-car SAT (:292-318): ego pairs (i<j) and ego x NPC, one pair per lane
-    for (int pbase = 0; pbase < N * N; pbase += nthr) {
+    for (int pbase = 0; pbase < N * N; pbase += WAVE) {
         const int pi = pbase + tid;
         if (pi < N * N) {
             const int a = pi / N, b = pi % N;
             if (a < b && el.alive[a] && el.alive[b] &&
-                sat_collide(el.cx[a], el.cy[a], el.c[a], el.s[a], el.cx[b], el.cy[b], el.c[b], el.s[b]))
+                sat_collide(reinterpret_cast<const float*>(&el.cx[a]), reinterpret_cast<const float*>(&el.cy[a]),
+                            el.c[a], el.s[a], reinterpret_cast<const float*>(&el.cx[b]),
+                            reinterpret_cast<const float*>(&el.cy[b]), el.c[b], el.s[b]))
                 atomicOr(&el.col[a], 1ull << b);
         }
     }
     if constexpr (TRAFFIC) {
-        for (int pbase = 0; pbase < N * ncnt; pbase += nthr) {
+        for (int pbase = 0; pbase < N * ncnt; pbase += WAVE) {
             const int pi = pbase + tid;
             if (pi < N * ncnt) {
                 const int a = pi / ncnt, b = pi % ncnt;
-                if (el.alive[a] && sat_collide(el.cx[a], el.cy[a], el.c[a], el.s[a], nl->cx[b], nl->cy[b], nl->c[b], nl->s[b]))
+                if (el.alive[a] && sat_collide(reinterpret_cast<const float*>(&el.cx[a]),
+                                               reinterpret_cast<const float*>(&el.cy[a]), el.c[a], el.s[a],
+                                               nl->cx[b], nl->cy[b], nl->c[b], nl->s[b]))
                     el.colnpc[a] = 1;
             }
         }
@@ -704,7 +781,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
             if ((crash >> i) & 1ull) { el.done[i] = 1; el.status[i] = ST_CRASH_CAR; }
     }
     __syncthreads();
-    for (int i = tid; i < N; i += nthr) {
+    for (int i = tid; i < N; i += WAVE) {
         if (el.done[i]) {
             const uint8_t st = el.status[i];
             if (st == ST_CRASH_CAR) el.rew[i] += p.k_cv;
@@ -740,21 +817,29 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
     }
     __syncthreads();
-    // respawn crashed egos (:339-351); lane = agent
-    for (int i = tid; i < N; i += nthr) {
+    // respawn crashed egos (Car::respawn, Car.cpp:76-84; :339-351) and write the
+    // final ego state back (lane = agent)
+    for (int i = tid; i < N; i += WAVE) {
         const int g = e * N + i;
         out.rew[g] = el.rew[i];
         out.done[g] = el.done[i];
         out.status[g] = el.status[i];
         const uint8_t st = el.status[i];
         if (p.respawn && el.alive[i] && el.done[i] && (st == ST_CRASH_CAR || st == ST_CRASH_WALL || st == ST_CRASH_LINE)) {
-            const float sx = p.ego.sx[g], sy = p.ego.sy[g], sv = p.ego.sv[g], sh = p.ego.sh[g];
-            p.ego.x[g] = sx; p.ego.y[g] = sy; p.ego.v[g] = sv; p.ego.h[g] = sh;
-            p.ego.pidx[g] = 0; p.ego.prev_dist[g] = 0.0f; p.ego.pa0[g] = 0.0f; p.ego.pa1[g] = 0.0f;
-            p.ego.acc[g] = 0.0f; p.ego.steer[g] = 0.0f;
+            const float sh = el.sh[i];
             float s, c;
             sincosf(sh, &s, &c);
-            el.x[i] = sx; el.y[i] = sy; el.v[i] = sv; el.h[i] = sh; el.c[i] = c; el.s[i] = s; el.pidx[i] = 0;
+            el.x[i] = el.sx[i]; el.y[i] = el.sy[i]; el.v[i] = el.sv[i]; el.h[i] = sh; el.c[i] = c; el.s[i] = s;
+            el.pidx[i] = 0; el.prev_dist[i] = 0.0f; el.pa0[i] = 0.0f; el.pa1[i] = 0.0f;
+            el.acc[i] = 0.0f; el.steer[i] = 0.0f;
+            el.tgx[i] = el.t10x[i]; el.tgy[i] = el.t10y[i];  // path[min(0 + 10, 159)]
+        }
+        p.ego.x[g] = el.x[i]; p.ego.y[g] = el.y[i]; p.ego.v[g] = el.v[i]; p.ego.h[g] = el.h[i];
+        p.ego.acc[g] = el.acc[i]; p.ego.steer[g] = el.steer[i]; p.ego.pidx[g] = el.pidx[i];
+        p.ego.prev_dist[g] = el.prev_dist[i]; p.ego.pa0[g] = el.pa0[i]; p.ego.pa1[g] = el.pa1[i];
+        if (do_reset) {
+            p.ego.sx[g] = el.sx[i]; p.ego.sy[g] = el.sy[i]; p.ego.sv[g] = el.sv[i]; p.ego.sh[g] = el.sh[i];
+            p.ego.intent[g] = el.intent[i]; p.ego.alive[g] = el.alive[i];
         }
     }
     __syncthreads();
@@ -764,53 +849,122 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
     // published to HBM for k_lidar together with each agent's candidate mask
     const int nob = N + ncnt;
     const int OB = p.ob_stride;
-    for (int o = tid; o < nob; o += nthr) {
+    for (int o = tid; o < nob; o += WAVE) {
         float x, y, h, c, s;
         if (o < N) { x = el.x[o]; y = el.y[o]; h = el.h[o]; c = el.c[o]; s = el.s[o]; }
         else { const int k = o - N; x = nl->x[k]; y = nl->y[k]; h = nl->h[k]; c = nl->c[k]; s = nl->s[k]; }
         const PxBox bx = aabb_px(x, y, c, s);
-        ob.x0[o] = bx.x0; ob.x1[o] = bx.x1; ob.y0[o] = bx.y0; ob.y1[o] = bx.y1;
-        ob.px[o] = x; ob.py[o] = y; ob.ph[o] = h;
-        p.ob_box[e * OB + o] = make_int4(bx.x0, bx.x1, bx.y0, bx.y1);
+        const int4 b4 = make_int4(bx.x0, bx.x1, bx.y0, bx.y1);
+        el.box[o] = b4;
+        el.px[o] = x; el.py[o] = y; el.ph[o] = h;
+        p.ob_box[e * OB + o] = b4;
     }
-    for (int i = tid; i < N; i += nthr) { ob.cand[i][0] = 0ull; ob.cand[i][1] = 0ull; }
+    for (int i = tid; i < N; i += WAVE) { el.cand[2 * i] = 0ull; el.cand[2 * i + 1] = 0ull; }
     __syncthreads();
     // per-agent candidate boxes: not self, not state-identical to self within
     // 1e-3 (Lidar.cpp:55-62), and within max_dist + 2 px of the agent (no probe
     // beyond max_dist exists, truncation moves a probe < 1 px)
-    for (int pbase = 0; pbase < N * nob; pbase += nthr) {
+    for (int pbase = 0; pbase < N * nob; pbase += WAVE) {
         const int pi = pbase + tid;
         if (pi < N * nob) {
             const int a = pi / nob, o = pi - a * nob;
             const float cx = el.x[a], cy = el.y[a];
             if (o != a && el.alive[a] &&
-                !(fabs_f(ob.px[o] - cx) < 1e-3f && fabs_f(ob.py[o] - cy) < 1e-3f && fabs_f(ob.ph[o] - el.h[a]) < 1e-3f)) {
-                const float ddx = fmaxf(fmaxf((float)ob.x0[o] - cx, cx - (float)ob.x1[o]), 0.0f);
-                const float ddy = fmaxf(fmaxf((float)ob.y0[o] - cy, cy - (float)ob.y1[o]), 0.0f);
+                !(fabs_f(el.px[o] - cx) < 1e-3f && fabs_f(el.py[o] - cy) < 1e-3f && fabs_f(el.ph[o] - el.h[a]) < 1e-3f)) {
+                const int4 bx = el.box[o];
+                const float ddx = fmaxf(fmaxf((float)bx.x - cx, cx - (float)bx.y), 0.0f);
+                const float ddy = fmaxf(fmaxf((float)bx.z - cy, cy - (float)bx.w), 0.0f);
                 const float reach = p.lidar_max + 2.0f;
-                if (ddx * ddx + ddy * ddy <= reach * reach) atomicOr(&ob.cand[a][o >> 6], 1ull << (o & 63));
+                if (ddx * ddx + ddy * ddy <= reach * reach) atomicOr(&el.cand[2 * a + (o >> 6)], 1ull << (o & 63));
             }
         }
     }
     __syncthreads();
-    for (int i = tid; i < N; i += nthr) {
+    for (int i = tid; i < N; i += WAVE) {
         const int g = e * N + i;
-        p.ob_cand[2 * g] = ob.cand[i][0];
-        p.ob_cand[2 * g + 1] = ob.cand[i][1];
+        p.ob_cand[2 * g] = el.cand[2 * i];
+        p.ob_cand[2 * g + 1] = el.cand[2 * i + 1];
     }
 
     STAMP(5);
-    // ---- observation head (:418-520); lane = agent
-    for (int i = tid; i < N; i += nthr) {
-        const int g = e * N + i;
-        float* row = out.obs + (size_t)g * p.D;
-        if (!el.alive[i]) {
-            for (int c = 0; c < OBS_HEAD; ++c) row[c] = 0.0f;
-            for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
-            continue;
+    // ---- observation head (:418-520)
+    const int C = N + (TRAFFIC ? ncnt : 0);
+    if (C <= 8) {
+        // lane (grp, sub): agent i0 + grp, neighbour candidate sub; rank = position
+        // in the stable distance order (== libstdc++ insertion sort, <= 16 elements)
+        for (int i0 = 0; i0 < N; i0 += 8) {
+            const int i = i0 + grp;
+            const bool act = i < N;
+            const int ii = act ? i : 0;
+            const bool alv = act && el.alive[ii] != 0;
+            const float x = el.x[ii], y = el.y[ii], v = el.v[ii], h = el.h[ii];
+            const int j = sub;
+            bool valid = false;
+            float ox = 0.0f, oy = 0.0f, ov = 0.0f, oh = 0.0f;
+            int oi = 0;
+            if (alv && j < C && j != ii) {
+                if (j < N) {
+                    valid = el.alive[j] != 0;
+                    ox = el.x[j]; oy = el.y[j]; ov = el.v[j]; oh = el.h[j]; oi = el.intent[j];
+                } else {
+                    const int kk = j - N;
+                    valid = nl->alive[kk] != 0;
+                    ox = nl->x[kk]; oy = nl->y[kk]; ov = nl->v[kk]; oh = nl->h[kk]; oi = nl->intent[kk];
+                }
+            }
+            const float ddx = ox - x, ddy = oy - y;
+            const float d = valid ? __builtin_sqrtf(ddx * ddx + ddy * ddy) : __builtin_inff();
+            int rank = 0;
+#pragma unroll
+            for (int sft = 1; sft < 8; ++sft) {
+                const int kk = (sub + sft) & 7;
+                const float dk = __shfl(d, (grp << 3) + kk);
+                const int vk = __shfl((int)valid, (grp << 3) + kk);
+                rank += (vk != 0) && (dk < d || (dk == d && kk < j));
+            }
+            const int nb = __builtin_popcountll(ballot(valid) & gmask);
+            if (act) {
+                float* row = out.obs + (size_t)(e * N + i) * p.D;
+                if (!alv) {
+                    for (int cc = sub; cc < OBS_HEAD; cc += 8) row[cc] = 0.0f;
+                } else {
+                    if (sub == 0) {
+                        row[0] = x / float(WIDTH);
+                        row[1] = y / float(HEIGHT);
+                        row[2] = v / PHYSICS_MAX_SPEED;
+                        row[3] = h / PI_F;
+                    } else if (sub == 1) {
+                        const float dxd = el.tgx[i] - x, dyd = el.tgy[i] - y;
+                        row[4] = __builtin_sqrtf(dxd * dxd + dyd * dyd) / float(WIDTH);
+                        row[5] = wrap_angle(atan2f(-dyd, dxd) - h) / PI_F;
+                    }
+                    if (valid && rank < NEIGHBOR_COUNT) {
+                        float* o = row + 6 + 5 * rank;
+                        o[0] = (ox - x) / float(WIDTH);
+                        o[1] = (oy - y) / float(HEIGHT);
+                        o[2] = (ov - v) / PHYSICS_MAX_SPEED;
+                        o[3] = wrap_angle(oh - h) / PI_F;
+                        o[4] = float(oi);
+                    }
+                    if (sub < NEIGHBOR_COUNT && sub >= nb) {
+                        float* o = row + 6 + 5 * sub;
+                        o[0] = o[1] = o[2] = o[3] = o[4] = 0.0f;
+                    }
+                }
+                for (int cc = OBS_HEAD + p.lidar_slots + sub; cc < p.D; cc += 8) row[cc] = 0.0f;
+            }
         }
-        const float* path = p.rt.path + (size_t)p.ego.route[g] * (2 * PATH_LEN);
-        write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row);
+    } else {
+        for (int i = tid; i < N; i += WAVE) {
+            const int g = e * N + i;
+            float* row = out.obs + (size_t)g * p.D;
+            if (!el.alive[i]) {
+                for (int c = 0; c < OBS_HEAD; ++c) row[c] = 0.0f;
+                for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
+                continue;
+            }
+            write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row);
+        }
     }
     STAMP(6);
 }
@@ -1145,8 +1299,9 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
 hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
                        const hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[0], s);
-    if (p.traffic) hipLaunchKernelGGL(k_cars<true>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
-    else hipLaunchKernelGGL(k_cars<false>, dim3(p.E), dim3(WAVE), 0, s, p, in, out);
+    const unsigned cars_lds = (unsigned)cars_lds_bytes(p.N, p.K);
+    if (p.traffic) hipLaunchKernelGGL(k_cars<true>, dim3(p.E), dim3(WAVE), cars_lds, s, p, in, out);
+    else hipLaunchKernelGGL(k_cars<false>, dim3(p.E), dim3(WAVE), cars_lds, s, p, in, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], s);
