@@ -38,7 +38,8 @@ def _inputs():
 VARIANTS = {"": [], "stamps": ["-DMEV_STAMPS"]}
 # timing-only experiment builds (wrong results by construction; never used by the product)
 EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOCARS"],
-               "exp_none": ["-DMEV_EXP_NOROAD", "-DMEV_EXP_NOCARS"], "exp_iters": ["-DMEV_ITERS"]}
+               "exp_none": ["-DMEV_EXP_NOROAD", "-DMEV_EXP_NOCARS"], "exp_iters": ["-DMEV_ITERS"],
+               "stampsx": ["-DMEV_STAMPS", "-DMEV_STAMPS_X"]}
 VARIANTS.update(EXPERIMENTS)
 
 

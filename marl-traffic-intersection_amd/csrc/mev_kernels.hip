@@ -24,14 +24,23 @@ constexpr int WAVE = 64;
 
 // Diagnostic build only (-DMEV_STAMPS): per-env phase timestamps (s_memtime)
 // into SimParams::debug[e*8 + k]; never compiled into the product library.
+// -DMEV_STAMPS_X moves stamps 1-5 into k_cars' physics phase (STAMPX).
 #ifdef MEV_STAMPS
-#define STAMP(k)                                                         \
+#define STAMP_RAW(k)                                                     \
     do {                                                                 \
-        __syncthreads();                                                 \
+        __builtin_amdgcn_wave_barrier();                                 \
         if (threadIdx.x == 0) p.debug[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#ifdef MEV_STAMPS_X
+#define STAMP(k) do { if ((k) == 0 || (k) == 6) STAMP_RAW(k); } while (0)
+#define STAMPX(k) STAMP_RAW(k)
+#else
+#define STAMP(k) STAMP_RAW(k)
+#define STAMPX(k) do {} while (0)
+#endif
 #else
 #define STAMP(k) do {} while (0)
+#define STAMPX(k) do {} while (0)
 #endif
 constexpr int MAXN = 64;
 constexpr int MAXK = 64;
@@ -39,6 +48,16 @@ constexpr int MAXOB = MAXN + MAXK;
 
 // --------------------------------------------------------------- helpers ---
 __device__ inline unsigned long long ballot(bool p) { return __ballot(p); }
+
+// LDS visibility between the lanes of one wave.  k_cars, k_reset and the NPC
+// phase run as single-wave workgroups and k_lidar's waves are independent, so
+// no s_barrier is needed -- and unlike __syncthreads() this does not wait for
+// outstanding global stores.
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ inline float wave_min(float v) {
 #pragma unroll
@@ -207,14 +226,14 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             }
         }
     }
-    __syncthreads();
+    wave_lds_sync();
     if (lane < cnt) {
         float s, c;
         sincosf(nl.h[lane], &s, &c);
         nl.s[lane] = s;
         nl.c[lane] = c;
     }
-    __syncthreads();
+    wave_lds_sync();
 
     // -- sequential controller over NPCs in vector order (Gauss-Seidel, :337-344)
     const float CXf = WIDTH * 0.5f, CYf = HEIGHT * 0.5f;
@@ -320,7 +339,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             nl.pair_ok[j] = pok;
             nl.yield_far[j] = yfar;
         }
-        __syncthreads();
+        wave_lds_sync();
         // scan ghost points path[pidx, min(pidx+120, 160)); first conflicting point wins
         const int g_start = pidx;
         int g_end = pidx + 120;
@@ -363,13 +382,13 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         float cn, sn;
         car_update(kin, thr, steer_cmd, in.dt, &cn, &sn);
         pidx = path_index_update(path, pidx, kin.x, kin.y, lane);
-        __syncthreads();
+        wave_lds_sync();
         if (lane == 0) {
             nl.x[k] = kin.x; nl.y[k] = kin.y; nl.v[k] = kin.v; nl.h[k] = kin.h;
             nl.acc[k] = kin.acc; nl.steer[k] = kin.steer; nl.pidx[k] = pidx;
             nl.c[k] = cn; nl.s[k] = sn;
         }
-        __syncthreads();
+        wave_lds_sync();
     }
 
     // -- NPC-NPC collision: greedy i<j, both removed (:347-356)
@@ -377,7 +396,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
         nl.col[lane] = 0ull;
     }
-    __syncthreads();
+    wave_lds_sync();
     for (int pbase = 0; pbase < cnt * cnt; pbase += WAVE) {
         const int pi = pbase + lane;
         if (pi < cnt * cnt) {
@@ -386,7 +405,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                 atomicOr(&nl.col[a], 1ull << b);
         }
     }
-    __syncthreads();
+    wave_lds_sync();
     unsigned long long alive_m = ballot(lane < cnt && nl.alive[lane]);
     for (int i = 0; i < cnt; ++i) {
         if (!((alive_m >> i) & 1ull)) continue;
@@ -412,13 +431,13 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         kx = nl.x[lane]; ky = nl.y[lane]; kv = nl.v[lane]; kh = nl.h[lane]; ka = nl.acc[lane]; ks = nl.steer[lane];
         kc = nl.c[lane]; ksn = nl.s[lane]; kp = nl.pidx[lane]; kr = nl.route[lane]; ki = nl.intent[lane];
     }
-    __syncthreads();
+    wave_lds_sync();
     if (keep) {
         nl.x[dst] = kx; nl.y[dst] = ky; nl.v[dst] = kv; nl.h[dst] = kh; nl.acc[dst] = ka; nl.steer[dst] = ks;
         nl.c[dst] = kc; nl.s[dst] = ksn; nl.pidx[dst] = kp; nl.route[dst] = kr; nl.intent[dst] = ki; nl.alive[dst] = 1;
     }
     const int newcnt = __builtin_popcountll(keep_m);
-    __syncthreads();
+    wave_lds_sync();
     // store back + corners of the survivors (for ego-NPC SAT)
     if (lane < newcnt) {
         const int g = e * K + lane;
@@ -428,7 +447,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
     }
     if (lane == 0) p.npc.count[e] = newcnt;
-    __syncthreads();
+    wave_lds_sync();
     return newcnt;
 }
 
@@ -599,7 +618,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
     }
     const int step_no = prev_step + 1;  // res.step = ++step_count (:137)
     if (tid == 0) p.step_count[e] = step_no;
-    __syncthreads();
+    wave_lds_sync();
 
     STAMP(0);
     int ncnt = 0;
@@ -631,6 +650,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         float cH, sH;
         if (alive) car_update(k, el.a0[ii], el.a1[ii], in.dt, &cH, &sH);
         else sincosf(k.h, &sH, &cH);
+        STAMPX(1);
         // Car::update_path_index (Car.cpp:47-74): first minimum over the window, in order
         float bd = __builtin_inff();
         int bi = 0x7fffffff;
@@ -665,6 +685,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
                 el.tgy[i] = P[tidx].y;
             }
         }
+        STAMPX(2);
         float rew = 0.0f, cur = 0.0f, an = 0.0f, sn = 0.0f;
         bool succ = false;
         float ccx[4], ccy[4];
@@ -692,6 +713,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
             if (fabs_f(dxr) > fabs_f(dyr)) succ = fabs_f(k.y - pend.y) < 15.0f && fabs_f(k.x - pend.x) < 40.0f;
             else succ = fabs_f(k.x - pend.x) < 15.0f && fabs_f(k.y - pend.y) < 40.0f;
         }
+        STAMPX(3);
         // corner tests, one per lane: sub 0-3 corner q (screen margin, road, yellow line,
         // line mask), sub 4-7 edge midpoint q (line mask)
         bool oos_q = false, off_q = false, line_q = false;
@@ -715,6 +737,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         const bool any_oos = (ballot(oos_q) & gmask) != 0ull;
         const bool any_off = (ballot(off_q) & gmask) != 0ull;
         const bool any_line = (ballot(line_q) & gmask) != 0ull;
+        STAMPX(4);
         if (act) {
             if (sub < 4) {
                 reinterpret_cast<float*>(&el.cx[i])[sub] = ccx[sub];
@@ -734,8 +757,9 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
                 el.col[i] = 0ull; el.colnpc[i] = 0;
             }
         }
+        STAMPX(5);
     }
-    __syncthreads();
+    wave_lds_sync();
 
     STAMP(2);
     // ---- car-car SAT (:292-318): ego pairs (i<j) and ego x NPC, one pair per lane
@@ -762,61 +786,60 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
             }
         }
     }
-    __syncthreads();
+    wave_lds_sync();
 
     STAMP(3);
-    // ---- greedy resolution in (i, j) order, bonuses, team mix, respawn, flags (:292-370)
-    // lane 0 owns the order-dependent scan; masks are 64-bit (N <= 64)
-    if (tid == 0) {
-        unsigned long long donem = 0ull, crash = 0ull;
-        for (int i = 0; i < N; ++i) if (el.done[i] || !el.alive[i]) donem |= 1ull << i;
-        for (int i = 0; i < N; ++i) {
-            if ((donem >> i) & 1ull) continue;
-            const unsigned long long higher = (i == 63) ? 0ull : (~0ull << (i + 1));
-            const unsigned long long hits = el.col[i] & ~donem & higher;
-            if (hits) { donem |= hits | (1ull << i); crash |= hits | (1ull << i); }
-            if (TRAFFIC && el.colnpc[i]) { donem |= 1ull << i; crash |= 1ull << i; }
+    // ---- greedy resolution in (i, j) order, bonuses, team mix, flags (:292-370).
+    // lane = agent (N <= 64); the order-dependent scan runs on wave-uniform masks.
+    {
+        const int i = tid;
+        const bool in_env = i < N;
+        const uint8_t alive_i = in_env ? el.alive[i] : 0;
+        uint8_t done_i = in_env ? el.done[i] : 0, st_i = in_env ? el.status[i] : 0;
+        float rew_i = in_env ? el.rew[i] : 0.0f;
+        const unsigned long long col_i = in_env ? el.col[i] : 0ull;
+        const bool colnpc_i = TRAFFIC && in_env && el.colnpc[i];
+        unsigned long long donem = ballot(in_env && (done_i || !alive_i));
+        const unsigned long long npcm = ballot(colnpc_i);
+        unsigned long long crash = 0ull;
+        const unsigned col_lo = (unsigned)col_i, col_hi = (unsigned)(col_i >> 32);
+        for (int a = 0; a < N; ++a) {
+            if ((donem >> a) & 1ull) continue;
+            const unsigned long long ca = ((unsigned long long)__builtin_amdgcn_readlane(col_hi, a) << 32) |
+                                          (unsigned)__builtin_amdgcn_readlane(col_lo, a);
+            const unsigned long long higher = (a == 63) ? 0ull : (~0ull << (a + 1));
+            const unsigned long long hits = ca & ~donem & higher;
+            if (hits) { donem |= hits | (1ull << a); crash |= hits | (1ull << a); }
+            if (TRAFFIC && ((npcm >> a) & 1ull)) { donem |= 1ull << a; crash |= 1ull << a; }
         }
-        for (int i = 0; i < N; ++i)
-            if ((crash >> i) & 1ull) { el.done[i] = 1; el.status[i] = ST_CRASH_CAR; }
-    }
-    __syncthreads();
-    for (int i = tid; i < N; i += WAVE) {
-        if (el.done[i]) {
-            const uint8_t st = el.status[i];
-            if (st == ST_CRASH_CAR) el.rew[i] += p.k_cv;
-            else if (st == ST_CRASH_WALL || st == ST_CRASH_LINE) el.rew[i] += p.k_co;
-            else if (st == ST_SUCCESS) el.rew[i] += p.k_succ;
+        if ((crash >> i) & 1ull) { done_i = 1; st_i = ST_CRASH_CAR; }
+        if (done_i) {
+            if (st_i == ST_CRASH_CAR) rew_i += p.k_cv;
+            else if (st_i == ST_CRASH_WALL || st_i == ST_CRASH_LINE) rew_i += p.k_co;
+            else if (st_i == ST_SUCCESS) rew_i += p.k_succ;
         }
-    }
-    __syncthreads();
-    if (tid == 0) {
-        if (p.use_team && N > 0) {
+        if (p.use_team && N > 0) {  // sequential sum in agent order, as the reference
             float avg = 0.0f;
-            for (int i = 0; i < N; ++i) avg += el.rew[i];
+            for (int a = 0; a < N; ++a) avg += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), a));
             avg /= float(N);
-            for (int i = 0; i < N; ++i) el.rew[i] = (1.0f - p.alpha) * el.rew[i] + p.alpha * avg;
+            rew_i = (1.0f - p.alpha) * rew_i + p.alpha * avg;
         }
-        bool terminated = false;
-        int alive_cnt = 0, succ_cnt = 0;
-        for (int i = 0; i < N; ++i) {
-            if (!el.alive[i]) continue;
-            ++alive_cnt;
-            if (el.done[i] && el.status[i] == ST_SUCCESS) ++succ_cnt;
-        }
-        if (p.respawn) {
-            if (succ_cnt > 0 && succ_cnt == alive_cnt) terminated = true;
-        } else {
-            for (int i = 0; i < N; ++i) if (el.done[i]) { terminated = true; break; }
-        }
+        const unsigned long long alive_m = ballot(in_env && alive_i);
+        const unsigned long long succ_m = ballot(in_env && alive_i && done_i && st_i == ST_SUCCESS);
+        const unsigned long long done_m = ballot(in_env && done_i);
+        const int alive_cnt = __builtin_popcountll(alive_m), succ_cnt = __builtin_popcountll(succ_m);
+        const bool terminated = p.respawn ? (succ_cnt > 0 && succ_cnt == alive_cnt) : (done_m != 0ull);
         const bool truncated = p.max_steps > 0 && step_no >= p.max_steps;
-        out.term[e] = terminated;
-        out.trunc[e] = truncated;
-        out.alive_cnt[e] = alive_cnt;
-        out.step[e] = step_no;
-        p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
+        if (in_env) { el.done[i] = done_i; el.status[i] = st_i; el.rew[i] = rew_i; }
+        if (tid == 0) {
+            out.term[e] = terminated;
+            out.trunc[e] = truncated;
+            out.alive_cnt[e] = alive_cnt;
+            out.step[e] = step_no;
+            p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
+        }
     }
-    __syncthreads();
+    wave_lds_sync();
     // respawn crashed egos (Car::respawn, Car.cpp:76-84; :339-351) and write the
     // final ego state back (lane = agent)
     for (int i = tid; i < N; i += WAVE) {
@@ -842,7 +865,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
             p.ego.intent[g] = el.intent[i]; p.ego.alive[g] = el.alive[i];
         }
     }
-    __syncthreads();
+    wave_lds_sync();
 
     STAMP(4);
     // ---- LiDAR obstacle table (:374-388): every ego (alive or not), then NPCs,
@@ -860,7 +883,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         p.ob_box[e * OB + o] = b4;
     }
     for (int i = tid; i < N; i += WAVE) { el.cand[2 * i] = 0ull; el.cand[2 * i + 1] = 0ull; }
-    __syncthreads();
+    wave_lds_sync();
     // per-agent candidate boxes: not self, not state-identical to self within
     // 1e-3 (Lidar.cpp:55-62), and within max_dist + 2 px of the agent (no probe
     // beyond max_dist exists, truncation moves a probe < 1 px)
@@ -879,7 +902,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
             }
         }
     }
-    __syncthreads();
+    wave_lds_sync();
     for (int i = tid; i < N; i += WAVE) {
         const int g = e * N + i;
         p.ob_cand[2 * g] = el.cand[2 * i];
@@ -983,14 +1006,35 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 //     inside a road strip or the corner square, so it could not have stopped
 //     the march;
 //  2. cars: for each candidate box, the probes whose real point lies in the
-//     box's slab widened by >= 0.5 px form a superset range of k; those (and
+//     box's real slab (box_lo/box_hi) form a superset range of k; those (and
 //     only below the k of step 1) are probed exactly, in march order.
 // Bit-identical to the sequential march (tests/test_parity_gpu.py,
 // tests/test_gpu_vs_oracle.py).
-// A probe pixel (int)f lies in [x0, x1] only if f lies in (x0 - 1, x1 + 1);
-// the slab used is [x0 - 1.5, x1 + 2.5], so float rounding of the probe
-// position, of the reciprocal and of the accumulated distances can never
-// drop a real hit from the range.
+// The float rounding of the probe position, of the reciprocal and of the
+// accumulated distances is absorbed by the slab margins and by one extra probe
+// index at each end of the range, so a real hit is never dropped.
+
+// atan2 to ~1e-5 rad and wrap to [-pi, pi]: culling only (beam ranges carry one
+// beam of margin); every hit is still decided by exact probes.
+__device__ inline float atan2_fast(float y, float x) {
+    const float ax = fabs_f(x), ay = fabs_f(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    const float t = mn * __builtin_amdgcn_rcpf(fmaxf(mx, 1e-30f));
+    const float s2 = t * t;
+    float r = ((-0.0464964749f * s2 + 0.15931422f) * s2 - 0.327622764f) * s2 * t + t;
+    r = ay > ax ? 1.57079637f - r : r;
+    r = x < 0.0f ? 3.14159274f - r : r;
+    return y < 0.0f ? -r : r;
+}
+
+__device__ inline float wrap_pi_fast(float a) { return a - 6.28318531f * rintf(a * 0.159154943f); }
+
+// Real-coordinate slab of the pixels [lo, hi] of an integer box: (int)f lies
+// in [lo, hi] only if f lies in [lo, hi + 1) (f >= 0: truncation is floor) or
+// in (lo - 1, hi + 1) (f < 0 when lo <= 0); 0.01 px absorbs the float rounding
+// of the probe position (< 1e-4 px) and of the reciprocal.
+__device__ inline float box_lo(int lo) { return (float)(lo > 0 ? lo : lo - 1) - 0.01f; }
+__device__ inline float box_hi(int hi) { return (float)hi + 1.01f; }
 
 // Clip [lo, hi] (distances along the ray) to where coordinate c0 + dc*t lies in [a, b].
 __device__ inline void slab_clip(float c0, float dc, float idc, float a, float b, float& lo, float& hi) {
@@ -1007,17 +1051,34 @@ __device__ inline int lane_rank(unsigned long long mask) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
 }
 
-// LDS visibility between the lanes of one wave (no block barrier: waves are independent)
-__device__ inline void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Per-wave LDS of k_lidar: ag float4[G] (x, y, heading, agent id) of the
-// group's alive agents, dir float2[G*R] beam directions, res int[G*R] road
-// results (kr << 1 | hit).
-size_t lidar_wave_lds_bytes(int G, int R) { return (size_t)G * 16 + (size_t)G * R * 12; }
+// group's alive agents, dir float2[G*R] beam directions, res int[G*R] stop of
+// each beam (k << 1 | hit), and the car-phase segments: seg_jo int[C]
+// (agent << 8 | box), seg_rg int4[C] (three beam ranges lo | count << 16, total),
+// seg_bx int4[C] (the box), seg_beg int[G+1]; C = G * cmax, cmax = the most
+// candidate boxes one agent can have (every other ego, plus the NPC slots).
+struct LidarLayout {
+    int ag, dir, res, seg_jo, seg_rg, seg_bx, seg_beg, bytes;
+};
+
+__host__ __device__ inline int lidar_cand_max(const SimParams& p) { return p.N - 1 + (p.traffic ? p.K : 0); }
+
+__host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax) {
+    LidarLayout L;
+    const int C = G * cmax;
+    int off = 0;
+    L.ag = off; off += G * 16;
+    L.dir = off; off += G * R * 8;
+    L.res = off; off += G * R * 4;
+    off = (off + 15) & ~15;
+    L.seg_rg = off; off += C * 16;
+    L.seg_bx = off; off += C * 16;
+    L.seg_jo = off; off += C * 4;
+    L.seg_beg = off; off += (G + 1) * 4;
+    L.bytes = (off + 15) & ~15;
+    return L;
+}
 
 int lidar_group(int R) {
     // ~256 beams per wave pool: G = 4 agents at R = 64 (measured best of 1..16, tools/kernel_time.py)
@@ -1026,7 +1087,7 @@ int lidar_group(int R) {
 }
 
 template <bool TAB>
-__global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G, int wave_lds) {
+__global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) {
     // Each wave owns a group of G agents (G*R <= max(256, R) beams).  Phase 1
     // computes the beam directions in lockstep; phase 2 marches the road with
     // the group's beams fed to the 64 lanes from a queue, so a lane that
@@ -1042,10 +1103,11 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G, 
     const int a0 = __builtin_amdgcn_readfirstlane((blockIdx.x * (blockDim.x / WAVE) + wv) * G);
     if (a0 >= EN) return;  // wave-uniform exit: the kernel has no block-level barrier
     const int na = EN - a0 < G ? EN - a0 : G;
-    unsigned char* base = lds_raw + (size_t)wv * (size_t)wave_lds;
-    float4* ag = reinterpret_cast<float4*>(base);
-    float2* dir = reinterpret_cast<float2*>(base + (size_t)G * 16);
-    int* res = reinterpret_cast<int*>(base + (size_t)G * 16 + (size_t)G * R * 8);
+    const LidarLayout lay = lidar_layout(G, R, lidar_cand_max(p));
+    unsigned char* base = lds_raw + (size_t)wv * (size_t)lay.bytes;
+    float4* ag = reinterpret_cast<float4*>(base + lay.ag);
+    float2* dir = reinterpret_cast<float2*>(base + lay.dir);
+    int* res = reinterpret_cast<int*>(base + lay.res);
 
     // ---- phase 1: alive agents of the group (compacted), beam directions
     bool alv = false;
@@ -1173,67 +1235,141 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G, 
 #endif
     wave_lds_sync();
 
-    // ---- phase 3: cars (Lidar.cpp:50-80) per alive agent, lane = beam.  The
-    // env's obstacle boxes are loaded once into VGPRs (lane o holds box o) and
-    // broadcast with readlane, so the candidate loop issues no dependent loads.
-    const float d1 = march_dist(p, 1);
-    const int OB = p.ob_stride;  // <= 128
-    int cur_env = -1;
-    int4 vb0 = make_int4(0, 0, 0, 0), vb1 = make_int4(0, 0, 0, 0);
-    for (int j = 0; j < nal; ++j) {
-        const float4 a = ag[j];
-        const int g = __builtin_amdgcn_readfirstlane(__float_as_int(a.w));
-        const int e = g / p.N;
-        if (e != cur_env) {
-            const int4* boxes = p.ob_box + (size_t)e * OB;
-            if (lane < OB) vb0 = boxes[lane];
-            if (lane + WAVE < OB) vb1 = boxes[lane + WAVE];
-            cur_env = e;
-        }
+    // ---- phase 3: cars (Lidar.cpp:50-80) as a list of (agent, box, beam) pairs.
+    // A box can only stop the beams whose ray enters its slab box, i.e. the
+    // beams inside the angular span of its real slab box seen from the agent (+-1 beam):
+    // 3a lists (agent, candidate box) segments, 3b turns each into beam ranges,
+    // 3c packs the pairs of an agent into the 64 lanes (scan + segment lookup)
+    // and resolves each by exact probes inside its slab range, keeping the
+    // earliest stop per beam with an LDS atomicMin on (k << 1 | hit); 3d writes
+    // the LiDAR block.
+    int* seg_jo = reinterpret_cast<int*>(base + lay.seg_jo);
+    int4* seg_rg = reinterpret_cast<int4*>(base + lay.seg_rg);
+    int4* seg_bx = reinterpret_cast<int4*>(base + lay.seg_bx);
+    int* seg_beg = reinterpret_cast<int*>(base + lay.seg_beg);
+    const int OB = p.ob_stride;
+    int M = 0;
+    for (int j = 0; j < nal; ++j) {  // 3a
+        const int g = __builtin_amdgcn_readfirstlane(__float_as_int(ag[j].w));
 #ifdef MEV_EXP_NOCARS
-        const unsigned long long cand0 = 0, cand1 = 0;
+        const unsigned long long c0 = 0, c1 = 0;
 #else
-        const unsigned long long cand0 = p.ob_cand[2 * g], cand1 = p.ob_cand[2 * g + 1];
+        const unsigned long long c0 = p.ob_cand[2 * g], c1 = p.ob_cand[2 * g + 1];
 #endif
-        float* row = out.obs + (size_t)g * p.D + OBS_HEAD;
-        for (int b = lane; b < R; b += WAVE) {
-            const int r = res[j * R + b];
-            int kr = r >> 1;
-            bool hit = (r & 1) != 0;
-            const float2 dd = dir[j * R + b];
-            const float bdx = dd.x, bdy = dd.y;
-            const float bidx = __builtin_amdgcn_rcpf(bdx), bidy = __builtin_amdgcn_rcpf(bdy);
-            // the probes inside a box form the intersection of the x- and y-intervals
+        if (lane == 0) seg_beg[j] = M;
+        const int n0 = __popcll(c0);
+        if ((c0 >> lane) & 1ull) seg_jo[M + lane_rank(c0)] = (j << 8) | lane;
+        if ((c1 >> lane) & 1ull) seg_jo[M + n0 + lane_rank(c1)] = (j << 8) | (lane + WAVE);
+        M += n0 + __popcll(c1);
+    }
+    if (lane == 0) seg_beg[nal] = M;
+    wave_lds_sync();
+    // 3b: beam ranges.  Beam b points along h + rel[b], rel[b] = rel[0] + b*dphi;
+    // the range covers the span of the box's real slab (box_lo/box_hi), with one
+    // beam of margin (fast atan2, error ~1e-5 rad << one beam).
+    const float rel0 = p.rel_angles[0];
+    const float dphi = R > 1 ? (p.rel_angles[R - 1] - rel0) / (float)(R - 1) : 1.0f;
+    const float idphi = 1.0f / dphi;
+    const float period = 6.28318531f * idphi;  // beam indices per revolution
+    for (int m = lane; m < M; m += WAVE) {
+        const int jo = seg_jo[m];
+        const float4 a = ag[jo >> 8];
+        const int e = __float_as_int(a.w) / p.N;
+        const int4 bx = p.ob_box[(size_t)e * OB + (jo & 255)];
+        seg_bx[m] = bx;
+        const float ex0 = box_lo(bx.x), ex1 = box_hi(bx.y);
+        const float ey0 = box_lo(bx.z), ey1 = box_hi(bx.w);
+        int4 rg;
+        if (R == 1 || (a.x > ex0 && a.x < ex1 && a.y > ey0 && a.y < ey1)) {
+            rg = make_int4(0 | (R << 16), 0, 0, R);  // inside the widened box: every beam
+        } else {
+            const float phc = atan2_fast(-(0.5f * (ey0 + ey1) - a.y), 0.5f * (ex0 + ex1) - a.x);
+            float dmin = 0.0f, dmax = 0.0f;
 #pragma unroll
-            for (int wd = 0; wd < 2; ++wd)
-            for (unsigned long long cm = wd ? cand1 : cand0; cm; cm &= cm - 1ull) {
-                const int o = __builtin_ctzll(cm);
-                const int4 vb = wd ? vb1 : vb0;
-                const int4 bx = make_int4(__builtin_amdgcn_readlane(vb.x, o), __builtin_amdgcn_readlane(vb.y, o),
-                                          __builtin_amdgcn_readlane(vb.z, o), __builtin_amdgcn_readlane(vb.w, o));
-                if (kr <= 1) break;
-                // probes that can land in the box: the real slab interval of the
-                // ray, widened by >= 0.5 px, as a superset range of k ...
-                float lo = 0.0f, hi = 1.0e6f;
-                slab_clip(a.x, bdx, bidx, (float)bx.x - 1.5f, (float)bx.y + 2.5f, lo, hi);
-                slab_clip(a.y, bdy, bidy, (float)bx.z - 1.5f, (float)bx.w + 2.5f, lo, hi);
-                if (lo > hi) continue;
-                int ka = (int)(lo * inv_stp) - 1, kb = (int)(hi * inv_stp) + 1;
-                ka = ka < 1 ? 1 : ka;  // no car test at dist == 0
-                kb = kb < kr - 1 ? kb : kr - 1;
-                // ... resolved by exact probes in march order (Lidar.cpp:50-80)
-                for (int kk = ka; kk <= kb; ++kk) {
-                    const float d = march_dist(p, kk);
-                    const int px = (int)(a.x + bdx * d), py = (int)(a.y + bdy * d);
-                    if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) {
-                        kr = kk;
-                        hit = true;
-                        break;
+            for (int c = 0; c < 4; ++c) {
+                const float X = (c & 1) ? ex1 : ex0, Y = (c & 2) ? ey1 : ey0;
+                const float dd = wrap_pi_fast(atan2_fast(-(Y - a.y), X - a.x) - phc);
+                dmin = fminf(dmin, dd);
+                dmax = fmaxf(dmax, dd);
+            }
+            float w = phc + dmin - a.z - rel0;
+            w -= 6.28318531f * floorf(w * 0.159154943f);  // [0, 2*pi)
+            const float ulo = w * idphi, uhi = ulo + (dmax - dmin) * idphi;
+            int lo[3], cn[3];
+#pragma unroll
+            for (int sft = 0; sft < 3; ++sft) {
+                const float sh = (float)(sft - 1) * period;
+                int l0 = (int)floorf(ulo + sh) - 1, l1 = (int)ceilf(uhi + sh) + 1;
+                l0 = l0 < 0 ? 0 : l0;
+                l1 = l1 > R - 1 ? R - 1 : l1;
+                lo[sft] = l0;
+                cn[sft] = l1 >= l0 ? l1 - l0 + 1 : 0;
+            }
+            rg = make_int4(lo[0] | (cn[0] << 16), lo[1] | (cn[1] << 16), lo[2] | (cn[2] << 16), cn[0] + cn[1] + cn[2]);
+        }
+        seg_rg[m] = rg;
+    }
+    wave_lds_sync();
+    const float d1 = march_dist(p, 1);
+    for (int j = 0; j < nal; ++j) {  // 3c
+        const float4 a = ag[j];
+        const int sbeg = seg_beg[j], send = seg_beg[j + 1];
+        for (int cb = sbeg; cb < send; cb += WAVE) {
+            const int nseg = send - cb < WAVE ? send - cb : WAVE;
+            const int cnt = lane < nseg ? seg_rg[cb + lane].w : 0;
+            int incl = cnt;
+#pragma unroll
+            for (int off = 1; off < WAVE; off <<= 1) {
+                const int t = __shfl_up(incl, off);
+                if (lane >= off) incl += t;
+            }
+            const int excl = incl - cnt;
+            const int T = __builtin_amdgcn_readlane(incl, WAVE - 1);
+            for (int q0 = 0; q0 < T; q0 += WAVE) {
+                const int q = q0 + lane;
+                int sm = 0;
+                for (int mm = 1; mm < nseg; ++mm) sm = __builtin_amdgcn_readlane(excl, mm) <= q ? mm : sm;
+                const int r = q - __shfl(excl, sm);
+                if (q < T) {
+                    const int4 rg = seg_rg[cb + sm];
+                    const int4 bx = seg_bx[cb + sm];
+                    const int cA = rg.x >> 16, cB = rg.y >> 16;
+                    const int b = r < cA ? (rg.x & 0xffff) + r
+                                         : (r < cA + cB ? (rg.y & 0xffff) + r - cA : (rg.z & 0xffff) + r - cA - cB);
+                    const int slot = j * R + b;
+                    const int kr = res[slot] >> 1;
+                    const float2 dd = dir[slot];
+                    // probes that can land in the box: the ray's interval inside the
+                    // box's real slab (see box_lo), as a superset range of k ...
+                    float lo = 0.0f, hi = 1.0e6f;
+                    slab_clip(a.x, dd.x, __builtin_amdgcn_rcpf(dd.x), box_lo(bx.x), box_hi(bx.y), lo, hi);
+                    slab_clip(a.y, dd.y, __builtin_amdgcn_rcpf(dd.y), box_lo(bx.z), box_hi(bx.w), lo, hi);
+                    int ka = (int)(fmaxf(lo, 0.0f) * inv_stp) - 1, kb = (int)(fminf(hi, 1.0e6f) * inv_stp) + 1;
+                    ka = ka < 1 ? 1 : ka;  // no car test at dist == 0
+                    kb = kb < kr - 1 ? kb : kr - 1;
+                    if (lo > hi) kb = 0;
+                    // ... resolved by exact probes in march order
+                    for (int kk = ka; kk <= kb; ++kk) {
+                        const float d = march_dist(p, kk);
+                        const int px = (int)(a.x + dd.x * d), py = (int)(a.y + dd.y * d);
+                        if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) {
+                            atomicMin(&res[slot], (kk << 1) | 1);
+                            break;
+                        }
                     }
                 }
             }
-            const float final_dist = hit ? march_dist(p, kr) : p.lidar_max;
-            if (b < p.lidar_slots) row[b] = final_dist * p.lidar_inv;  // Lidar::normalized (:92-98)
+        }
+    }
+    (void)d1;
+    wave_lds_sync();
+    for (int j = 0; j < nal; ++j) {  // 3d: Lidar::normalized (:92-98)
+        const int g = __float_as_int(ag[j].w);
+        float* row = out.obs + (size_t)g * p.D + OBS_HEAD;
+        for (int b = lane; b < p.lidar_slots; b += WAVE) {
+            const int r = res[j * R + b];
+            const float final_dist = (r & 1) ? march_dist(p, r >> 1) : p.lidar_max;
+            row[b] = final_dist * p.lidar_inv;
         }
     }
 }
@@ -1282,7 +1418,7 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
             nl->intent[lane] = p.npc.intent[g]; nl->alive[lane] = p.npc.alive[g];
         }
     }
-    __syncthreads();
+    wave_lds_sync();
     for (int i = lane; i < N; i += WAVE) {
         const int g = e * N + i;
         float* row = out.obs + (size_t)g * p.D;
@@ -1308,14 +1444,17 @@ hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& 
     int G = lidar_group(p.R);
     static const int g_env = [] { const char* v = getenv("MEV_LIDAR_G"); return v ? atoi(v) : 0; }();
     if (g_env > 0 && g_env <= 64 && (size_t)g_env * p.R <= 1024) G = g_env;  // experiments (tools/kernel_time.py)
-    const int wave_lds = (int)((lidar_wave_lds_bytes(G, p.R) + 15) / 16 * 16);
-    constexpr int WPB = 4;  // waves per block
+    // LDS: shrink the group, then the waves per block, to stay within 40 KB (64 KB hard) per block
+    int wpb = 4;
+    while (G > 1 && wpb * lidar_layout(G, p.R, lidar_cand_max(p)).bytes > 40 * 1024) G = (G + 1) / 2;
+    const int wave_lds = lidar_layout(G, p.R, lidar_cand_max(p)).bytes;
+    while (wpb > 1 && wpb * wave_lds > 64 * 1024) wpb /= 2;
     const int groups = (p.E * p.N + G - 1) / G;
-    const unsigned blocks = (unsigned)((groups + WPB - 1) / WPB);
+    const unsigned blocks = (unsigned)((groups + wpb - 1) / wpb);
     if (p.dist_tab)
-        hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(WPB * WAVE), WPB * wave_lds, s, p, out, G, wave_lds);
+        hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(wpb * WAVE), wpb * wave_lds, s, p, out, G);
     else
-        hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(WPB * WAVE), WPB * wave_lds, s, p, out, G, wave_lds);
+        hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(wpb * WAVE), wpb * wave_lds, s, p, out, G);
     e = hipGetLastError();
     if (ev && e == hipSuccess) (void)hipEventRecord(ev[2], s);
     return e;

@@ -1,7 +1,7 @@
 """Diagnostic: per-phase cycle shares of the step kernel (stamps build).
 
 Builds/loads libmarlenv_hip_stamps.so (-DMEV_STAMPS: s_memtime at each phase
-boundary of k_step, lane 0 of every env) and prints median / mean cycles per
+boundary of k_cars, lane 0 of every env) and prints median / mean cycles per
 phase.  Shares only — the stamps' barriers perturb the schedule, so the
 absolute length of this build is not the product kernel's.
     MEV_LIB_VARIANT=stamps python tools/phase_profile.py [--envs 4096 --agents 8 --rays 64 --traffic 0]
@@ -16,7 +16,10 @@ import numpy as np  # noqa: E402
 
 import pkgload  # noqa: E402
 
-PHASES = ["npc", "physics+status", "SAT", "resolve+respawn", "lidar(obstacles+march)", "obs head"]
+PHASES = ["npc", "physics+status", "SAT", "resolve+respawn+writeback", "obstacles+candidates", "obs head"]
+# MEV_LIB_VARIANT=stampsx: stamps 1-5 inside the physics phase
+PHASES_X = ["npc+car_update", "path index+target", "reward+success", "corner tests", "LDS writes",
+            "rest of the kernel"]
 
 
 def main():
@@ -43,7 +46,8 @@ def main():
     tot = d.sum(1)
     print(f"envs={args.envs} agents={args.agents} rays={args.rays} traffic={args.traffic}: "
           f"total per env median {np.median(tot):.0f} cycles")
-    for k, name in enumerate(PHASES):
+    names = PHASES_X if os.environ.get("MEV_LIB_VARIANT") == "stampsx" else PHASES
+    for k, name in enumerate(names):
         print(f"  {name:24s} median {np.median(d[:, k]):9.0f}  mean {d[:, k].mean():9.0f}  share {d[:, k].sum() / tot.sum():6.1%}")
 
 
