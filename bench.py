@@ -10,10 +10,11 @@ uniform [-1, 1) f32) and obs [E, 8, 95] / reward / done / status /
 terminated / truncated written to HBM.
 
 --gpus N > 1 (one process per GPU, torchrun): every rank steps its own 4096
-envs (weak scaling: envs are independent, no data-path collective inside a
-step) and each step's packed outputs are gathered to rank 0 with one RCCL
-gather over xGMI (sharding.py), overlapped with the next step (double
-buffered).
+envs (weak scaling: envs are independent, so the step has no data-path
+collective; a barrier and a max-over-ranks reduction bracket the timed
+region).  --gather adds the optional output collection of sharding.py: each
+step's packed outputs gathered to rank 0 with one RCCL gather over xGMI,
+overlapped with the next step (double buffered).
 
 Prints ONE JSON line on rank 0, including "roofline" for the dominant kernel
 (k_lidar; device durations from HIP events the library records on its stream
@@ -85,7 +86,8 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--envs", type=int, default=E_PER_GPU, help="envs per GPU")
-    ap.add_argument("--no-gather", action="store_true", help="skip the per-step RCCL gather to rank 0")
+    ap.add_argument("--gather", action="store_true",
+                    help="also gather every step's packed outputs to rank 0 (one RCCL gather over xGMI)")
     ap.add_argument("--no-kernel-events", action="store_true", help="do not record per-kernel HIP events")
     ap.add_argument("--event-every", type=int, default=4, help="record the per-kernel events on every n-th step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -124,7 +126,7 @@ def main():
     layout = sharding.PackedOutputs(E, N, D)  # every rank steps E envs: the gather needs no padding
     bufs = [torch.zeros(layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
     ptrs = [layout.pointers(b.data_ptr()) for b in bufs]
-    gather_on = world > 1 and not args.no_gather
+    gather_on = world > 1 and args.gather
     stacked = torch.empty((world, layout.nbytes), dtype=torch.uint8, device=dev) if gather_on and rank == 0 else None
     works = [None, None]
     env.reset(device=True)

@@ -1014,6 +1014,28 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 // accumulated distances is absorbed by the slab margins and by one extra probe
 // index at each end of the range, so a real hit is never dropped.
 
+// Distance along a beam from its real point (fx, fy) over which every probe is
+// provably on screen and on the road (margin 1.5 px > the < 1 px truncation
+// shift).  Inside a strip the bound is directional (distance to the strip edge
+// the ray is heading for); in the corner square it is the distance to the
+// grass disc or the square's edge; plus the distance to the screen edge.
+__device__ inline float road_safe(float fx, float fy, float dx, float dy, float idx, float idy, float iadx,
+                                  float iady, float rwm, float ccen, float crf) {
+    const float rx = fx - 375.0f, ry = fy - 375.0f;
+    const float ax = fabs_f(rx), ay = fabs_f(ry);
+    const bool in_x = ax < rwm, in_y = ay < rwm;
+    const float sx = in_x ? rwm * iadx - rx * idx : 0.0f;
+    const float sy = in_y ? rwm * iady - ry * idy : 0.0f;
+    // corner square: road outside the grass disc on its outer corner
+    // (approximate sqrt: bound only, extra 0.05 px margin)
+    const float qx = ax - ccen, qy = ay - ccen;
+    const float corner = fminf(__builtin_amdgcn_sqrtf(qx * qx + qy * qy) - crf, fminf(ccen - ax, ccen - ay)) - 1.55f;
+    const float road = (in_x | in_y) ? fmaxf(sx, sy) : (fmaxf(ax, ay) < ccen ? corner : 0.0f);
+    const float tx = (dx > 0.0f ? 748.5f - fx : fx - 0.5f) * iadx;
+    const float ty = (dy > 0.0f ? 748.5f - fy : fy - 0.5f) * iady;
+    return fminf(road, fminf(tx, ty));
+}
+
 // atan2 to ~1e-5 rad and wrap to [-pi, pi]: culling only (beam ranges carry one
 // beam of margin); every hit is still decided by exact probes.
 __device__ inline float atan2_fast(float y, float x) {
@@ -1053,7 +1075,7 @@ __device__ inline int lane_rank(unsigned long long mask) {
 
 
 // Per-wave LDS of k_lidar: ag float4[G] (x, y, heading, agent id) of the
-// group's alive agents, dir float2[G*R] beam directions, res int[G*R] stop of
+// group's alive agents, bm float4[G*R] beams (origin x, y, direction dx, dy), res int[G*R] stop of
 // each beam (k << 1 | hit), and the car-phase segments: seg_jo int[C]
 // (agent << 8 | box), seg_rg int4[C] (three beam ranges lo | count << 16, total),
 // seg_bx int4[C] (the box), seg_beg int[G+1]; C = G * cmax, cmax = the most
@@ -1069,7 +1091,7 @@ __host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax) {
     const int C = G * cmax;
     int off = 0;
     L.ag = off; off += G * 16;
-    L.dir = off; off += G * R * 8;
+    L.dir = off; off += G * R * 16;
     L.res = off; off += G * R * 4;
     off = (off + 15) & ~15;
     L.seg_rg = off; off += C * 16;
@@ -1106,7 +1128,7 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
     const LidarLayout lay = lidar_layout(G, R, lidar_cand_max(p));
     unsigned char* base = lds_raw + (size_t)wv * (size_t)lay.bytes;
     float4* ag = reinterpret_cast<float4*>(base + lay.ag);
-    float2* dir = reinterpret_cast<float2*>(base + lay.dir);
+    float4* bm = reinterpret_cast<float4*>(base + lay.dir);
     int* res = reinterpret_cast<int*>(base + lay.res);
 
     // ---- phase 1: alive agents of the group (compacted), beam directions
@@ -1126,18 +1148,6 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
         }
     }
     wave_lds_sync();
-    for (int j = 0; j < nal; ++j) {
-        const float h = ag[j].z;
-        for (int b = lane; b < R; b += WAVE) {
-            float sn, cs;
-            sincosf(h + p.rel_angles[b], &sn, &cs);  // Lidar.cpp:24-26
-            dir[j * R + b] = make_float2(cs, -sn);
-        }
-    }
-    wave_lds_sync();
-
-    // ---- phase 2: pooled road + screen march (Lidar.cpp:31-48, first stop wins)
-    const int total = nal * R;
     const float stp = p.lidar_step;
     const int S = p.lidar_steps;
     const float rwf = (float)p.irw;
@@ -1146,22 +1156,43 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
     const float crf = CORNER_RADIUS, ccen = rwf + crf;
     const float cr2p1 = crf * crf + 1.0f;
     const float rwm = rwf - 1.5f;
-    const float invR = 1.0f / (float)R;
+    // directions, and the first probe the march has to evaluate: probe 0 is
+    // only screen-tested (no road test at dist 0); if the car centre is on
+    // screen, every probe within the safe distance from it is skipped too
+    for (int j = 0; j < nal; ++j) {
+        const float4 a = ag[j];
+        for (int b = lane; b < R; b += WAVE) {
+            float sn, cs;
+            sincosf(a.z + p.rel_angles[b], &sn, &cs);  // Lidar.cpp:24-26
+            const float dx = cs, dy = -sn;
+            bm[j * R + b] = make_float4(a.x, a.y, dx, dy);
+            const int px = (int)a.x, py = (int)a.y;
+            const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
+            int k1 = 0;
+            if (pmax < (unsigned)WIDTH) {
+                const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
+                const float safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
+                k1 = (safe >= two_stp) ? (int)(safe * inv_stp) : 1;
+            }
+            res[j * R + b] = k1;  // start probe of the march (phase 2)
+        }
+    }
+    wave_lds_sync();
+
+    // ---- phase 2: pooled road + screen march (Lidar.cpp:31-48, first stop wins)
+    const int total = nal * R;
     int next = total < WAVE ? total : WAVE;
     int q = lane < total ? lane : -1;
     float cx = 0.0f, cy = 0.0f, dx = 0.0f, dy = 0.0f, idx = 0.0f, idy = 0.0f, iadx = 0.0f, iady = 0.0f;
     int k = 0;
     auto load_beam = [&](int qq) {
-        int j = (int)((float)qq * invR);
-        j = (j + 1) * R <= qq ? j + 1 : (j * R > qq ? j - 1 : j);
-        const float4 a = ag[j];
-        const float2 d = dir[qq];
-        cx = a.x; cy = a.y; dx = d.x; dy = d.y;
+        const float4 r = bm[qq];
+        cx = r.x; cy = r.y; dx = r.z; dy = r.w;
         idx = __builtin_amdgcn_rcpf(dx);
         idy = __builtin_amdgcn_rcpf(dy);
         iadx = fabs_f(idx);
         iady = fabs_f(idy);
-        k = 0;
+        k = res[qq];
     };
     if (q >= 0) load_beam(q);
 #ifdef MEV_ITERS
@@ -1172,51 +1203,30 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
     q = -1;
 #endif
     while (ballot(q >= 0) != 0ull) {
-        bool fin = false;
-        if (q >= 0) {
-            const float d = TAB ? p.dist_tab[k] : (float)k * stp;
-            const float fx = cx + dx * d;
-            const float fy = cy + dy * d;
-            const int px = (int)fx, py = (int)fy;
-            // exact reference predicates at the truncated pixel: screen, then
-            // (k > 0) road == RoadGeometry::is_on_road at integer pixels:
-            //   on_road <=> dist^2 to the grass-disc centre >= cr^2 + 1
-            //               and (in a strip: min(ax, ay) <= rw  or  corner square: max <= rw + cr)
-            const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
-            const bool off_screen = pmax >= (unsigned)WIDTH;
-            const float iax = fabs_f((float)(px - 375)), iay = fabs_f((float)(py - 375));
-            const float qdx = iax - ccen, qdy = iay - ccen;
-            const float onv = fmaxf(fminf(fminf(iax, iay) - rwf, fmaxf(iax, iay) - ccen), cr2p1 - (qdx * qdx + qdy * qdy));
-            const bool off_road = (k > 0) & (onv > 0.0f);
-            if (off_screen | off_road) {
-                res[q] = (k << 1) | (off_screen ? 0 : 1);
-                fin = true;
-            } else {
-                // distance along the ray that provably keeps every truncated
-                // probe on screen and on the road (margin 1.5 px > the < 1 px
-                // truncation shift): inside a strip the bound is directional
-                // (the distance to the strip edge the ray is heading for)
-                const float rx = fx - 375.0f, ry = fy - 375.0f;
-                const float ax = fabs_f(rx), ay = fabs_f(ry);
-                const bool in_x = ax < rwm, in_y = ay < rwm;
-                const float sx = in_x ? rwm * iadx - rx * idx : 0.0f;
-                const float sy = in_y ? rwm * iady - ry * idy : 0.0f;
-                // corner square: road outside the grass disc on its outer corner
-                // (approximate sqrt: bound only, extra 0.05 px margin)
-                const float qx = ax - ccen, qy = ay - ccen;
-                const float corner = fminf(__builtin_amdgcn_sqrtf(qx * qx + qy * qy) - crf, fminf(ccen - ax, ccen - ay)) - 1.55f;
-                const float road = (in_x | in_y) ? fmaxf(sx, sy) : (fmaxf(ax, ay) < ccen ? corner : 0.0f);
-                const float tx = (dx > 0.0f ? 748.5f - fx : fx - 0.5f) * iadx;
-                const float ty = (dy > 0.0f ? 748.5f - fy : fy - 0.5f) * iady;
-                const float safe = fminf(road, fminf(tx, ty));
-                // probes k+1 .. k+j-1 lie within (j-1)*step <= safe of this point
-                k += (safe >= two_stp) ? (int)(safe * inv_stp) : 1;
-                if (k >= S) {
-                    res[q] = S << 1;
-                    fin = true;
-                }
-            }
-        }
+        // branch-free body: every lane evaluates its probe k; idle lanes only skip the store
+        const bool act = q >= 0;
+        const bool past = k >= S;
+        const int kc = past ? S - 1 : k;
+        const float d = TAB ? p.dist_tab[kc] : (float)kc * stp;
+        const float fx = cx + dx * d;
+        const float fy = cy + dy * d;
+        const int px = (int)fx, py = (int)fy;
+        // exact reference predicates at the truncated pixel: screen, then
+        // (k > 0) road == RoadGeometry::is_on_road at integer pixels:
+        //   on_road <=> dist^2 to the grass-disc centre >= cr^2 + 1
+        //               and (in a strip: min(ax, ay) <= rw  or  corner square: max <= rw + cr)
+        const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
+        const bool off_screen = pmax >= (unsigned)WIDTH;
+        const float iax = fabs_f((float)(px - 375)), iay = fabs_f((float)(py - 375));
+        const float qdx = iax - ccen, qdy = iay - ccen;
+        const float onv = fmaxf(fminf(fminf(iax, iay) - rwf, fmaxf(iax, iay) - ccen), cr2p1 - (qdx * qdx + qdy * qdy));
+        const bool stop = !past & (off_screen | ((k > 0) & (onv > 0.0f)));
+        const float safe = road_safe(fx, fy, dx, dy, idx, idy, iadx, iady, rwm, ccen, crf);
+        // probes k+1 .. k+j-1 lie within (j-1)*step <= safe of this point
+        const int kn = k + ((safe >= two_stp) ? (int)(safe * inv_stp) : 1);
+        const bool fin = act & (past | stop | (kn >= S));
+        if (fin) res[q] = stop ? ((k << 1) | (off_screen ? 0 : 1)) : (S << 1);
+        k = kn;
 #ifdef MEV_ITERS
         ++iters;
 #endif
@@ -1338,7 +1348,8 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
                                          : (r < cA + cB ? (rg.y & 0xffff) + r - cA : (rg.z & 0xffff) + r - cA - cB);
                     const int slot = j * R + b;
                     const int kr = res[slot] >> 1;
-                    const float2 dd = dir[slot];
+                    const float4 bq = bm[slot];
+                    const float2 dd = make_float2(bq.z, bq.w);
                     // probes that can land in the box: the ray's interval inside the
                     // box's real slab (see box_lo), as a superset range of k ...
                     float lo = 0.0f, hi = 1.0e6f;
