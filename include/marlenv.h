@@ -177,6 +177,26 @@ int mev_set_state(mev_handle* h, const mev_state* in);
 int mev_device_outputs(mev_handle* h, float** obs, float** reward, uint8_t** done, uint8_t** status,
                        uint8_t** terminated, uint8_t** truncated);
 
+/* Route randomisation at reset (the reference's test.py draws
+ * a random route from the mapping on every reset, test.py:36-39,118-119): with
+ * count > 0, every reset -- mev_reset and the MEV_AUTO_RESET of mev_step --
+ * draws each agent's route uniformly from routes[0..count) (Philox keyed by the
+ * handle seed, the reset counter, env and agent).  count = 0 restores fixed
+ * routes (mev_set_ego_routes), the reference env.py behaviour. */
+int mev_set_reset_routes(mev_handle* h, const int32_t* routes, int32_t count);
+
+/* Device snapshots for batched rollbacks (EnvState +
+ * get_state/set_state, reference cpp/EnvState.h:9-15, IntersectionEnv.cpp:394-416):
+ * the whole state of every env plus the last step's outputs, in one
+ * self-describing buffer of mev_snapshot_size bytes.  With MEV_DEVICE_PTRS the
+ * buffer (and env_mask) live on the handle's device and the copies are
+ * device-to-device.  mev_restore restores every env (env_mask NULL; also the
+ * handle's Philox counter) or only the envs with env_mask[e] != 0; afterwards
+ * mev_get_outputs returns the snapshot's outputs. */
+int mev_snapshot_size(mev_handle* h, uint64_t* bytes);
+int mev_snapshot(mev_handle* h, void* dst, uint32_t flags);
+int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_t flags);
+
 /* Diagnostics: spawns dropped because max_npcs was full (cumulative). */
 int mev_npc_overflow(mev_handle* h, int64_t* count);
 /* Diagnostics: per-env phase timestamps [E][8] of the last step; all zero

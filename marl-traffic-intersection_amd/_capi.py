@@ -32,7 +32,8 @@ EXPORTED = (
     "mev_default_traffic_routes", "mev_reset", "mev_step", "mev_get_outputs", "mev_get_state", "mev_set_state",
     "mev_device_outputs", "mev_npc_overflow", "mev_use_own_stream", "mev_debug_stamps",
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
-    "mev_kernel_timing", "mev_kernel_times",
+    "mev_kernel_timing", "mev_kernel_times", "mev_set_reset_routes", "mev_snapshot_size", "mev_snapshot",
+    "mev_restore",
 )
 
 
@@ -126,6 +127,10 @@ def load_library(variant: str = None):
     L.mev_use_own_stream.argtypes = [_vp]
     L.mev_debug_stamps.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64)]
     L.mev_kernel_timing.argtypes = [_vp, ctypes.c_int32]
+    L.mev_set_reset_routes.argtypes = [_vp, i32p, ctypes.c_int32]
+    L.mev_snapshot_size.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64)]
+    L.mev_snapshot.argtypes = [_vp, _vp, ctypes.c_uint32]
+    L.mev_restore.argtypes = [_vp, _vp, _vp, ctypes.c_uint32]
     L.mev_kernel_times.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_int64)]
     L.mev_configure.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
@@ -334,10 +339,12 @@ class Handle:
         _check(self._lib.mev_step(self._h, ctypes.byref(a)))
         return out
 
-    def get_outputs(self, out: Optional[dict] = None):
+    def get_outputs(self, out: Optional[dict] = None, device: bool = False):
+        """Outputs of the last step/reset/restore; device=True: `out` holds device buffers (D2D copies)."""
         out = out or self.alloc_outputs()
         _check(self._lib.mev_get_outputs(self._h, *[_ptr(out.get(k)) for k in (
-            "obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step")], 0))
+            "obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step")],
+            MEV_DEVICE_PTRS if device else 0))
         return out
 
     def observations(self) -> np.ndarray:
@@ -394,6 +401,30 @@ class Handle:
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
         _check(self._lib.mev_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
         return a.value, b.value, n.value
+
+    def set_reset_routes(self, routes):
+        """Draw every agent's route from `routes` at each reset (empty: fixed routes)."""
+        r = np.ascontiguousarray(np.asarray(routes, np.int32).reshape(-1))
+        _check(self._lib.mev_set_reset_routes(self._h, r.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)) if r.size
+                                              else None, int(r.size)))
+
+    def snapshot_size(self) -> int:
+        n = ctypes.c_uint64()
+        _check(self._lib.mev_snapshot_size(self._h, ctypes.byref(n)))
+        return n.value
+
+    def snapshot(self, dst=None, device: bool = False):
+        """Whole-state snapshot into `dst` (host uint8 array, or a device buffer/tensor with device=True)."""
+        if dst is None:
+            if device:
+                raise ValueError("device snapshots need a caller-provided device buffer")
+            dst = np.zeros(self.snapshot_size(), np.uint8)
+        _check(self._lib.mev_snapshot(self._h, _ptr(dst), MEV_DEVICE_PTRS if device else 0))
+        return dst
+
+    def restore(self, src, env_mask=None, device: bool = False):
+        mask = None if env_mask is None else (env_mask if device else np.ascontiguousarray(env_mask, np.uint8))
+        _check(self._lib.mev_restore(self._h, _ptr(src), _ptr(mask), MEV_DEVICE_PTRS if device else 0))
 
     def npc_overflow(self) -> int:
         v = ctypes.c_int64()

@@ -64,6 +64,9 @@ struct mev_handle {
     int32_t* d_intent = nullptr;
     float* d_rel = nullptr;
     int32_t* d_traffic = nullptr;
+    int32_t* d_reset_routes = nullptr;  // [nroutes]: pool for per-reset route draws
+    uint8_t* d_snap_stage = nullptr;    // device copy of a host snapshot (masked restore)
+    size_t snap_stage_bytes = 0;
     uint64_t rng_counter = 0;
     // per-kernel timing (mev_kernel_timing): 3 events per step, folded into sums when the ring fills
     std::vector<hipEvent_t> tev;
@@ -104,6 +107,7 @@ struct mev_handle {
     }
     ~mev_handle() {
         free_timing();
+        if (d_snap_stage) (void)hipFree(d_snap_stage);
         for (void* p : allocs) (void)hipFree(p);
         if (own_stream) (void)hipStreamDestroy(own_stream);
     }
@@ -231,6 +235,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&h->d_actions, EN * 2); A(&h->d_spawn, size_t(E)); A(&h->d_mask, size_t(E));
     A(&h->d_paths, h->h_paths.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
     A(&h->d_rel, rel.size()); A(&h->d_traffic, size_t(h->P) * size_t(h->P));
+    A(&h->d_reset_routes, size_t(h->P) * size_t(h->P));
     float* d_dist = nullptr;
     if (!dist_mul_exact) A(&d_dist, dists.size());
     if (err != hipSuccess) {
@@ -296,6 +301,8 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     p.rel_angles = h->d_rel;
     p.traffic_routes = h->d_traffic;
     p.n_traffic_routes = int(h->h_traffic.size());
+    p.reset_routes = h->d_reset_routes;
+    p.n_reset_routes = 0;
     *out = h;
     // initial state = a reset (the reference env.py constructor ends with reset(), env.py:136)
     return mev_reset(h, nullptr, nullptr, 0);
@@ -522,7 +529,7 @@ int mev_reset(mev_handle* h, const uint8_t* env_mask, float* obs, uint32_t flags
     }
     mev::Outputs o = h->internal;
     if (dev && obs) o.obs = obs;
-    HIP_TRY(mev::launch_reset(h->sp, d_mask, o, h->stream));
+    HIP_TRY(mev::launch_reset(h->sp, d_mask, o, h->stream, h->rng_counter++));
     h->last.obs = o.obs;
     if (!dev) {
         if (obs) HIP_TRY(hipMemcpyAsync(obs, o.obs, size_t(h->cfg.num_envs) * size_t(h->cfg.num_agents) * size_t(h->D) * sizeof(float),
@@ -681,6 +688,178 @@ int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* 
     *steps = h->t_steps;
     h->t_cars_ms = h->t_lidar_ms = 0.0;
     h->t_steps = 0;
+    return MEV_OK;
+}
+
+int mev_set_reset_routes(mev_handle* h, const int32_t* routes, int32_t count) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (count < 0 || count > h->nroutes) return fail(MEV_E_INVALID, "count must be in [0, number of routes]");
+    if (count > 0 && !routes) return fail(MEV_E_INVALID, "null routes");
+    for (int32_t i = 0; i < count; ++i)
+        if (routes[i] < 0 || routes[i] >= h->nroutes) return fail(MEV_E_RANGE, "route id out of range");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (count > 0) {
+        HIP_TRY(hipMemcpyAsync(h->d_reset_routes, routes, size_t(count) * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    h->sp.n_reset_routes = count;
+    return MEV_OK;
+}
+
+// ---- device snapshots: header + every state field + the last outputs, each
+// field [E][bytes per env] at a 256-B aligned offset
+namespace {
+struct SnapField {
+    uint8_t* live;     // device field (state, or the outputs the snapshot reads)
+    uint8_t* restore;  // where mev_restore writes it
+    size_t bpe;        // bytes per env
+};
+struct SnapHeader {
+    uint32_t magic, version;
+    int32_t E, N, K, D, R, nfields;
+    uint64_t rng_counter, total_bytes;
+    uint8_t pad[16];
+};
+static_assert(sizeof(SnapHeader) == 64, "snapshot header");
+constexpr uint32_t kSnapMagic = 0x5356454du;  // "MEVS"
+
+std::vector<SnapField> snap_fields(mev_handle* h) {
+    const size_t N = size_t(h->cfg.num_agents), K = size_t(h->cfg.max_npcs), D = size_t(h->D);
+    std::vector<SnapField> f;
+    auto add = [&](void* live, void* restore, size_t bpe) {
+        if (bpe) f.push_back({static_cast<uint8_t*>(live), static_cast<uint8_t*>(restore), bpe});
+    };
+#define SNAP(name, dev, n, T) add(h->sp.dev, h->sp.dev, (std::string(#n) == "EN" ? N : std::string(#n) == "EK" ? K : 1) * sizeof(T));
+    STATE_FIELDS(SNAP)
+#undef SNAP
+    add(h->sp.pending_reset, h->sp.pending_reset, 1);
+    const mev::Outputs& L = h->last;
+    const mev::Outputs& I = h->internal;
+    add(L.obs ? L.obs : I.obs, I.obs, N * D * sizeof(float));
+    add(L.rew ? L.rew : I.rew, I.rew, N * sizeof(float));
+    add(L.done ? L.done : I.done, I.done, N);
+    add(L.status ? L.status : I.status, I.status, N);
+    add(L.term ? L.term : I.term, I.term, 1);
+    add(L.trunc ? L.trunc : I.trunc, I.trunc, 1);
+    add(L.alive_cnt ? L.alive_cnt : I.alive_cnt, I.alive_cnt, sizeof(int32_t));
+    add(L.step ? L.step : I.step, I.step, sizeof(int32_t));
+    return f;
+}
+
+size_t snap_offsets(const std::vector<SnapField>& f, size_t E, std::vector<size_t>* off) {
+    size_t o = sizeof(SnapHeader);
+    for (const SnapField& x : f) {
+        o = (o + 255) & ~size_t(255);
+        if (off) off->push_back(o);
+        o += x.bpe * E;
+    }
+    return o;
+}
+}  // namespace
+
+int mev_snapshot_size(mev_handle* h, uint64_t* bytes) {
+    if (!h || !bytes) return fail(MEV_E_INVALID, "null argument");
+    *bytes = snap_offsets(snap_fields(h), size_t(h->cfg.num_envs), nullptr);
+    return MEV_OK;
+}
+
+int mev_snapshot(mev_handle* h, void* dst, uint32_t flags) {
+    if (!h || !dst) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
+    const size_t E = size_t(h->cfg.num_envs);
+    const std::vector<SnapField> f = snap_fields(h);
+    std::vector<size_t> off;
+    const size_t total = snap_offsets(f, E, &off);
+    SnapHeader hd{};
+    hd.magic = kSnapMagic; hd.version = 1;
+    hd.E = h->cfg.num_envs; hd.N = h->cfg.num_agents; hd.K = h->cfg.max_npcs; hd.D = h->D; hd.R = h->cfg.lidar_rays;
+    hd.nfields = int32_t(f.size()); hd.rng_counter = h->rng_counter; hd.total_bytes = total;
+    uint8_t* d = static_cast<uint8_t*>(dst);
+    const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (dev) HIP_TRY(hipMemcpyAsync(d, &hd, sizeof(hd), hipMemcpyHostToDevice, h->stream));
+    else memcpy(d, &hd, sizeof(hd));
+    for (size_t i = 0; i < f.size(); ++i) HIP_TRY(hipMemcpyAsync(d + off[i], f[i].live, f[i].bpe * E, kind, h->stream));
+    // the header copy reads host memory: always wait before returning in device mode too
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_t flags) {
+    if (!h || !src) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
+    const size_t E = size_t(h->cfg.num_envs);
+    SnapHeader hd{};
+    if (dev) {
+        HIP_TRY(hipMemcpyAsync(&hd, src, sizeof(hd), hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    } else {
+        memcpy(&hd, src, sizeof(hd));
+    }
+    // the live outputs are restored into the handle's own buffers; envs a masked
+    // restore leaves alone keep their current outputs, so bring those in first
+    {
+        const size_t EN = E * size_t(h->cfg.num_agents);
+        auto pull = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+            if (!src || src == dst) return hipSuccess;
+            return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, h->stream);
+        };
+        const mev::Outputs& L = h->last;
+        mev::Outputs& I = h->internal;
+        if (env_mask) {
+            HIP_TRY(pull(I.obs, L.obs, EN * size_t(h->D) * sizeof(float)));
+            HIP_TRY(pull(I.rew, L.rew, EN * sizeof(float)));
+            HIP_TRY(pull(I.done, L.done, EN));
+            HIP_TRY(pull(I.status, L.status, EN));
+            HIP_TRY(pull(I.term, L.term, E));
+            HIP_TRY(pull(I.trunc, L.trunc, E));
+            HIP_TRY(pull(I.alive_cnt, L.alive_cnt, E * sizeof(int32_t)));
+            HIP_TRY(pull(I.step, L.step, E * sizeof(int32_t)));
+        }
+    }
+    h->last = h->internal;
+    const std::vector<SnapField> f = snap_fields(h);
+    std::vector<size_t> off;
+    const size_t total = snap_offsets(f, E, &off);
+    if (hd.magic != kSnapMagic || hd.version != 1 || hd.E != h->cfg.num_envs || hd.N != h->cfg.num_agents ||
+        hd.K != h->cfg.max_npcs || hd.D != h->D || hd.nfields != int32_t(f.size()) || hd.total_bytes != total)
+        return fail(MEV_E_INVALID, "snapshot does not match this handle");
+    const uint8_t* s = static_cast<const uint8_t*>(src);
+    if (!env_mask) {
+        const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+        for (size_t i = 0; i < f.size(); ++i) HIP_TRY(hipMemcpyAsync(f[i].restore, s + off[i], f[i].bpe * E, kind, h->stream));
+        h->rng_counter = hd.rng_counter;
+    } else {
+        if (f.size() > size_t(mev::kMaxRestoreFields)) return fail(MEV_E_INVALID, "too many snapshot fields");
+        const uint8_t* dsrc = s;
+        const uint8_t* dmask = env_mask;
+        if (!dev) {  // stage the snapshot and the mask on the device
+            if (h->snap_stage_bytes < total) {
+                if (h->d_snap_stage) {
+                    HIP_TRY(hipStreamSynchronize(h->stream));
+                    HIP_TRY(hipFree(h->d_snap_stage));
+                    h->d_snap_stage = nullptr;
+                    h->snap_stage_bytes = 0;
+                }
+                HIP_TRY(hipMalloc(reinterpret_cast<void**>(&h->d_snap_stage), total));
+                h->snap_stage_bytes = total;
+            }
+            HIP_TRY(hipMemcpyAsync(h->d_snap_stage, s, total, hipMemcpyHostToDevice, h->stream));
+            HIP_TRY(hipMemcpyAsync(h->d_mask, env_mask, E, hipMemcpyHostToDevice, h->stream));
+            dsrc = h->d_snap_stage;
+            dmask = h->d_mask;
+        }
+        mev::RestoreTab tab{};
+        tab.n = int32_t(f.size());
+        for (size_t i = 0; i < f.size(); ++i) {
+            tab.dst[i] = f[i].restore;
+            tab.src_off[i] = off[i];
+            tab.bpe[i] = int32_t(f[i].bpe);
+        }
+        HIP_TRY(mev::launch_restore(tab, dsrc, dmask, h->cfg.num_envs, h->stream));
+    }
+    if (!dev) HIP_TRY(hipStreamSynchronize(h->stream));
     return MEV_OK;
 }
 

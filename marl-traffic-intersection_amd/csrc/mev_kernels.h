@@ -79,6 +79,9 @@ struct SimParams {
     int4* ob_box;                  // [E][ob_stride] integer pixel AABB (x0, x1, y0, y1)
     unsigned long long* ob_cand;   // [E*N][2] candidate obstacle bits per agent
     int32_t ob_stride;             // N + max_npcs
+    // route pool drawn per agent at every reset (n_reset_routes == 0: routes stay fixed)
+    const int32_t* reset_routes;
+    int32_t n_reset_routes;
 };
 
 struct StepInputs {
@@ -92,8 +95,19 @@ struct StepInputs {
 // ev (nullable): three events recorded before k_cars, between k_cars and k_lidar, after k_lidar
 hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
                        const hipEvent_t* ev = nullptr);
-hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s);
+hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s,
+                        uint64_t rng_counter);
 // recompute the observation rows from the current state with LiDAR = max (after set_state)
 hipError_t launch_observe_reset_lidar(const SimParams& p, const Outputs& out, hipStream_t s);
+
+// masked per-env copy of snapshot fields (mev_restore)
+constexpr int kMaxRestoreFields = 48;
+struct RestoreTab {
+    int32_t n;
+    uint8_t* dst[kMaxRestoreFields];
+    unsigned long long src_off[kMaxRestoreFields];
+    int32_t bpe[kMaxRestoreFields];  // bytes per env
+};
+hipError_t launch_restore(const RestoreTab& tab, const uint8_t* src, const uint8_t* env_mask, int E, hipStream_t s);
 
 }  // namespace mev

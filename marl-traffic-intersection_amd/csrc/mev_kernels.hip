@@ -103,6 +103,16 @@ __device__ inline void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint64_t se
 
 __device__ inline float u01(uint32_t r) { return (float)(r >> 8) * 0x1p-24f; }
 
+// Route of agent i of env e at a reset: fixed (reference env.py) unless a reset
+// route pool is set, then drawn uniformly per (reset, env, agent) with Philox,
+// like the reference test.py's random.choice(all_routes) on every reset.
+__device__ inline int reset_route(const SimParams& p, uint64_t ctr, int e, int i, int fixed) {
+    if (p.n_reset_routes <= 0) return fixed;
+    uint32_t r0, r1;
+    philox((uint32_t)ctr, (uint32_t)(ctr >> 32) ^ 0x9E3779B9u, (uint32_t)e * 64u + (uint32_t)i, p.seed, &r0, &r1);
+    return p.reset_routes[(int)(((uint64_t)r0 * (uint32_t)p.n_reset_routes) >> 32)];
+}
+
 // dist of march probe k: the reference accumulates `dist += step_size` in
 // float (Lidar.cpp:33); when that sum equals k*step exactly (checked on the
 // host, e.g. step 4) we multiply, otherwise read the host-accumulated table.
@@ -598,7 +608,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
     const int prev_npcs = TRAFFIC ? (do_reset ? 0 : p.npc.count[e]) : 0;
     for (int i = tid; i < N; i += WAVE) {
         const int g = e * N + i;
-        const int rid = p.ego.route[g];
+        const int rid = do_reset ? reset_route(p, in.rng_counter, e, i, p.ego.route[g]) : p.ego.route[g];
         el.route[i] = rid;
         el.a0[i] = in.actions[2 * g];
         el.a1[i] = in.actions[2 * g + 1];
@@ -862,7 +872,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         p.ego.prev_dist[g] = el.prev_dist[i]; p.ego.pa0[g] = el.pa0[i]; p.ego.pa1[g] = el.pa1[i];
         if (do_reset) {
             p.ego.sx[g] = el.sx[i]; p.ego.sy[g] = el.sy[i]; p.ego.sv[g] = el.sv[i]; p.ego.sh[g] = el.sh[i];
-            p.ego.intent[g] = el.intent[i]; p.ego.alive[g] = el.alive[i];
+            p.ego.intent[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; p.ego.route[g] = el.route[i];
         }
     }
     wave_lds_sync();
@@ -1389,7 +1399,8 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
 // IntersectionEnv::reset + add_car_with_route (cpp/IntersectionEnv.cpp:66-131)
 // and the reset observation (LiDAR block = max_dist / max_dist).
 template <bool TRAFFIC>
-__global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask, Outputs out, int do_reset) {
+__global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask, Outputs out, int do_reset,
+                                                uint64_t rng_counter) {
     const int e = blockIdx.x;
     const int lane = threadIdx.x;
     const int N = p.N;
@@ -1401,7 +1412,8 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
     for (int i = lane; i < N; i += WAVE) {
         const int g = e * N + i;
         if (do_reset) {
-            const int rid = p.ego.route[g];
+            const int rid = reset_route(p, rng_counter, e, i, p.ego.route[g]);
+            p.ego.route[g] = rid;
             p.ego.x[g] = p.rt.spawn[3 * rid];
             p.ego.y[g] = p.rt.spawn[3 * rid + 1];
             p.ego.v[g] = 0.0f;
@@ -1471,15 +1483,38 @@ hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& 
     return e;
 }
 
-hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s) {
-    if (p.traffic) hipLaunchKernelGGL(k_reset<true>, dim3(p.E), dim3(WAVE), 0, s, p, env_mask, out, 1);
-    else hipLaunchKernelGGL(k_reset<false>, dim3(p.E), dim3(WAVE), 0, s, p, env_mask, out, 1);
+hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s,
+                        uint64_t rng_counter) {
+    if (p.traffic) hipLaunchKernelGGL(k_reset<true>, dim3(p.E), dim3(WAVE), 0, s, p, env_mask, out, 1, rng_counter);
+    else hipLaunchKernelGGL(k_reset<false>, dim3(p.E), dim3(WAVE), 0, s, p, env_mask, out, 1, rng_counter);
     return hipGetLastError();
 }
 
 hipError_t launch_observe_reset_lidar(const SimParams& p, const Outputs& out, hipStream_t s) {
-    if (p.traffic) hipLaunchKernelGGL(k_reset<true>, dim3(p.E), dim3(WAVE), 0, s, p, nullptr, out, 0);
-    else hipLaunchKernelGGL(k_reset<false>, dim3(p.E), dim3(WAVE), 0, s, p, nullptr, out, 0);
+    if (p.traffic) hipLaunchKernelGGL(k_reset<true>, dim3(p.E), dim3(WAVE), 0, s, p, nullptr, out, 0, 0ull);
+    else hipLaunchKernelGGL(k_reset<false>, dim3(p.E), dim3(WAVE), 0, s, p, nullptr, out, 0, 0ull);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------- masked restore ---
+// mev_restore with an env mask: block (e, field) copies env e's slice of one
+// snapshot field back into the live state when mask[e] is set.
+__global__ __launch_bounds__(WAVE) void k_restore(RestoreTab tab, const uint8_t* src, const uint8_t* mask) {
+    const int e = blockIdx.x, f = blockIdx.y;
+    if (f >= tab.n || !mask[e]) return;
+    const int bpe = tab.bpe[f];
+    const uint8_t* s = src + tab.src_off[f] + (size_t)e * bpe;
+    uint8_t* d = tab.dst[f] + (size_t)e * bpe;
+    if ((bpe & 3) == 0) {
+        for (int w = threadIdx.x; w < (bpe >> 2); w += WAVE)
+            reinterpret_cast<uint32_t*>(d)[w] = reinterpret_cast<const uint32_t*>(s)[w];
+    } else {
+        for (int b = threadIdx.x; b < bpe; b += WAVE) d[b] = s[b];
+    }
+}
+
+hipError_t launch_restore(const RestoreTab& tab, const uint8_t* src, const uint8_t* env_mask, int E, hipStream_t s) {
+    hipLaunchKernelGGL(k_restore, dim3(E, tab.n), dim3(WAVE), 0, s, tab, src, env_mask);
     return hipGetLastError();
 }
 

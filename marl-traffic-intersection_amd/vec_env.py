@@ -111,6 +111,46 @@ class VecIntersectionEnv:
             routes = np.asarray(ids, np.int32)
         self._h.set_ego_routes(np.asarray(routes, np.int32))
 
+    def set_reset_routes(self, routes):
+        """Draw every agent's route from `routes` (names or ids) at each reset, as the
+        reference test.py does with random.choice(all_routes); [] restores fixed routes."""
+        ids = []
+        P = 8 * self.num_lanes
+        for r in routes:
+            if isinstance(r, (tuple, list)):
+                si, ei = point_index(r[0], self.num_lanes), point_index(r[1], self.num_lanes)
+                if si < 0 or ei < 0:
+                    raise IndexError(f"unknown lane id in route {tuple(r)!r}")
+                ids.append(si * P + ei)
+            else:
+                ids.append(int(r))
+        self._h.set_reset_routes(ids)
+
+    def snapshot(self, out=None):
+        """Whole-batch state + last outputs (torch: a device uint8 tensor; numpy: host bytes)."""
+        if self.backend == "torch":
+            self._bind_stream()
+            if out is None:
+                out = self._torch.empty(self._h.snapshot_size(), dtype=self._torch.uint8,
+                                        device=self._out["obs"].device)
+            self._h.snapshot(out, device=True)
+            return out
+        return self._h.snapshot(out)
+
+    def restore(self, snap, env_mask=None):
+        """Roll all envs (or those with env_mask != 0) back to `snap`; outputs follow."""
+        if self.backend == "torch":
+            self._bind_stream()
+            mask = None
+            if env_mask is not None:
+                mask = self._torch.as_tensor(env_mask, device=self._out["obs"].device).to(self._torch.uint8)
+                mask = mask.contiguous()
+            self._h.restore(snap, env_mask=mask, device=True)
+            self._h.get_outputs(self._out, device=True)
+            return self._out["obs"]
+        self._h.restore(snap, env_mask=env_mask)
+        return self._h.get_outputs(self._out)["obs"]
+
     def set_traffic_routes(self, routes):
         """The NPC route list (reference configure_routes); names or route ids."""
         P = 8 * self.num_lanes
