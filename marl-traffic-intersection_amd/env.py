@@ -125,8 +125,16 @@ class IntersectionEnv:
         return obs, rewards, info["terminated"], info["truncated"], info
 
     def render(self, show_lane_ids: Optional[bool] = None, show_lidar: Optional[bool] = None):
-        """The reference's GLFW renderer is out of scope (Windows-only there); a no-op here."""
-        return None
+        """The reference opens a GLFW window (Windows-only, Renderer.cpp).  Here
+        render_mode "rgb_array" returns a frame from the headless debug renderer
+        (render.py); any other mode is a no-op."""
+        if self.render_mode != "rgb_array":
+            return None
+        from . import render as _render
+        h = self.env._sync()
+        if h is None:
+            return None
+        return _render.render(h, 0, show_lidar=self.show_lidar if show_lidar is None else bool(show_lidar))
 
     def close(self):
         self.env.close()

@@ -130,3 +130,13 @@ def test_backend_classes_shape():
     assert s.next_agent_id == 1 and s.cars == [] and s.step_count == 0
     c = cpp_backend.Car()
     assert (c.length, c.width, c.alive, c.intention, c.path_index) == (54.0, 24.0, True, 0, 0)
+
+
+def test_render_masks_match_reference_geometry():
+    """The debug renderer's road and line masks equal the reference's rasters
+    (tests/golden/static_lanes*.npz, recorded from RoadGeometry / LineMask)."""
+    from marl_traffic_intersection_amd import render
+    for L in (2, 3):
+        g = np.load(f"{G.GOLDEN_DIR}/static_lanes{L}.npz")["grid"]
+        assert np.array_equal(render.road_mask(L), (g & 1).astype(bool))
+        assert np.array_equal(render.line_mask(L), (g & 4).astype(bool))

@@ -197,3 +197,15 @@ def test_vec_env_replays_reference_in_every_env(backend):
             assert all(G.bits_equal(obs[e], g["obs"][t]) for e in range(E)), t
             assert all(G.bits_equal(rew[e], g["rew"][t]) for e in range(E)), t
     v.close()
+
+
+def test_rgb_array_render():
+    from marl_traffic_intersection_amd import render
+    e = env_mod.IntersectionEnv({"num_agents": 4, "render_mode": "rgb_array", "show_lidar": True})
+    for _ in range(5):
+        e.step(np.zeros((4, 2), np.float32))
+    frame = e.render()
+    assert frame.shape == (750, 750, 3) and frame.dtype == np.uint8
+    assert (frame == np.array(render.EGO, np.uint8)).all(-1).sum() > 4 * 400  # four 54x24 cars
+    assert (frame == np.array(render.HIT, np.uint8)).all(-1).any()
+    e.close()
