@@ -1025,22 +1025,33 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 // index at each end of the range, so a real hit is never dropped.
 
 // Distance along a beam from its real point (fx, fy) over which every probe is
-// provably on screen and on the road (margin 1.5 px > the < 1 px truncation
-// shift).  Inside a strip the bound is directional (distance to the strip edge
-// the ray is heading for); in the corner square it is the distance to the
-// grass disc or the square's edge; plus the distance to the screen edge.
+// provably on screen and on the road (the truncated pixel is within 1 px per
+// axis, < 1.42 px, of the real point).  Each bound below alone guarantees its
+// stretch, so the road bound is their maximum; all are directional:
+//  - strips: distance to the strip edge (|x - 375| = rw - 1.5) the ray heads for;
+//  - centre square: inside the square shrunk by 1.55 px, within the current
+//    quadrant (only its own grass disc can be met there), outside that disc
+//    grown by 2 px (extra margin for the tangent-case rounding of the root):
+//    distance to the first of the grown disc, the shrunk square's edge and the
+//    quadrant's edge;
+//  - screen: distance to the half-pixel-inset screen edge.
 __device__ inline float road_safe(float fx, float fy, float dx, float dy, float idx, float idy, float iadx,
                                   float iady, float rwm, float ccen, float crf) {
+    const float big = 1.0e6f;
     const float rx = fx - 375.0f, ry = fy - 375.0f;
     const float ax = fabs_f(rx), ay = fabs_f(ry);
-    const bool in_x = ax < rwm, in_y = ay < rwm;
-    const float sx = in_x ? rwm * iadx - rx * idx : 0.0f;
-    const float sy = in_y ? rwm * iady - ry * idy : 0.0f;
-    // corner square: road outside the grass disc on its outer corner
-    // (approximate sqrt: bound only, extra 0.05 px margin)
-    const float qx = ax - ccen, qy = ay - ccen;
-    const float corner = fminf(__builtin_amdgcn_sqrtf(qx * qx + qy * qy) - crf, fminf(ccen - ax, ccen - ay)) - 1.55f;
-    const float road = (in_x | in_y) ? fmaxf(sx, sy) : (fmaxf(ax, ay) < ccen ? corner : 0.0f);
+    const float sx = ax < rwm ? rwm * iadx - rx * idx : 0.0f;
+    const float sy = ay < rwm ? rwm * iady - ry * idy : 0.0f;
+    const float sqm = ccen - 1.55f, rg = crf + 2.0f;
+    const float ocx = rx - (rx >= 0.0f ? ccen : -ccen), ocy = ry - (ry >= 0.0f ? ccen : -ccen);
+    const float bq = ocx * dx + ocy * dy;
+    const float cq = ocx * ocx + ocy * ocy - rg * rg;
+    const float disc = bq * bq - cq;
+    const float tdisc = cq <= 0.0f ? 0.0f : ((disc < 0.0f || bq >= 0.0f) ? big : -bq - __builtin_amdgcn_sqrtf(disc));
+    const float tsq = fminf(sqm * iadx - rx * idx, sqm * iady - ry * idy);
+    const float tq = fminf(rx * dx < 0.0f ? -rx * idx : big, ry * dy < 0.0f ? -ry * idy : big);
+    const float sc = fmaxf(ax, ay) < sqm ? fminf(tdisc, fminf(tsq, tq)) : 0.0f;
+    const float road = fmaxf(fmaxf(sx, sy), sc);
     const float tx = (dx > 0.0f ? 748.5f - fx : fx - 0.5f) * iadx;
     const float ty = (dy > 0.0f ? 748.5f - fy : fy - 0.5f) * iady;
     return fminf(road, fminf(tx, ty));
