@@ -154,7 +154,30 @@ MEV_HD void sincosf_impl(float y, float* sinp, float* cosp) {
     }
 }
 
-MEV_HD void sincosf(float y, float* s, float* c) { sincosf_impl<MEV_SINCOS_FMA != 0>(y, s, c); }
+
+// Same results as sincosf for every finite |y| < 120 with one code path: below
+// pi/4 reduce_fast yields n = 0 and x unchanged, so the reduced polynomial is
+// glibc's small-argument one; the |y| < 2^-12 shortcut becomes a select --
+// checked for every float |y| <= 8 by tests/native/devmath_check.cpp.  A wave
+// of beams then does not evaluate the polynomial twice.
+template <bool FMA>
+MEV_HD void sincosf_reduced_impl(float y, float* sinp, float* cosp) {
+    if (!(abstop12(y) < abstop12(120.0f))) {
+        sincosf_impl<FMA>(y, sinp, cosp);
+        return;
+    }
+    int n;
+    const double x = reduce_fast<FMA>((double)y, kSinCos[0], &n);
+    const double s = kSinCos[0].sign[n & 3];
+    float sv, cv;
+    sincosf_poly<FMA>(x * s, x * x, kSinCos[(n & 2) ? 1 : 0], n, &sv, &cv);
+    const bool tiny = abstop12(y) < abstop12(0x1p-12f);  // glibc's shortcut (keeps the sign of -0)
+    *sinp = tiny ? y : sv;
+    *cosp = tiny ? 1.0f : cv;
+}
+
+// the simulator's sincosf (glibc results; single path below 120)
+MEV_HD void sincosf(float y, float* s, float* c) { sincosf_reduced_impl<MEV_SINCOS_FMA != 0>(y, s, c); }
 
 // ------------------------------------------------------------------ tanf ---
 MEV_HD float kernel_tanf(float x, float y, int iy) {
