@@ -1096,7 +1096,7 @@ __device__ inline int lane_rank(unsigned long long mask) {
 
 
 // Per-wave LDS of k_lidar: ag float4[G] (x, y, heading, agent id) of the
-// group's alive agents, bm float4[G*R] beams (origin x, y, direction dx, dy), res int[G*R] stop of
+// group's alive agents, dir float2[G*R] beam directions, res int[G*R] stop of
 // each beam (k << 1 | hit), and the car-phase segments: seg_jo int[C]
 // (agent << 8 | box), seg_rg int4[C] (three beam ranges lo | count << 16, total),
 // seg_bx int4[C] (the box), seg_beg int[G+1]; C = G * cmax, cmax = the most
@@ -1112,7 +1112,7 @@ __host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax) {
     const int C = G * cmax;
     int off = 0;
     L.ag = off; off += G * 16;
-    L.dir = off; off += G * R * 16;
+    L.dir = off; off += G * R * 8;
     L.res = off; off += G * R * 4;
     off = (off + 15) & ~15;
     L.seg_rg = off; off += C * 16;
@@ -1130,7 +1130,7 @@ int lidar_group(int R) {
 }
 
 template <bool TAB>
-__global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) {
+__global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int G) {
     // Each wave owns a group of G agents (G*R <= max(256, R) beams).  Phase 1
     // computes the beam directions in lockstep; phase 2 marches the road with
     // the group's beams fed to the 64 lanes from a queue, so a lane that
@@ -1149,7 +1149,7 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
     const LidarLayout lay = lidar_layout(G, R, lidar_cand_max(p));
     unsigned char* base = lds_raw + (size_t)wv * (size_t)lay.bytes;
     float4* ag = reinterpret_cast<float4*>(base + lay.ag);
-    float4* bm = reinterpret_cast<float4*>(base + lay.dir);
+    float2* dir = reinterpret_cast<float2*>(base + lay.dir);
     int* res = reinterpret_cast<int*>(base + lay.res);
 
     // ---- phase 1: alive agents of the group (compacted), beam directions
@@ -1186,7 +1186,7 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
             float sn, cs;
             sincosf(a.z + p.rel_angles[b], &sn, &cs);  // Lidar.cpp:24-26
             const float dx = cs, dy = -sn;
-            bm[j * R + b] = make_float4(a.x, a.y, dx, dy);
+            dir[j * R + b] = make_float2(dx, dy);
             const int px = (int)a.x, py = (int)a.y;
             const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
             int k1 = 0;
@@ -1202,13 +1202,17 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
 
     // ---- phase 2: pooled road + screen march (Lidar.cpp:31-48, first stop wins)
     const int total = nal * R;
+    const float invR = 1.0f / (float)R;
     int next = total < WAVE ? total : WAVE;
     int q = lane < total ? lane : -1;
     float cx = 0.0f, cy = 0.0f, dx = 0.0f, dy = 0.0f, idx = 0.0f, idy = 0.0f, iadx = 0.0f, iady = 0.0f;
     int k = 0;
     auto load_beam = [&](int qq) {
-        const float4 r = bm[qq];
-        cx = r.x; cy = r.y; dx = r.z; dy = r.w;
+        // agent of pool beam qq = j*R + b: exact float quotient (qq < 2^20, R <= 1024)
+        const int j = (int)(((float)qq + 0.5f) * invR);
+        const float4 a = ag[j];
+        const float2 d = dir[qq];
+        cx = a.x; cy = a.y; dx = d.x; dy = d.y;
         idx = __builtin_amdgcn_rcpf(dx);
         idy = __builtin_amdgcn_rcpf(dy);
         iadx = fabs_f(idx);
@@ -1369,8 +1373,7 @@ __global__ __launch_bounds__(256) void k_lidar(SimParams p, Outputs out, int G) 
                                          : (r < cA + cB ? (rg.y & 0xffff) + r - cA : (rg.z & 0xffff) + r - cA - cB);
                     const int slot = j * R + b;
                     const int kr = res[slot] >> 1;
-                    const float4 bq = bm[slot];
-                    const float2 dd = make_float2(bq.z, bq.w);
+                    const float2 dd = dir[slot];
                     // probes that can land in the box: the ray's interval inside the
                     // box's real slab (see box_lo), as a superset range of k ...
                     float lo = 0.0f, hi = 1.0e6f;
