@@ -1479,6 +1479,8 @@ hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& 
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], s);
     int G = lidar_group(p.R);
+    // small batches: trade pool size for waves (~4 per SIMD on 256 CUs) so latency is hidden
+    while (G > 1 && (p.E * p.N) / G < 4096) G = (G + 1) / 2;
     static const int g_env = [] { const char* v = getenv("MEV_LIDAR_G"); return v ? atoi(v) : 0; }();
     if (g_env > 0 && g_env <= 64 && (size_t)g_env * p.R <= 1024) G = g_env;  // experiments (tools/kernel_time.py)
     // LDS: shrink the group, then the waves per block, to stay within 40 KB (64 KB hard) per block

@@ -1,0 +1,75 @@
+"""Throughput of the BASELINE configs on one GPU (documentation; bench.py is the
+contract and measures config 3).  Same method as bench.py: actions resident
+in HBM, outputs to HBM, auto-reset, warm-up then timed steps; per-kernel
+device time from the library's events (every 4th step).
+    python tools/bench_sweep.py [--steps 500] [--out profiles/r1_sweep.json]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CONFIGS = [
+    dict(name="cfg1", desc="1 env x 1 agent x 16 beams", E=1, N=1, R=16),
+    dict(name="cfg2", desc="4096 envs x 1 agent x 64 beams", E=4096, N=1, R=64),
+    dict(name="cfg3", desc="4096 envs x 8 agents x 64 beams, team reward", E=4096, N=8, R=64, team=1),
+    dict(name="cfg4", desc="4096 envs x 1 agent x 64 beams, traffic density 0.5", E=4096, N=1, R=64, traffic=1),
+    dict(name="cfg5/GPU", desc="4096 envs x 8 agents x 128 beams, team reward (per-GPU share of 32768)",
+         E=4096, N=8, R=128, team=1),
+    dict(name="96-beam", desc="4096 envs x 8 agents x 96 beams (reference default LiDAR), obs 127",
+         E=4096, N=8, R=96, D=127),
+]
+
+
+def run(cfg, steps, warmup):
+    import torch
+    import pkgload
+    mev = pkgload.load()
+    dev = torch.device("cuda", 0)
+    E, N, R = cfg["E"], cfg["N"], cfg["R"]
+    h = mev.Handle(num_envs=E, num_agents=N, lidar_rays=R, obs_dim=cfg.get("D", 0),
+                   use_team_reward=cfg.get("team", 0), traffic_flow=cfg.get("traffic", 0), traffic_density=0.5,
+                   max_npcs=32)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(st)
+    h.set_stream(st.cuda_stream)
+    acts = torch.rand((warmup + steps, E, N, 2), device=dev) * 2 - 1
+    out = {k: torch.zeros_like(torch.as_tensor(v), device=dev) for k, v in h.alloc_outputs().items()}
+    for t in range(warmup):
+        h.step(acts[t], out=out, auto_reset=True, device=True)
+    torch.cuda.synchronize()
+    h.kernel_timing(4)
+    t0 = time.perf_counter()
+    for t in range(steps):
+        h.step(acts[warmup + t], out=out, auto_reset=True, device=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    c, l_, n = h.kernel_times()
+    npc = float(h.get_state()["npc_count"].mean()) if cfg.get("traffic") else 0.0
+    h.close()
+    return dict(name=cfg["name"], workload=cfg["desc"], agent_steps_per_s=round(E * N / dt, 1),
+                ms_per_step=round(dt * 1e3, 5), k_cars_ms=round(c / n, 5), k_lidar_ms=round(l_ / n, 5),
+                mean_npcs=round(npc, 3))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    res = []
+    for cfg in CONFIGS:
+        r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup)
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
