@@ -155,6 +155,7 @@ struct NpcLDS {
     float cx[MAXK][4], cy[MAXK][4];
     unsigned long long col[MAXK];
     uint8_t pair_ok[MAXK], yield_far[MAXK];
+    float2 path[2][PATH_LEN];  // the route of the NPC being controlled (double buffered)
 };
 
 
@@ -245,11 +246,36 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     }
     wave_lds_sync();
 
-    // -- sequential controller over NPCs in vector order (Gauss-Seidel, :337-344)
+    // -- sequential controller over NPCs in vector order (Gauss-Seidel, :337-344).
+    // Each NPC's route is staged in LDS (one round trip, prefetched during the
+    // previous NPC), so the path-index windows, the look-ahead target and the
+    // 120-point ghost scan read no global memory.
     const float CXf = WIDTH * 0.5f, CYf = HEIGHT * 0.5f;
+    constexpr int PPL = (PATH_LEN + WAVE - 1) / WAVE;  // route points per lane
+    float2 pre[PPL];
+    auto fetch_route = [&](int kk) {  // issue the loads of NPC kk's route (or nothing)
+        if (kk >= cnt) return;
+        const float2* g = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+#pragma unroll
+        for (int u = 0; u < PPL; ++u) {
+            const int i = lane + u * WAVE;
+            if (i < PATH_LEN) pre[u] = g[i];
+        }
+    };
+    auto stage_route = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < PPL; ++u) {
+            const int i = lane + u * WAVE;
+            if (i < PATH_LEN) nl.path[buf][i] = pre[u];
+        }
+    };
+    fetch_route(0);
     for (int k = 0; k < cnt; ++k) {
+        stage_route(k & 1);
+        wave_lds_sync();
+        fetch_route(k + 1);  // in flight while NPC k is controlled
         if (!nl.alive[k]) continue;
-        const float* path = p.rt.path + (size_t)nl.route[k] * (2 * PATH_LEN);
+        const float* path = reinterpret_cast<const float*>(nl.path[k & 1]);
         float x = nl.x[k], y = nl.y[k];
         int pidx = path_index_update(path, nl.pidx[k], x, y, lane);
         const float h = nl.h[k], v = nl.v[k];
