@@ -1,0 +1,65 @@
+"""Error behaviour of the C ABI (negative MEV_E* codes + mev_last_error, never an
+exception across the boundary), mirrored by the Python binding as MevError /
+IndexRangeError (IndexError, like the reference's std::out_of_range)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(num_envs=0), dict(num_agents=0), dict(num_agents=65), dict(num_lanes=0), dict(num_lanes=9),
+    dict(lidar_rays=0), dict(lidar_rays=1025), dict(lidar_step=0.0), dict(lidar_max_dist=-1.0),
+    dict(max_npcs=65), dict(obs_dim=20), dict(device=99),
+])
+def test_invalid_configs_are_rejected(mev, cfg):
+    with pytest.raises(mev.MevError) as ei:
+        mev.Handle(**cfg)
+    assert str(ei.value)
+
+
+def test_out_of_range_routes_raise_index_error(mev):
+    h = mev.Handle(num_envs=2, num_agents=2, lidar_rays=16)
+    P = h.num_points
+    with pytest.raises(IndexError):
+        h.route_id(P, 0)
+    with pytest.raises(IndexError):
+        h.route_info(P * P)
+    with pytest.raises(IndexError):
+        h.set_ego_routes(np.full((2, 2), P * P, np.int32))
+    with pytest.raises(IndexError):
+        h.set_traffic_routes([-1])
+    with pytest.raises(IndexError):
+        h.set_reset_routes([P * P + 5])
+    st = h.get_state()
+    st["npc_count"][:] = 99
+    with pytest.raises(IndexError):
+        h.set_state(st)
+    h.close()
+
+
+def test_wrong_action_shape_is_rejected_before_the_device(mev):
+    h = mev.Handle(num_envs=3, num_agents=2, lidar_rays=16)
+    with pytest.raises(ValueError):
+        h.step(np.zeros((3, 3, 2), np.float32))
+    h.close()
+
+
+def test_handle_survives_errors(mev):
+    h = mev.Handle(num_envs=4, num_agents=2, lidar_rays=16)
+    with pytest.raises(IndexError):
+        h.route_info(-1)
+    o = h.step(np.zeros((4, 2, 2), np.float32))
+    assert o["step"].tolist() == [1, 1, 1, 1]
+    h.close()
+
+
+def test_large_batch_allocates_and_steps(mev):
+    """One handle of 131072 envs x 8 agents (a quarter of cfg5's node-wide batch on one GPU)."""
+    E = 131072
+    h = mev.Handle(num_envs=E, num_agents=8, lidar_rays=64, use_team_reward=1)
+    rng = np.random.default_rng(0)
+    for _ in range(3):
+        o = h.step(rng.uniform(-1, 1, (E, 8, 2)).astype(np.float32), auto_reset=True)
+    assert np.isfinite(o["obs"]).all() and (o["step"] == 3).all()
+    h.close()
