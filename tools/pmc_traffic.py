@@ -32,7 +32,9 @@ def _read(d, counter):
                 if row["Counter_Name"] != counter:
                     continue
                 name = row["Kernel_Name"]
-                for short in ("k_lidar", "k_cars", "k_reset"):
+                if "mev::" not in name:
+                    continue            # the library's kernels only (not torch's input generation)
+                for short in ("k_lidar", "k_cars", "k_reset", "k_restore"):
                     if short in name:
                         name = short + name[name.find(short) + len(short):].split("(")[0]
                         break
