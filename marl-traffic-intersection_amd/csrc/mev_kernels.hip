@@ -1127,8 +1127,16 @@ __device__ inline int lane_rank(unsigned long long mask) {
 // (agent << 8 | box), seg_rg int4[C] (three beam ranges lo | count << 16, total),
 // seg_bx int4[C] (the box), seg_beg int[G+1]; C = G * cmax, cmax = the most
 // candidate boxes one agent can have (every other ego, plus the NPC slots).
+// The road march's queue of unfinished beams, ushort[G*R], is only live
+// before the car phase and shares the segment area.
+// Probes tested per step of the road march (phase 1 and each pooled iteration).
+#ifndef MEV_LIDAR_NPR
+#define MEV_LIDAR_NPR 3
+#endif
+constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
+
 struct LidarLayout {
-    int ag, dir, res, seg_jo, seg_rg, seg_bx, seg_beg, bytes;
+    int ag, dir, res, seg_jo, seg_rg, seg_bx, seg_beg, queue, bytes;
 };
 
 __host__ __device__ inline int lidar_cand_max(const SimParams& p) { return p.N - 1 + (p.traffic ? p.K : 0); }
@@ -1144,6 +1152,9 @@ __host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax) {
     L.seg_rg = off; off += C * 16;
     L.seg_bx = off; off += C * 16;
     L.seg_jo = off; off += C * 4;
+    L.queue = L.seg_rg;
+    if (off < L.queue + G * R * 2) off = L.queue + G * R * 2;
+    off = (off + 3) & ~3;
     L.seg_beg = off; off += (G + 1) * 4;
     L.bytes = (off + 15) & ~15;
     return L;
@@ -1203,64 +1214,15 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     const float crf = CORNER_RADIUS, ccen = rwf + crf;
     const float cr2p1 = crf * crf + 1.0f;
     const float rwm = rwf - 1.5f;
-    // directions, and the first probe the march has to evaluate: probe 0 is
-    // only screen-tested (no road test at dist 0); if the car centre is on
-    // screen, every probe within the safe distance from it is skipped too
-    for (int j = 0; j < nal; ++j) {
-        const float4 a = ag[j];
-        for (int b = lane; b < R; b += WAVE) {
-            float sn, cs;
-            sincosf(a.z + p.rel_angles[b], &sn, &cs);  // Lidar.cpp:24-26
-            const float dx = cs, dy = -sn;
-            dir[j * R + b] = make_float2(dx, dy);
-            const int px = (int)a.x, py = (int)a.y;
-            const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
-            int k1 = 0;
-            if (pmax < (unsigned)WIDTH) {
-                const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
-                const float safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
-                k1 = (safe >= two_stp) ? (int)(safe * inv_stp) : 1;
-            }
-            res[j * R + b] = k1;  // start probe of the march (phase 2)
-        }
-    }
-    wave_lds_sync();
-
-    // ---- phase 2: pooled road + screen march (Lidar.cpp:31-48, first stop wins)
-    const int total = nal * R;
-    const float invR = 1.0f / (float)R;
-    int next = total < WAVE ? total : WAVE;
-    int q = lane < total ? lane : -1;
-    float cx = 0.0f, cy = 0.0f, dx = 0.0f, dy = 0.0f, idx = 0.0f, idy = 0.0f, iadx = 0.0f, iady = 0.0f;
-    int k = 0;
-    auto load_beam = [&](int qq) {
-        // agent of pool beam qq = j*R + b: exact float quotient (qq < 2^20, R <= 1024)
-        const int j = (int)(((float)qq + 0.5f) * invR);
-        const float4 a = ag[j];
-        const float2 d = dir[qq];
-        cx = a.x; cy = a.y; dx = d.x; dy = d.y;
-        idx = __builtin_amdgcn_rcpf(dx);
-        idy = __builtin_amdgcn_rcpf(dy);
-        iadx = fabs_f(idx);
-        iady = fabs_f(idy);
-        k = res[qq];
-    };
-    if (q >= 0) load_beam(q);
-#ifdef MEV_ITERS
-    int iters = 0;
-#endif
-#ifdef MEV_EXP_NOROAD
-    for (int qq = lane; qq < total; qq += WAVE) res[qq] = S << 1;
-    q = -1;
-#endif
-    while (ballot(q >= 0) != 0ull) {
-        // branch-free body: every lane evaluates its probe k; idle lanes only skip the store
-        const bool act = q >= 0;
-        const bool past = k >= S;
-        const int kc = past ? S - 1 : k;
+    // the reference's stop test of march probe k at (cx_, cy_) + d_k (dx_, dy_):
+    // returns the beam's result (k << 1 | hit; S << 1 past the last probe) or -1
+    // to go on, and the probe's real point
+    auto probe = [&](float cx_, float cy_, float dx_, float dy_, int k_, float& fx, float& fy) -> int {
+        const bool past = k_ >= S;
+        const int kc = past ? S - 1 : k_;
         const float d = TAB ? p.dist_tab[kc] : (float)kc * stp;
-        const float fx = cx + dx * d;
-        const float fy = cy + dy * d;
+        fx = cx_ + dx_ * d;
+        fy = cy_ + dy_ * d;
         const int px = (int)fx, py = (int)fy;
         // exact reference predicates at the truncated pixel: screen, then
         // (k > 0) road == RoadGeometry::is_on_road at integer pixels:
@@ -1271,12 +1233,97 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
         const float iax = fabs_f((float)(px - 375)), iay = fabs_f((float)(py - 375));
         const float qdx = iax - ccen, qdy = iay - ccen;
         const float onv = fmaxf(fminf(fminf(iax, iay) - rwf, fmaxf(iax, iay) - ccen), cr2p1 - (qdx * qdx + qdy * qdy));
-        const bool stop = !past & (off_screen | ((k > 0) & (onv > 0.0f)));
+        const bool stop = off_screen | ((k_ > 0) & (onv > 0.0f));
+        return past ? (S << 1) : (stop ? ((k_ << 1) | (off_screen ? 0 : 1)) : -1);
+    };
+    // probes k_ .. k_ + NPR - 1 in march order: the first stop wins; (fx, fy) is
+    // the last probe's point
+    auto probes = [&](float cx_, float cy_, float dx_, float dy_, int k_, float& fx, float& fy) -> int {
+        int r = -1;
+#pragma unroll
+        for (int t = 0; t < LIDAR_NPR; ++t) {
+            const int c = probe(cx_, cy_, dx_, dy_, k_ + t, fx, fy);
+            r = r >= 0 ? r : c;
+        }
+        return r;
+    };
+
+    // directions; then the first probes of each beam: probe 0 is only
+    // screen-tested (no road test at dist 0); if the car centre is on screen,
+    // every probe within the safe distance from it is skipped, and the next
+    // LIDAR_NPR probes are tested right here — most beams stop among them (the
+    // edge of the road lies within a few steps of the provably safe stretch).
+    // Beams still running go to the queue of the pooled march.
+    unsigned short* queue = reinterpret_cast<unsigned short*>(base + lay.queue);
+    int qn = 0;
+    for (int j = 0; j < nal; ++j) {
+        const float4 a = ag[j];
+        const int px = (int)a.x, py = (int)a.y;
+        const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
+        for (int b0 = 0; b0 < R; b0 += WAVE) {
+            const int b = b0 + lane;
+            bool pend = false;
+            if (b < R) {
+                float sn, cs;
+                sincosf(a.z + p.rel_angles[b], &sn, &cs);  // Lidar.cpp:24-26
+                const float dx = cs, dy = -sn;
+                dir[j * R + b] = make_float2(dx, dy);
+                int k1 = 0;
+                if (pmax < (unsigned)WIDTH) {
+                    const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
+                    const float safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
+                    k1 = (safe >= two_stp) ? (int)(safe * inv_stp) : 1;
+                }
+#ifdef MEV_EXP_NOROAD
+                res[j * R + b] = S << 1;
+#else
+                float fx, fy;
+                const int r = probes(a.x, a.y, dx, dy, k1, fx, fy);
+                res[j * R + b] = r >= 0 ? r : k1 + LIDAR_NPR;  // result, or the next probe to test
+                pend = r < 0;
+#endif
+            }
+            const unsigned long long pm = ballot(pend);
+            if (pend) queue[qn + lane_rank(pm)] = (unsigned short)(j * R + b);
+            qn += __popcll(pm);
+        }
+    }
+    wave_lds_sync();
+
+    // ---- phase 2: pooled road + screen march of the queued beams
+    // (Lidar.cpp:31-48, first stop wins): LIDAR_NPR exact probes, then a jump
+    // over the provably safe stretch after the last one
+    const float invR = 1.0f / (float)R;
+    int next = qn < WAVE ? qn : WAVE;
+    int slot = lane < qn ? (int)queue[lane] : -1;
+    float cx = 0.0f, cy = 0.0f, dx = 0.0f, dy = 0.0f, idx = 0.0f, idy = 0.0f, iadx = 0.0f, iady = 0.0f;
+    int k = 0;
+    auto load_beam = [&](int qq) {
+        // agent of beam slot qq = j*R + b: exact float quotient (qq < 2^20, R <= 1024)
+        const int j = (int)(((float)qq + 0.5f) * invR);
+        const float4 a = ag[j];
+        const float2 d = dir[qq];
+        cx = a.x; cy = a.y; dx = d.x; dy = d.y;
+        idx = __builtin_amdgcn_rcpf(dx);
+        idy = __builtin_amdgcn_rcpf(dy);
+        iadx = fabs_f(idx);
+        iady = fabs_f(idy);
+        k = res[qq];
+    };
+    if (slot >= 0) load_beam(slot);
+#ifdef MEV_ITERS
+    int iters = 0;
+#endif
+    while (ballot(slot >= 0) != 0ull) {
+        // branch-free body: every lane evaluates its probes; idle lanes only skip the store
+        const bool act = slot >= 0;
+        float fx, fy;
+        const int r = probes(cx, cy, dx, dy, k, fx, fy);
         const float safe = road_safe(fx, fy, dx, dy, idx, idy, iadx, iady, rwm, ccen, crf);
-        // probes k+1 .. k+j-1 lie within (j-1)*step <= safe of this point
-        const int kn = k + ((safe >= two_stp) ? (int)(safe * inv_stp) : 1);
-        const bool fin = act & (past | stop | (kn >= S));
-        if (fin) res[q] = stop ? ((k << 1) | (off_screen ? 0 : 1)) : (S << 1);
+        // probes kl+1 .. kl+j-1 lie within (j-1)*step <= safe of the last probe kl
+        const int kn = k + (LIDAR_NPR - 1) + ((safe >= two_stp) ? (int)(safe * inv_stp) : 1);
+        const bool fin = act & ((r >= 0) | (kn >= S));
+        if (fin) res[slot] = r >= 0 ? r : (S << 1);
         k = kn;
 #ifdef MEV_ITERS
         ++iters;
@@ -1285,8 +1332,8 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
         if (fm != 0ull) {
             if (fin) {
                 const int nq = next + lane_rank(fm);
-                q = nq < total ? nq : -1;
-                if (q >= 0) load_beam(q);
+                slot = nq < qn ? (int)queue[nq] : -1;
+                if (slot >= 0) load_beam(slot);
             }
             next += __popcll(fm);
         }
