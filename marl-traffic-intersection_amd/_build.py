@@ -41,7 +41,9 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "exp_none": ["-DMEV_EXP_NOROAD", "-DMEV_EXP_NOCARS"], "exp_iters": ["-DMEV_ITERS"],
                "stampsx": ["-DMEV_STAMPS", "-DMEV_STAMPS_X"],
                # exact variants: probes per road-march step (product: 3)
-               "npr1": ["-DMEV_LIDAR_NPR=1"], "npr2": ["-DMEV_LIDAR_NPR=2"], "npr4": ["-DMEV_LIDAR_NPR=4"]}
+               "npr1": ["-DMEV_LIDAR_NPR=1"], "npr2": ["-DMEV_LIDAR_NPR=2"], "npr4": ["-DMEV_LIDAR_NPR=4"],
+               # deliberately wrong: beam spans narrowed, to show the stress test catches it
+               "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 VARIANTS.update(EXPERIMENTS)
 
 

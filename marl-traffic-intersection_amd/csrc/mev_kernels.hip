@@ -1345,7 +1345,7 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
 
     // ---- phase 3: cars (Lidar.cpp:50-80) as a list of (agent, box, beam) pairs.
     // A box can only stop the beams whose ray enters its slab box, i.e. the
-    // beams inside the angular span of its real slab box seen from the agent (+-1 beam):
+    // beams inside the angular span of its real slab box seen from the agent:
     // 3a lists (agent, candidate box) segments, 3b turns each into beam ranges,
     // 3c packs the pairs of an agent into the 64 lanes (scan + segment lookup)
     // and resolves each by exact probes inside its slab range, keeping the
@@ -1373,8 +1373,9 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     if (lane == 0) seg_beg[nal] = M;
     wave_lds_sync();
     // 3b: beam ranges.  Beam b points along h + rel[b], rel[b] = rel[0] + b*dphi;
-    // the range covers the span of the box's real slab (box_lo/box_hi), with one
-    // beam of margin (fast atan2, error ~1e-5 rad << one beam).
+    // the range covers the angular span of the box's real slab (box_lo/box_hi):
+    // a ray outside it never meets the slab, so none of its probes can land in
+    // the box.
     const float rel0 = p.rel_angles[0];
     const float dphi = R > 1 ? (p.rel_angles[R - 1] - rel0) / (float)(R - 1) : 1.0f;
     const float idphi = 1.0f / dphi;
@@ -1402,12 +1403,19 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
             }
             float w = phc + dmin - a.z - rel0;
             w -= 6.28318531f * floorf(w * 0.159154943f);  // [0, 2*pi)
-            const float ulo = w * idphi, uhi = ulo + (dmax - dmin) * idphi;
+            // beams b with rel0 + b*dphi in the span, widened by 2e-4 rad (20x the
+            // error of atan2_fast and of the linear model of the host's angles)
+#ifdef MEV_EXP_BADRANGE
+            const float marg = -0.02f;  // test-of-the-test: spans too narrow, hits must be dropped
+#else
+            const float marg = 2.0e-4f;
+#endif
+            const float ulo = (w - marg) * idphi, uhi = (w + (dmax - dmin) + marg) * idphi;
             int lo[3], cn[3];
 #pragma unroll
             for (int sft = 0; sft < 3; ++sft) {
                 const float sh = (float)(sft - 1) * period;
-                int l0 = (int)floorf(ulo + sh) - 1, l1 = (int)ceilf(uhi + sh) + 1;
+                int l0 = (int)ceilf(ulo + sh), l1 = (int)floorf(uhi + sh);
                 l0 = l0 < 0 ? 0 : l0;
                 l1 = l1 > R - 1 ? R - 1 : l1;
                 lo[sft] = l0;
@@ -1452,7 +1460,16 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
                     float lo = 0.0f, hi = 1.0e6f;
                     slab_clip(a.x, dd.x, __builtin_amdgcn_rcpf(dd.x), box_lo(bx.x), box_hi(bx.y), lo, hi);
                     slab_clip(a.y, dd.y, __builtin_amdgcn_rcpf(dd.y), box_lo(bx.z), box_hi(bx.w), lo, hi);
-                    int ka = (int)(fmaxf(lo, 0.0f) * inv_stp) - 1, kb = (int)(fminf(hi, 1.0e6f) * inv_stp) + 1;
+                    // d_k = k*step exactly without the table: the slab's 0.01 px absorbs the
+                    // rounding of k = lo/step; the table's accumulated distances get one probe
+                    int ka, kb;
+                    if (TAB) {
+                        ka = (int)(fmaxf(lo, 0.0f) * inv_stp) - 1;
+                        kb = (int)(fminf(hi, 1.0e6f) * inv_stp) + 1;
+                    } else {
+                        ka = (int)ceilf(fmaxf(lo, 0.0f) * inv_stp);
+                        kb = (int)(fminf(hi, 1.0e6f) * inv_stp);
+                    }
                     ka = ka < 1 ? 1 : ka;  // no car test at dist == 0
                     kb = kb < kr - 1 ? kb : kr - 1;
                     if (lo > hi) kb = 0;
