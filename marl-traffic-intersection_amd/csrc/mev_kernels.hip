@@ -1069,7 +1069,9 @@ __device__ inline float road_safe(float fx, float fy, float dx, float dy, float 
     const float sx = ax < rwm ? rwm * iadx - rx * idx : 0.0f;
     const float sy = ay < rwm ? rwm * iady - ry * idy : 0.0f;
     const float sqm = ccen - 1.55f, rg = crf + 2.0f;
-    const float ocx = rx - (rx >= 0.0f ? ccen : -ccen), ocy = ry - (ry >= 0.0f ? ccen : -ccen);
+    // the quadrant the ray is in, or heads into from an axis (rx == 0: the sign of dx)
+    const float qx = rx != 0.0f ? rx : dx, qy = ry != 0.0f ? ry : dy;
+    const float ocx = rx - (qx >= 0.0f ? ccen : -ccen), ocy = ry - (qy >= 0.0f ? ccen : -ccen);
     const float bq = ocx * dx + ocy * dy;
     const float cq = ocx * ocx + ocy * ocy - rg * rg;
     const float disc = bq * bq - cq;

@@ -50,8 +50,8 @@ def safe_v0(fx, fy, dx, dy, rw):
     sx = np.where(ax < rwm, rwm * iadx - rx * idx, 0)
     sy = np.where(ay < rwm, rwm * iady - ry * idy, 0)
     sqm, rg = ccen - f32(1.55), crf + f32(2)
-    ocx = rx - np.where(rx >= 0, ccen, -ccen)
-    ocy = ry - np.where(ry >= 0, ccen, -ccen)
+    ocx = rx - np.where(np.where(rx != 0, rx, dx) >= 0, ccen, -ccen)
+    ocy = ry - np.where(np.where(ry != 0, ry, dy) >= 0, ccen, -ccen)
     return _rest(fx, fy, dx, dy, idx, idy, iadx, iady, rx, ry, ax, ay, sx, sy, sqm, rg, ocx, ocy, f32(0.5), f32(748.5))
 
 
@@ -70,8 +70,8 @@ def safe_v1(fx, fy, dx, dy, rw, strip_half=None):
     sx = np.where(ax < rwm, rwm * iadx - rx * idx, 0)
     sy = np.where(ay < rwm, rwm * iady - ry * idy, 0)
     sqm, rg = ccen + f32(0.5) - eps, crf + f32(0.7072) + eps
-    ocx = rx - np.where(rx >= 0, ccen, -ccen)
-    ocy = ry - np.where(ry >= 0, ccen, -ccen)
+    ocx = rx - np.where(np.where(rx != 0, rx, dx) >= 0, ccen, -ccen)
+    ocy = ry - np.where(np.where(ry != 0, ry, dy) >= 0, ccen, -ccen)
     return _rest(fx, fy, dx, dy, idx, idy, iadx, iady, rx, ry, ax, ay, sx, sy, sqm, rg, ocx, ocy, eps, f32(750) - eps)
 
 
