@@ -1133,7 +1133,7 @@ __device__ inline int lane_rank(unsigned long long mask) {
 // before the car phase and shares the segment area.
 // Probes tested per step of the road march (phase 1 and each pooled iteration).
 #ifndef MEV_LIDAR_NPR
-#define MEV_LIDAR_NPR 3
+#define MEV_LIDAR_NPR 2
 #endif
 constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
 
@@ -1212,7 +1212,6 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     const int S = p.lidar_steps;
     const float rwf = (float)p.irw;
     const float inv_stp = __builtin_amdgcn_rcpf(stp);
-    const float two_stp = 2.0f * stp;
     const float crf = CORNER_RADIUS, ccen = rwf + crf;
     const float cr2p1 = crf * crf + 1.0f;
     const float rwm = rwf - 1.5f;
@@ -1274,7 +1273,8 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
                 if (pmax < (unsigned)WIDTH) {
                     const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
                     const float safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
-                    k1 = (safe >= two_stp) ? (int)(safe * inv_stp) : 1;
+                    // probes 1 .. j lie within j*step <= safe of the centre
+                    k1 = 1 + ((safe >= stp) ? (int)(safe * inv_stp) : 0);
                 }
 #ifdef MEV_EXP_NOROAD
                 res[j * R + b] = S << 1;
@@ -1322,8 +1322,8 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
         float fx, fy;
         const int r = probes(cx, cy, dx, dy, k, fx, fy);
         const float safe = road_safe(fx, fy, dx, dy, idx, idy, iadx, iady, rwm, ccen, crf);
-        // probes kl+1 .. kl+j-1 lie within (j-1)*step <= safe of the last probe kl
-        const int kn = k + (LIDAR_NPR - 1) + ((safe >= two_stp) ? (int)(safe * inv_stp) : 1);
+        // probes kl+1 .. kl+j lie within j*step <= safe of the last probe kl = k + NPR - 1
+        const int kn = k + LIDAR_NPR + ((safe >= stp) ? (int)(safe * inv_stp) : 0);
         const bool fin = act & ((r >= 0) | (kn >= S));
         if (fin) res[slot] = r >= 0 ? r : (S << 1);
         k = kn;

@@ -168,12 +168,29 @@ MEV_HD void sincosf_reduced_impl(float y, float* sinp, float* cosp) {
     }
     int n;
     const double x = reduce_fast<FMA>((double)y, kSinCos[0], &n);
-    const double s = kSinCos[0].sign[n & 3];
-    float sv, cv;
-    sincosf_poly<FMA>(x * s, x * x, kSinCos[(n & 2) ? 1 : 0], n, &sv, &cv);
+    // no per-lane table loads: sign[n & 3] = {1, -1, -1, 1} multiplies x by +-1
+    // (an exact negation), and kSinCos[1] is kSinCos[0] with the cosine
+    // coefficients c0..c4 negated, so its cosine polynomial -- and the rounded
+    // float -- is exactly the negation of kSinCos[0]'s
+    const double xs = ((n + 1) & 2) ? -x : x;
+    const SinCosTab& p = kSinCos[0];
+    const double x2 = x * x;
+    const double x4 = x2 * x2;
+    const double x3 = x2 * xs;
+    const double c2 = madd<FMA>(p.c3, x2, p.c4);
+    const double s1 = madd<FMA>(p.s2, x2, p.s3);
+    const double c1 = madd<FMA>(p.c0, x2, p.c1);
+    const double x5 = x3 * x2;
+    const double x6 = x4 * x2;
+    const double sp = madd<FMA>(xs, x3, p.s1);
+    const double cp = madd<FMA>(c1, x4, p.c2);
+    const float sv = (float)madd<FMA>(sp, x5, s1);
+    float cv = (float)madd<FMA>(cp, x6, c2);
+    cv = (n & 2) ? -cv : cv;
     const bool tiny = abstop12(y) < abstop12(0x1p-12f);  // glibc's shortcut (keeps the sign of -0)
-    *sinp = tiny ? y : sv;
-    *cosp = tiny ? 1.0f : cv;
+    const float so = (n & 1) ? cv : sv, co = (n & 1) ? sv : cv;
+    *sinp = tiny ? y : so;
+    *cosp = tiny ? 1.0f : co;
 }
 
 // the simulator's sincosf (glibc results; single path below 120)
