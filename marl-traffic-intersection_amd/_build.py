@@ -39,9 +39,9 @@ VARIANTS = {"": [], "stamps": ["-DMEV_STAMPS"]}
 # timing-only experiment builds (wrong results by construction; never used by the product)
 EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOCARS"],
                "exp_none": ["-DMEV_EXP_NOROAD", "-DMEV_EXP_NOCARS"], "exp_iters": ["-DMEV_ITERS"],
-               "stampsx": ["-DMEV_STAMPS", "-DMEV_STAMPS_X"],
-               # exact variants: probes per road-march step (product: 3)
-               "npr1": ["-DMEV_LIDAR_NPR=1"], "npr2": ["-DMEV_LIDAR_NPR=2"], "npr4": ["-DMEV_LIDAR_NPR=4"],
+               "stampsx": ["-DMEV_STAMPS", "-DMEV_STAMPS_X"], "stampsy": ["-DMEV_STAMPS", "-DMEV_STAMPS_Y"],
+               # exact variants: probes per road-march step (product: 2)
+               "npr1": ["-DMEV_LIDAR_NPR=1"], "npr3": ["-DMEV_LIDAR_NPR=3"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
                "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 VARIANTS.update(EXPERIMENTS)

@@ -31,16 +31,23 @@ constexpr int WAVE = 64;
         __builtin_amdgcn_wave_barrier();                                 \
         if (threadIdx.x == 0) p.debug[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-#ifdef MEV_STAMPS_X
+#if defined(MEV_STAMPS_X)
 #define STAMP(k) do { if ((k) == 0 || (k) == 6) STAMP_RAW(k); } while (0)
 #define STAMPX(k) STAMP_RAW(k)
+#define STAMPY(k) do {} while (0)
+#elif defined(MEV_STAMPS_Y)  // stamps 1-5 in resolution, write-back, obstacles and the obs head
+#define STAMP(k) do { if ((k) == 0 || (k) == 6) STAMP_RAW(k); } while (0)
+#define STAMPX(k) do {} while (0)
+#define STAMPY(k) STAMP_RAW(k)
 #else
 #define STAMP(k) STAMP_RAW(k)
 #define STAMPX(k) do {} while (0)
+#define STAMPY(k) do {} while (0)
 #endif
 #else
 #define STAMP(k) do {} while (0)
 #define STAMPX(k) do {} while (0)
+#define STAMPY(k) do {} while (0)
 #endif
 constexpr int MAXN = 64;
 constexpr int MAXK = 64;
@@ -848,6 +855,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
             if (hits) { donem |= hits | (1ull << a); crash |= hits | (1ull << a); }
             if (TRAFFIC && ((npcm >> a) & 1ull)) { donem |= 1ull << a; crash |= 1ull << a; }
         }
+        STAMPY(1);
         if ((crash >> i) & 1ull) { done_i = 1; st_i = ST_CRASH_CAR; }
         if (done_i) {
             if (st_i == ST_CRASH_CAR) rew_i += p.k_cv;
@@ -876,6 +884,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         }
     }
     wave_lds_sync();
+    STAMPY(2);
     // respawn crashed egos (Car::respawn, Car.cpp:76-84; :339-351) and write the
     // final ego state back (lane = agent)
     for (int i = tid; i < N; i += WAVE) {
@@ -902,6 +911,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         }
     }
     wave_lds_sync();
+    STAMPY(3);
 
     STAMP(4);
     // ---- LiDAR obstacle table (:374-388): every ego (alive or not), then NPCs,
@@ -946,6 +956,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
     }
 
     STAMP(5);
+    STAMPY(4);
     // ---- observation head (:418-520)
     const int C = N + (TRAFFIC ? ncnt : 0);
     if (C <= 8) {
@@ -982,6 +993,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
                 rank += (vk != 0) && (dk < d || (dk == d && kk < j));
             }
             const int nb = __builtin_popcountll(ballot(valid) & gmask);
+            STAMPY(5);
             if (act) {
                 float* row = out.obs + (size_t)(e * N + i) * p.D;
                 if (!alv) {
@@ -1127,10 +1139,11 @@ __device__ inline int lane_rank(unsigned long long mask) {
 // group's alive agents, dir float2[G*R] beam directions, res int[G*R] stop of
 // each beam (k << 1 | hit), and the car-phase segments: seg_jo int[C]
 // (agent << 8 | box), seg_rg int4[C] (three beam ranges lo | count << 16, total),
-// seg_bx int4[C] (the box), seg_beg int[G+1]; C = G * cmax, cmax = the most
+// seg_bx int4[C] (the box); C = G * cmax, cmax = the most
 // candidate boxes one agent can have (every other ego, plus the NPC slots).
 // The road march's queue of unfinished beams, ushort[G*R], is only live
 // before the car phase and shares the segment area.
+
 // Probes tested per step of the road march (phase 1 and each pooled iteration).
 #ifndef MEV_LIDAR_NPR
 #define MEV_LIDAR_NPR 2
@@ -1138,7 +1151,7 @@ __device__ inline int lane_rank(unsigned long long mask) {
 constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
 
 struct LidarLayout {
-    int ag, dir, res, seg_jo, seg_rg, seg_bx, seg_beg, queue, bytes;
+    int ag, dir, res, seg_jo, seg_rg, seg_bx, queue, bytes;
 };
 
 __host__ __device__ inline int lidar_cand_max(const SimParams& p) { return p.N - 1 + (p.traffic ? p.K : 0); }
@@ -1156,8 +1169,6 @@ __host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax) {
     L.seg_jo = off; off += C * 4;
     L.queue = L.seg_rg;
     if (off < L.queue + G * R * 2) off = L.queue + G * R * 2;
-    off = (off + 3) & ~3;
-    L.seg_beg = off; off += (G + 1) * 4;
     L.bytes = (off + 15) & ~15;
     return L;
 }
@@ -1349,14 +1360,13 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     // A box can only stop the beams whose ray enters its slab box, i.e. the
     // beams inside the angular span of its real slab box seen from the agent:
     // 3a lists (agent, candidate box) segments, 3b turns each into beam ranges,
-    // 3c packs the pairs of an agent into the 64 lanes (scan + segment lookup)
+    // 3c packs the pairs of all the group's agents into the 64 lanes (scan + segment lookup)
     // and resolves each by exact probes inside its slab range, keeping the
     // earliest stop per beam with an LDS atomicMin on (k << 1 | hit); 3d writes
     // the LiDAR block.
     int* seg_jo = reinterpret_cast<int*>(base + lay.seg_jo);
     int4* seg_rg = reinterpret_cast<int4*>(base + lay.seg_rg);
     int4* seg_bx = reinterpret_cast<int4*>(base + lay.seg_bx);
-    int* seg_beg = reinterpret_cast<int*>(base + lay.seg_beg);
     const int OB = p.ob_stride;
     int M = 0;
     for (int j = 0; j < nal; ++j) {  // 3a
@@ -1366,13 +1376,11 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
 #else
         const unsigned long long c0 = p.ob_cand[2 * g], c1 = p.ob_cand[2 * g + 1];
 #endif
-        if (lane == 0) seg_beg[j] = M;
         const int n0 = __popcll(c0);
         if ((c0 >> lane) & 1ull) seg_jo[M + lane_rank(c0)] = (j << 8) | lane;
         if ((c1 >> lane) & 1ull) seg_jo[M + n0 + lane_rank(c1)] = (j << 8) | (lane + WAVE);
         M += n0 + __popcll(c1);
     }
-    if (lane == 0) seg_beg[nal] = M;
     wave_lds_sync();
     // 3b: beam ranges.  Beam b points along h + rel[b], rel[b] = rel[0] + b*dphi;
     // the range covers the angular span of the box's real slab (box_lo/box_hi):
@@ -1428,67 +1436,71 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
         seg_rg[m] = rg;
     }
     wave_lds_sync();
-    const float d1 = march_dist(p, 1);
-    for (int j = 0; j < nal; ++j) {  // 3c
-        const float4 a = ag[j];
-        const int sbeg = seg_beg[j], send = seg_beg[j + 1];
-        for (int cb = sbeg; cb < send; cb += WAVE) {
-            const int nseg = send - cb < WAVE ? send - cb : WAVE;
-            const int cnt = lane < nseg ? seg_rg[cb + lane].w : 0;
-            int incl = cnt;
+    // 3c: the pairs of all the group's agents packed into the 64 lanes
+    for (int cb = 0; cb < M; cb += WAVE) {
+        const int nseg = M - cb < WAVE ? M - cb : WAVE;
+        const int cnt = lane < nseg ? seg_rg[cb + lane].w : 0;
+        int incl = cnt;
 #pragma unroll
-            for (int off = 1; off < WAVE; off <<= 1) {
-                const int t = __shfl_up(incl, off);
-                if (lane >= off) incl += t;
+        for (int off = 1; off < WAVE; off <<= 1) {
+            const int t = __shfl_up(incl, off);
+            if (lane >= off) incl += t;
+        }
+        const int excl = incl - cnt;
+        const int T = __builtin_amdgcn_readlane(incl, WAVE - 1);
+        for (int q0 = 0; q0 < T; q0 += WAVE) {
+            const int q = q0 + lane;
+            // segment of pair q: the last m < nseg with excl[m] <= q (binary search)
+            int sm = 0;
+#pragma unroll
+            for (int st = WAVE / 2; st > 0; st >>= 1) {
+                const int c = sm + st;
+                const int ec = __shfl(excl, c < nseg ? c : 0);
+                sm = (c < nseg && ec <= q) ? c : sm;
             }
-            const int excl = incl - cnt;
-            const int T = __builtin_amdgcn_readlane(incl, WAVE - 1);
-            for (int q0 = 0; q0 < T; q0 += WAVE) {
-                const int q = q0 + lane;
-                int sm = 0;
-                for (int mm = 1; mm < nseg; ++mm) sm = __builtin_amdgcn_readlane(excl, mm) <= q ? mm : sm;
-                const int r = q - __shfl(excl, sm);
-                if (q < T) {
-                    const int4 rg = seg_rg[cb + sm];
-                    const int4 bx = seg_bx[cb + sm];
-                    const int cA = rg.x >> 16, cB = rg.y >> 16;
-                    const int b = r < cA ? (rg.x & 0xffff) + r
-                                         : (r < cA + cB ? (rg.y & 0xffff) + r - cA : (rg.z & 0xffff) + r - cA - cB);
-                    const int slot = j * R + b;
-                    const int kr = res[slot] >> 1;
-                    const float2 dd = dir[slot];
-                    // probes that can land in the box: the ray's interval inside the
-                    // box's real slab (see box_lo), as a superset range of k ...
-                    float lo = 0.0f, hi = 1.0e6f;
-                    slab_clip(a.x, dd.x, __builtin_amdgcn_rcpf(dd.x), box_lo(bx.x), box_hi(bx.y), lo, hi);
-                    slab_clip(a.y, dd.y, __builtin_amdgcn_rcpf(dd.y), box_lo(bx.z), box_hi(bx.w), lo, hi);
-                    // d_k = k*step exactly without the table: the slab's 0.01 px absorbs the
-                    // rounding of k = lo/step; the table's accumulated distances get one probe
-                    int ka, kb;
-                    if (TAB) {
-                        ka = (int)(fmaxf(lo, 0.0f) * inv_stp) - 1;
-                        kb = (int)(fminf(hi, 1.0e6f) * inv_stp) + 1;
-                    } else {
-                        ka = (int)ceilf(fmaxf(lo, 0.0f) * inv_stp);
-                        kb = (int)(fminf(hi, 1.0e6f) * inv_stp);
-                    }
-                    ka = ka < 1 ? 1 : ka;  // no car test at dist == 0
-                    kb = kb < kr - 1 ? kb : kr - 1;
-                    if (lo > hi) kb = 0;
-                    // ... resolved by exact probes in march order
-                    for (int kk = ka; kk <= kb; ++kk) {
-                        const float d = march_dist(p, kk);
-                        const int px = (int)(a.x + dd.x * d), py = (int)(a.y + dd.y * d);
-                        if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) {
-                            atomicMin(&res[slot], (kk << 1) | 1);
-                            break;
-                        }
+            const int r = q - __shfl(excl, sm);
+            if (q < T) {
+                const int m = cb + sm;
+                const int j = seg_jo[m] >> 8;
+                const float4 a = ag[j];
+                const int4 rg = seg_rg[m];
+                const int4 bx = seg_bx[m];
+                const int cA = rg.x >> 16, cB = rg.y >> 16;
+                const int b = r < cA ? (rg.x & 0xffff) + r
+                                     : (r < cA + cB ? (rg.y & 0xffff) + r - cA : (rg.z & 0xffff) + r - cA - cB);
+                const int slot = j * R + b;
+                const int kr = res[slot] >> 1;
+                const float2 dd = dir[slot];
+                // probes that can land in the box: the ray's interval inside the
+                // box's real slab (see box_lo), as a superset range of k ...
+                float lo = 0.0f, hi = 1.0e6f;
+                slab_clip(a.x, dd.x, __builtin_amdgcn_rcpf(dd.x), box_lo(bx.x), box_hi(bx.y), lo, hi);
+                slab_clip(a.y, dd.y, __builtin_amdgcn_rcpf(dd.y), box_lo(bx.z), box_hi(bx.w), lo, hi);
+                // d_k = k*step exactly without the table: the slab's 0.01 px absorbs the
+                // rounding of k = lo/step; the table's accumulated distances get one probe
+                int ka, kb;
+                if (TAB) {
+                    ka = (int)(fmaxf(lo, 0.0f) * inv_stp) - 1;
+                    kb = (int)(fminf(hi, 1.0e6f) * inv_stp) + 1;
+                } else {
+                    ka = (int)ceilf(fmaxf(lo, 0.0f) * inv_stp);
+                    kb = (int)(fminf(hi, 1.0e6f) * inv_stp);
+                }
+                ka = ka < 1 ? 1 : ka;  // no car test at dist == 0
+                kb = kb < kr - 1 ? kb : kr - 1;
+                if (lo > hi) kb = 0;
+                // ... resolved by exact probes in march order
+                for (int kk = ka; kk <= kb; ++kk) {
+                    const float d = march_dist(p, kk);
+                    const int px = (int)(a.x + dd.x * d), py = (int)(a.y + dd.y * d);
+                    if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) {
+                        atomicMin(&res[slot], (kk << 1) | 1);
+                        break;
                     }
                 }
             }
         }
     }
-    (void)d1;
     wave_lds_sync();
     for (int j = 0; j < nal; ++j) {  // 3d: Lidar::normalized (:92-98)
         const int g = __float_as_int(ag[j].w);
