@@ -3,9 +3,10 @@
 Workload (BASELINE.json metric, config 3): per GPU 4096 envs x 8 ego agents,
 64-beam LiDAR, team reward, respawn on, max_steps 2000, per-env auto-reset.
 One "step" = IntersectionEnv::step + get_observations for all of the GPU's
-4096 envs: the k_cars kernel (one wave per env: physics, status, collisions,
-rewards, respawn, observation head) followed by k_lidar (one wave per group
-of 4 agents: the 64-beam march over a pooled beam queue), with the actions already resident in HBM (pre-generated
+4096 envs: one launch of the fused k_step kernel (one wave per env: physics,
+status, collisions, rewards, respawn, observation head, then the 64-beam LiDAR
+of the env's 8 agents as one pooled beam queue, all from the wave's LDS), with
+the actions already resident in HBM (pre-generated
 uniform [-1, 1) f32) and obs [E, 8, 95] / reward / done / status /
 terminated / truncated written to HBM.
 
@@ -17,8 +18,8 @@ step's packed outputs gathered to rank 0 with one RCCL gather over xGMI,
 overlapped with the next step (double buffered).
 
 Prints ONE JSON line on rank 0, including "roofline" for the dominant kernel
-(k_lidar; device durations from HIP events the library records on its stream
-around each kernel during the timed region) and "cpu_baseline" (the
+(k_step, the only kernel of a step; device durations from HIP events the
+library records on its stream around it during the timed region) and "cpu_baseline" (the
 reference's own C++ simulator, compiled from its sources, on this host).
 """
 from __future__ import annotations
@@ -89,8 +90,10 @@ def main():
     ap.add_argument("--gather", action="store_true",
                     help="also gather every step's packed outputs to rank 0 (one RCCL gather over xGMI)")
     ap.add_argument("--no-kernel-events", action="store_true", help="do not record per-kernel HIP events")
-    ap.add_argument("--event-every", type=int, default=4, help="record the per-kernel events on every n-th step")
+    ap.add_argument("--event-every", type=int, default=10, help="record the per-kernel events on every n-th step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--step-kernel", type=int, default=0,
+                    help="0 automatic (fused k_step at this size), 1 k_cars + k_lidar, 2 fused")
     args = ap.parse_args()
 
     import torch
@@ -115,6 +118,7 @@ def main():
 
     env = mev.Handle(num_envs=E, num_agents=N, lidar_rays=RAYS, use_team_reward=1, respawn_enabled=1,
                      max_steps=2000, seed=rank, device=local_rank)
+    env.set_step_kernel(args.step_kernel)
     stream = torch.cuda.Stream(dev)  # the env kernels, the events and the gather are all ordered on it
     torch.cuda.set_stream(stream)
     env.set_stream(stream.cuda_stream)
@@ -164,6 +168,7 @@ def main():
     elapsed = time.perf_counter() - t0
     stream_ms = ev0.elapsed_time(ev1) / K
     cars_ms = lidar_ms = None
+    fused = env.step_kernel() == 2  # one k_step launch per step (else k_cars + k_lidar)
     if not args.no_kernel_events:
         c_sum, l_sum, n_steps = env.kernel_times()
         assert n_steps == (K + args.event_every - 1) // args.event_every, (n_steps, K)
@@ -183,22 +188,34 @@ def main():
         total_agent_steps = world * E * N * K
         value = total_agent_steps / elapsed
         roofline = None
-        if lidar_ms is not None:
+        traffic_of = {}
+        pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_file):
+            try:
+                pm = json.load(open(pmc_file))
+                if pm.get("envs") == E and pm.get("agents") == N and pm.get("rays") == RAYS:
+                    traffic_of = {k: v.get("hbm_bytes_per_launch") for k, v in pm.items() if isinstance(v, dict)}
+            except Exception:
+                traffic_of = {}
+        if cars_ms is not None and fused:
+            pb = algorithmic_bytes_per_agent_step(RAYS) * E * N
+            achieved = pb / (cars_ms * 1e-3) / 1e9
+            roofline = {
+                "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic_of.get("k_step"),
+                "kernel": "mev::k_step<false, false>", "kernel_ms": round(cars_ms, 5),
+                "algorithmic_bytes_per_agent_step": algorithmic_bytes_per_agent_step(RAYS), "bytes_per_launch": pb,
+                "kernel_events": f"library HIP events around the k_step launch on every {args.event_every}th timed step",
+                "step_pipeline": {"stream_ms_per_step": round(stream_ms, 5),
+                                  "achieved_GBs": round(pb / (stream_ms * 1e-3) / 1e9, 3)},
+            }
+        elif lidar_ms is not None:
             lb = lidar_bytes_per_agent_step(RAYS) * E * N
             pb = algorithmic_bytes_per_agent_step(RAYS) * E * N
             achieved = lb / (lidar_ms * 1e-3) / 1e9
-            traffic = None
-            pmc_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc_file):
-                try:
-                    pm = json.load(open(pmc_file))
-                    if pm.get("envs") == E and pm.get("agents") == N and pm.get("rays") == RAYS:
-                        traffic = pm.get("k_lidar", {}).get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
             roofline = {
                 "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic_of.get("k_lidar"),
                 "kernel": "mev::k_lidar<false>", "kernel_ms": round(lidar_ms, 5),
                 "algorithmic_bytes_per_agent_step": lidar_bytes_per_agent_step(RAYS), "bytes_per_launch": lb,
                 "other_kernels": {"mev::k_cars<false>": {"kernel_ms": round(cars_ms, 5),

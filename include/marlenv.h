@@ -207,9 +207,21 @@ int mev_debug_stamps(mev_handle* h, uint64_t* out);
  * k_lidar, and after k_lidar (every = 0 disables).  mev_kernel_times returns
  * the summed device durations (ms) of the two kernels over the timed steps
  * and their count since the previous call (or since enabling), then clears
- * them; it waits for the recorded steps to finish. */
+ * them; it waits for the recorded steps to finish.  With the fused step kernel
+ * (mev_set_step_kernel) cars_ms holds k_step's duration and lidar_ms is 0. */
 int mev_kernel_timing(mev_handle* h, int32_t every);
 int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* steps);
+/* Scheduling (results are identical either way): which kernels run a step.
+ * 1 = k_cars (one wave per env) then k_lidar (one wave per group of agents),
+ * with the obstacle table handed over through HBM; 2 = the fused k_step, one
+ * wave per env running both parts back to back from its LDS; 0 = automatic
+ * (fused for E >= 1024 when it applies).  The fused kernel needs traffic off
+ * and a LiDAR pool that fits a wave's 10 KB LDS budget: asking for it
+ * otherwise fails with MEV_E_INVALID.  mev_get_step_kernel returns the kernel
+ * the next step will use (1 or 2).  Replaces nothing in the reference (its
+ * step is one sequential loop, cpp/IntersectionEnv.cpp:133-392). */
+int mev_set_step_kernel(mev_handle* h, int32_t kernel);
+int mev_get_step_kernel(const mev_handle* h, int32_t* kernel);
 
 #ifdef __cplusplus
 }

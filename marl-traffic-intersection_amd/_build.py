@@ -40,6 +40,7 @@ VARIANTS = {"": [], "stamps": ["-DMEV_STAMPS"]}
 EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOCARS"],
                "exp_none": ["-DMEV_EXP_NOROAD", "-DMEV_EXP_NOCARS"], "exp_iters": ["-DMEV_ITERS"],
                "stampsx": ["-DMEV_STAMPS", "-DMEV_STAMPS_X"], "stampsy": ["-DMEV_STAMPS", "-DMEV_STAMPS_Y"],
+               "stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                # exact variants: probes per road-march step (product: 2)
                "npr1": ["-DMEV_LIDAR_NPR=1"], "npr3": ["-DMEV_LIDAR_NPR=3"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it

@@ -33,7 +33,7 @@ EXPORTED = (
     "mev_device_outputs", "mev_npc_overflow", "mev_use_own_stream", "mev_debug_stamps",
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
     "mev_kernel_timing", "mev_kernel_times", "mev_set_reset_routes", "mev_snapshot_size", "mev_snapshot",
-    "mev_restore",
+    "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel",
 )
 
 
@@ -133,6 +133,8 @@ def load_library(variant: str = None):
     L.mev_restore.argtypes = [_vp, _vp, _vp, ctypes.c_uint32]
     L.mev_kernel_times.argtypes = [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_int64)]
+    L.mev_set_step_kernel.argtypes = [_vp, ctypes.c_int32]
+    L.mev_get_step_kernel.argtypes = [_vp, i32p]
     L.mev_configure.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.mev_configure_traffic.argtypes = [_vp, ctypes.c_int32, ctypes.c_float]
     L.mev_set_reward.argtypes = [_vp, f32p]
@@ -401,6 +403,16 @@ class Handle:
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
         _check(self._lib.mev_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
         return a.value, b.value, n.value
+
+    def set_step_kernel(self, kernel: int = 0):
+        """0: automatic, 1: k_cars + k_lidar, 2: the fused k_step (scheduling only; results identical)."""
+        _check(self._lib.mev_set_step_kernel(self._h, int(kernel)))
+
+    def step_kernel(self) -> int:
+        """The kernel path the next step uses: 1 (k_cars + k_lidar) or 2 (fused k_step)."""
+        v = ctypes.c_int32()
+        _check(self._lib.mev_get_step_kernel(self._h, ctypes.byref(v)))
+        return v.value
 
     def set_reset_routes(self, routes):
         """Draw every agent's route from `routes` at each reset (empty: fixed routes)."""

@@ -374,6 +374,8 @@ int mev_configure(mev_handle* h, int32_t use_team, int32_t respawn, int32_t max_
 int mev_configure_traffic(mev_handle* h, int32_t enabled, float density) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (enabled && h->cfg.max_npcs == 0) return fail(MEV_E_INVALID, "traffic needs max_npcs > 0 (set at creation)");
+    if (enabled && h->sp.step_kernel == 2)
+        return fail(MEV_E_INVALID, "the fused step kernel (mev_set_step_kernel 2) does not support traffic");
     h->cfg.traffic_flow = enabled;
     h->cfg.traffic_density = density < 0.0f ? 0.0f : density;  // configure_traffic clamps (:56-60)
     h->sp.traffic = enabled;
@@ -688,6 +690,25 @@ int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* 
     *steps = h->t_steps;
     h->t_cars_ms = h->t_lidar_ms = 0.0;
     h->t_steps = 0;
+    return MEV_OK;
+}
+
+int mev_set_step_kernel(mev_handle* h, int32_t kernel) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (kernel < 0 || kernel > 2) return fail(MEV_E_INVALID, "step kernel must be 0 (auto), 1 (two kernels) or 2 (fused)");
+    mev::SimParams q = h->sp;
+    q.step_kernel = kernel;
+    if (mev::step_kernel_for(q) == 0)
+        return fail(MEV_E_INVALID, "the fused step kernel does not support this configuration (traffic mode or too much LDS)");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->sp.step_kernel = kernel;
+    return MEV_OK;
+}
+
+int mev_get_step_kernel(const mev_handle* h, int32_t* kernel) {
+    if (!h || !kernel) return fail(MEV_E_INVALID, "null argument");
+    *kernel = mev::step_kernel_for(h->sp);
     return MEV_OK;
 }
 

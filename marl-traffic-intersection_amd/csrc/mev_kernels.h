@@ -82,6 +82,8 @@ struct SimParams {
     // route pool drawn per agent at every reset (n_reset_routes == 0: routes stay fixed)
     const int32_t* reset_routes;
     int32_t n_reset_routes;
+    // step kernel choice (host side): 0 auto, 1 k_cars + k_lidar, 2 fused k_step
+    int32_t step_kernel;
 };
 
 struct StepInputs {
@@ -92,7 +94,12 @@ struct StepInputs {
     uint64_t rng_counter;      // handle-wide step counter (Philox counter for NPC spawns)
 };
 
+// The kernels launch_step will use for p: 1 = k_cars + k_lidar, 2 = the fused
+// k_step (one wave per env); 0 when p.step_kernel == 2 but k_step cannot run p
+// (traffic mode, or a pool that does not fit a wave's LDS budget).
+int step_kernel_for(const SimParams& p);
 // ev (nullable): three events recorded before k_cars, between k_cars and k_lidar, after k_lidar
+// (with k_step: before it, and twice after it)
 hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
                        const hipEvent_t* ev = nullptr);
 hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s,

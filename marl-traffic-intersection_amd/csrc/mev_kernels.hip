@@ -29,9 +29,19 @@ constexpr int WAVE = 64;
 #define STAMP_RAW(k)                                                     \
     do {                                                                 \
         __builtin_amdgcn_wave_barrier();                                 \
-        if (threadIdx.x == 0) p.debug[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+        if (threadIdx.x == 0) p.debug[e * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-#if defined(MEV_STAMPS_X)
+#if defined(MEV_STAMPS_R)  // wall-clock (s_memrealtime, 100 MHz) timeline: entry, after the loads, end
+#undef STAMP_RAW
+#define STAMP_RAW(k)                                                     \
+    do {                                                                 \
+        __builtin_amdgcn_wave_barrier();                                 \
+        if (threadIdx.x == 0) p.debug[e * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define STAMP(k) do { if ((k) == 0) STAMP_RAW(1); if ((k) == 6) STAMP_RAW(2); } while (0)
+#define STAMPX(k) do {} while (0)
+#define STAMPY(k) do {} while (0)
+#elif defined(MEV_STAMPS_X)
 #define STAMP(k) do { if ((k) == 0 || (k) == 6) STAMP_RAW(k); } while (0)
 #define STAMPX(k) STAMP_RAW(k)
 #define STAMPY(k) do {} while (0)
@@ -582,7 +592,10 @@ struct CarsLDS {
 
 __host__ __device__ inline size_t lds_al(size_t b) { return (b + 15) & ~size_t(15); }
 
-size_t cars_lds_bytes(int N, int K) {
+// NPC slots that need obstacle entries in k_cars' LDS (none without traffic)
+__host__ __device__ inline int cars_k(const SimParams& p) { return p.traffic ? p.K : 0; }
+
+__host__ __device__ inline size_t cars_lds_bytes(int N, int K) {
     const size_t n = (size_t)N, ob = (size_t)(N + K);
     return 22 * lds_al(n * 4) + 2 * lds_al(n * 16) + 3 * lds_al(n * 4) + 4 * lds_al(n) + lds_al(n * 8) +
            lds_al(ob * 16) + 3 * lds_al(ob * 4) + lds_al(n * 16);
@@ -615,23 +628,22 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
     return L;
 }
 
-template <bool TRAFFIC>
-__global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outputs out) {
+// The per-env body of the step (k_cars, or the first half of k_step): el and
+// nl are this wave's LDS.  FUSED: the LiDAR runs in the same wave right after
+// (k_step) and reads the obstacle table and candidate masks from LDS, so they
+// are not published to HBM.
+template <bool TRAFFIC, bool FUSED>
+__device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
+                                          const CarsLDS& el, NpcLDS* nl) {
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
     // status, collisions, respawn, observation head); the LiDAR block of the
-    // observation is filled by k_lidar right after.  Per-agent phases run on
+    // observation is filled by the LiDAR body right after.  Per-agent phases run on
     // groups of 8 lanes per agent (8 agents per pass) so the window search,
     // the corner tests and the neighbour ranking are lane-parallel; global
     // memory is touched in two dependent rounds (state, then route table) and
     // written once at the end.
-    extern __shared__ __align__(16) unsigned char cars_lds[];
-    const int e = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x & (WAVE - 1);
     const int N = p.N;
-    CarsLDS el = carve_cars_lds(cars_lds, N, p.K);
-    __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
-    NpcLDS* nl = nullptr;
-    if constexpr (TRAFFIC) nl = &nl_storage;
 
     // ---- phase 0: ego state -> LDS (lane = agent).  An env whose previous
     // step ended starts from its spawns (vector auto-reset; reset +
@@ -926,7 +938,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         const int4 b4 = make_int4(bx.x0, bx.x1, bx.y0, bx.y1);
         el.box[o] = b4;
         el.px[o] = x; el.py[o] = y; el.ph[o] = h;
-        p.ob_box[e * OB + o] = b4;
+        if (!FUSED) p.ob_box[e * OB + o] = b4;
     }
     for (int i = tid; i < N; i += WAVE) { el.cand[2 * i] = 0ull; el.cand[2 * i + 1] = 0ull; }
     wave_lds_sync();
@@ -949,10 +961,12 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         }
     }
     wave_lds_sync();
-    for (int i = tid; i < N; i += WAVE) {
-        const int g = e * N + i;
-        p.ob_cand[2 * g] = el.cand[2 * i];
-        p.ob_cand[2 * g + 1] = el.cand[2 * i + 1];
+    if (!FUSED) {
+        for (int i = tid; i < N; i += WAVE) {
+            const int g = e * N + i;
+            p.ob_cand[2 * g] = el.cand[2 * i];
+            p.ob_cand[2 * g + 1] = el.cand[2 * i + 1];
+        }
     }
 
     STAMP(5);
@@ -1038,6 +1052,20 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
         }
     }
     STAMP(6);
+}
+
+template <bool TRAFFIC>
+__global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outputs out, int e_begin) {
+    extern __shared__ __align__(16) unsigned char cars_lds[];
+    const int e = e_begin + (int)blockIdx.x;
+#if defined(MEV_STAMPS_R)
+    STAMP_RAW(0);
+#endif
+    const CarsLDS el = carve_cars_lds(cars_lds, p.N, cars_k(p));
+    __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
+    NpcLDS* nl = nullptr;
+    if constexpr (TRAFFIC) nl = &nl_storage;
+    cars_body<TRAFFIC, false>(p, in, out, e, el, nl);
 }
 
 // ------------------------------------------------------------- LiDAR ---
@@ -1179,37 +1207,63 @@ int lidar_group(int R) {
     return g < 1 ? 1 : (g > 64 ? 64 : g);
 }
 
-template <bool TAB>
-__global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int G) {
-    // Each wave owns a group of G agents (G*R <= max(256, R) beams).  Phase 1
-    // computes the beam directions in lockstep; phase 2 marches the road with
-    // the group's beams fed to the 64 lanes from a queue, so a lane that
-    // finishes a short beam takes the next one instead of idling until the
-    // longest beam of its agent is done (lockstep cost = max over the agent's
-    // beams, pooled cost ~ their mean); phase 3 resolves the cars per agent
-    // (lane = beam, candidate boxes wave-uniform) and writes the observation.
-    extern __shared__ __align__(16) unsigned char lds_raw[];
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int wv = threadIdx.x / WAVE;
+// Where the LiDAR body reads each agent's pose and the obstacle table from:
+// HBM as k_cars published it (k_lidar), or the LDS of the same wave's
+// cars_body (k_step).
+struct LidarSrcHbm {
+    const SimParams& p;
+    __device__ bool alive(int g) const { return p.ego.alive[g] != 0; }
+    __device__ float4 pose(int g) const { return make_float4(p.ego.x[g], p.ego.y[g], p.ego.h[g], __int_as_float(g)); }
+    __device__ void cand(int g, unsigned long long& c0, unsigned long long& c1) const {
+        c0 = p.ob_cand[2 * g];
+        c1 = p.ob_cand[2 * g + 1];
+    }
+    __device__ int4 box(int g, int o) const { return p.ob_box[(size_t)(g / p.N) * p.ob_stride + o]; }
+};
+struct LidarSrcLds {
+    const CarsLDS& el;
+    int g0;  // global index of the env's agent 0
+    __device__ bool alive(int g) const { return el.alive[g - g0] != 0; }
+    __device__ float4 pose(int g) const {
+        const int i = g - g0;
+        return make_float4(el.x[i], el.y[i], el.h[i], __int_as_float(g));
+    }
+    __device__ void cand(int g, unsigned long long& c0, unsigned long long& c1) const {
+        c0 = el.cand[2 * (g - g0)];
+        c1 = el.cand[2 * (g - g0) + 1];
+    }
+    __device__ int4 box(int, int o) const { return el.box[o]; }
+};
+
+// Lidar::update (Lidar.cpp:16-90) + Lidar::normalized for the agents
+// [a0, a0 + na) (na <= G) of one wave; base/lay: the wave's LDS.  Phase 1
+// computes the beam directions in lockstep; phase 2 marches the road with
+// the group's beams fed to the 64 lanes from a queue, so a lane that
+// finishes a short beam takes the next one instead of idling until the
+// longest beam of its agent is done (lockstep cost = max over the agent's
+// beams, pooled cost ~ their mean); phase 3 resolves the cars as packed
+// (agent, box, beam) pairs and writes the observation's LiDAR block.
+template <bool TAB, class Src>
+__device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& out, const Src& src, const int G,
+                                           const int a0, const int na, const int lane, unsigned char* base,
+                                           const LidarLayout& lay) {
     const int R = p.R;
-    const int EN = p.E * p.N;
-    const int a0 = __builtin_amdgcn_readfirstlane((blockIdx.x * (blockDim.x / WAVE) + wv) * G);
-    if (a0 >= EN) return;  // wave-uniform exit: the kernel has no block-level barrier
-    const int na = EN - a0 < G ? EN - a0 : G;
-    const LidarLayout lay = lidar_layout(G, R, lidar_cand_max(p));
-    unsigned char* base = lds_raw + (size_t)wv * (size_t)lay.bytes;
     float4* ag = reinterpret_cast<float4*>(base + lay.ag);
     float2* dir = reinterpret_cast<float2*>(base + lay.dir);
     int* res = reinterpret_cast<int*>(base + lay.res);
+#if defined(MEV_STAMPS_R)  // slots 3/4: entry of the env's first/second pool; 5/6: their car-phase end
+    const int se_ = a0 / p.N, sp_ = ((a0 % p.N) / G) & 1;
+    if (lane == 0) p.debug[se_ * 8 + 3 + sp_] = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // ---- phase 1: alive agents of the group (compacted), beam directions
     bool alv = false;
-    if (lane < na) alv = p.ego.alive[a0 + lane] != 0;
+    if (lane < na) alv = src.alive(a0 + lane);
     const unsigned long long am = ballot(alv);
     const int nal = __popcll(am);
     if (alv) {
         const int g = a0 + lane;
-        ag[lane_rank(am)] = make_float4(p.ego.x[g], p.ego.y[g], p.ego.h[g], __int_as_float(g));
+        ag[lane_rank(am)] = src.pose(g);
     }
     if (__popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
         for (int j = 0; j < na; ++j) {
@@ -1268,6 +1322,10 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     // Beams still running go to the queue of the pooled march.
     unsigned short* queue = reinterpret_cast<unsigned short*>(base + lay.queue);
     int qn = 0;
+    // beam offsets rel[b] of the first two chunks of 64 beams, loaded once:
+    // a global load inside the loop would expose its latency every iteration
+    const float rel_c0 = lane < R ? p.rel_angles[lane] : 0.0f;
+    const float rel_c1 = lane + WAVE < R ? p.rel_angles[lane + WAVE] : 0.0f;
     for (int j = 0; j < nal; ++j) {
         const float4 a = ag[j];
         const int px = (int)a.x, py = (int)a.y;
@@ -1277,7 +1335,8 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
             bool pend = false;
             if (b < R) {
                 float sn, cs;
-                sincosf(a.z + p.rel_angles[b], &sn, &cs);  // Lidar.cpp:24-26
+                const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : p.rel_angles[b]);
+                sincosf(a.z + rel_b, &sn, &cs);  // Lidar.cpp:24-26
                 const float dx = cs, dy = -sn;
                 dir[j * R + b] = make_float2(dx, dy);
                 int k1 = 0;
@@ -1302,6 +1361,9 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
         }
     }
     wave_lds_sync();
+#if defined(MEV_STAMPS_R)  // one pool per env: slot 4 = end of phase 1
+    if (lane == 0 && na == p.N) p.debug[se_ * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // ---- phase 2: pooled road + screen march of the queued beams
     // (Lidar.cpp:31-48, first stop wins): LIDAR_NPR exact probes, then a jump
@@ -1355,6 +1417,9 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     if (lane == 0 && a0 / G < p.E * 8) p.debug[a0 / G] = (unsigned long long)iters;
 #endif
     wave_lds_sync();
+#if defined(MEV_STAMPS_R)  // one pool per env: slot 6 = end of phase 2
+    if (lane == 0 && na == p.N) p.debug[se_ * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // ---- phase 3: cars (Lidar.cpp:50-80) as a list of (agent, box, beam) pairs.
     // A box can only stop the beams whose ray enters its slab box, i.e. the
@@ -1367,14 +1432,14 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     int* seg_jo = reinterpret_cast<int*>(base + lay.seg_jo);
     int4* seg_rg = reinterpret_cast<int4*>(base + lay.seg_rg);
     int4* seg_bx = reinterpret_cast<int4*>(base + lay.seg_bx);
-    const int OB = p.ob_stride;
     int M = 0;
     for (int j = 0; j < nal; ++j) {  // 3a
         const int g = __builtin_amdgcn_readfirstlane(__float_as_int(ag[j].w));
 #ifdef MEV_EXP_NOCARS
         const unsigned long long c0 = 0, c1 = 0;
 #else
-        const unsigned long long c0 = p.ob_cand[2 * g], c1 = p.ob_cand[2 * g + 1];
+        unsigned long long c0, c1;
+        src.cand(g, c0, c1);
 #endif
         const int n0 = __popcll(c0);
         if ((c0 >> lane) & 1ull) seg_jo[M + lane_rank(c0)] = (j << 8) | lane;
@@ -1393,8 +1458,7 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     for (int m = lane; m < M; m += WAVE) {
         const int jo = seg_jo[m];
         const float4 a = ag[jo >> 8];
-        const int e = __float_as_int(a.w) / p.N;
-        const int4 bx = p.ob_box[(size_t)e * OB + (jo & 255)];
+        const int4 bx = src.box(__float_as_int(a.w), jo & 255);
         seg_bx[m] = bx;
         const float ex0 = box_lo(bx.x), ex1 = box_hi(bx.y);
         const float ey0 = box_lo(bx.z), ey1 = box_hi(bx.w);
@@ -1502,6 +1566,9 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
         }
     }
     wave_lds_sync();
+#if defined(MEV_STAMPS_R)
+    if (lane == 0) p.debug[se_ * 8 + 5 + sp_] = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int j = 0; j < nal; ++j) {  // 3d: Lidar::normalized (:92-98)
         const int g = __float_as_int(ag[j].w);
         float* row = out.obs + (size_t)g * p.D + OBS_HEAD;
@@ -1510,6 +1577,47 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
             const float final_dist = (r & 1) ? march_dist(p, r >> 1) : p.lidar_max;
             row[b] = final_dist * p.lidar_inv;
         }
+    }
+}
+
+template <bool TAB>
+__global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int G, int a_begin, int a_end) {
+    // Each wave owns a group of G agents (G*R <= max(256, R) beams).
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int wv = threadIdx.x / WAVE;
+    const int a0 = __builtin_amdgcn_readfirstlane(a_begin + (int)(blockIdx.x * (blockDim.x / WAVE) + wv) * G);
+    if (a0 >= a_end) return;  // wave-uniform exit: the kernel has no block-level barrier
+    const int na = a_end - a0 < G ? a_end - a0 : G;
+    const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p));
+    lidar_body<TAB>(p, out, LidarSrcHbm{p}, G, a0, na, lane, lds_raw + (size_t)wv * (size_t)lay.bytes, lay);
+}
+
+// The whole step in one wave per env: cars_body, then the LiDAR of the env's
+// N agents in pools of G from the same wave's LDS (no HBM hand-off, no second
+// launch; a wave whose env finishes its car logic early starts its LiDAR
+// while other waves on the SIMD are still in theirs).
+template <bool TRAFFIC, bool TAB>
+__global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Outputs out, int G) {
+    extern __shared__ __align__(16) unsigned char step_lds[];
+    const int e = blockIdx.x;
+#if defined(MEV_STAMPS_R)
+    STAMP_RAW(0);
+#endif
+    const CarsLDS el = carve_cars_lds(step_lds, p.N, cars_k(p));
+    __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
+    NpcLDS* nl = nullptr;
+    if constexpr (TRAFFIC) nl = &nl_storage;
+    cars_body<TRAFFIC, true>(p, in, out, e, el, nl);
+    wave_lds_sync();
+    const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p));
+    unsigned char* lbase = step_lds + lds_al(cars_lds_bytes(p.N, cars_k(p)));
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int g0 = e * p.N;
+    for (int j0 = 0; j0 < p.N; j0 += G) {
+        const int na = p.N - j0 < G ? p.N - j0 : G;
+        lidar_body<TAB>(p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
+        wave_lds_sync();
     }
 }
 
@@ -1573,18 +1681,21 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
     }
 }
 
-hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
-                       const hipEvent_t* ev) {
+static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Outputs& out, int e0, int e1,
+                              hipStream_t s, const hipEvent_t* ev) {
+    // k_cars then k_lidar over the envs [e0, e1)
+    if (e1 <= e0) return hipSuccess;
     if (ev) (void)hipEventRecord(ev[0], s);
-    const unsigned cars_lds = (unsigned)cars_lds_bytes(p.N, p.K);
-    if (p.traffic) hipLaunchKernelGGL(k_cars<true>, dim3(p.E), dim3(WAVE), cars_lds, s, p, in, out);
-    else hipLaunchKernelGGL(k_cars<false>, dim3(p.E), dim3(WAVE), cars_lds, s, p, in, out);
+    const unsigned cars_lds = (unsigned)cars_lds_bytes(p.N, cars_k(p));
+    if (p.traffic) hipLaunchKernelGGL(k_cars<true>, dim3(e1 - e0), dim3(WAVE), cars_lds, s, p, in, out, e0);
+    else hipLaunchKernelGGL(k_cars<false>, dim3(e1 - e0), dim3(WAVE), cars_lds, s, p, in, out, e0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], s);
+    const int a_begin = e0 * p.N, a_end = e1 * p.N, na = a_end - a_begin;
     int G = lidar_group(p.R);
     // small batches: trade pool size for waves (~4 per SIMD on 256 CUs) so latency is hidden
-    while (G > 1 && (p.E * p.N) / G < 4096) G = (G + 1) / 2;
+    while (G > 1 && na / G < 4096) G = (G + 1) / 2;
     static const int g_env = [] { const char* v = getenv("MEV_LIDAR_G"); return v ? atoi(v) : 0; }();
     if (g_env > 0 && g_env <= 64 && (size_t)g_env * p.R <= 1024) G = g_env;  // experiments (tools/kernel_time.py)
     // LDS: shrink the group, then the waves per block, to stay within 40 KB (64 KB hard) per block
@@ -1592,15 +1703,58 @@ hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& 
     while (G > 1 && wpb * lidar_layout(G, p.R, lidar_cand_max(p)).bytes > 40 * 1024) G = (G + 1) / 2;
     const int wave_lds = lidar_layout(G, p.R, lidar_cand_max(p)).bytes;
     while (wpb > 1 && wpb * wave_lds > 64 * 1024) wpb /= 2;
-    const int groups = (p.E * p.N + G - 1) / G;
+    const int groups = (na + G - 1) / G;
     const unsigned blocks = (unsigned)((groups + wpb - 1) / wpb);
     if (p.dist_tab)
-        hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(wpb * WAVE), wpb * wave_lds, s, p, out, G);
+        hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(wpb * WAVE), wpb * wave_lds, s, p, out, G, a_begin, a_end);
     else
-        hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(wpb * WAVE), wpb * wave_lds, s, p, out, G);
+        hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(wpb * WAVE), wpb * wave_lds, s, p, out, G, a_begin, a_end);
     e = hipGetLastError();
     if (ev && e == hipSuccess) (void)hipEventRecord(ev[2], s);
     return e;
+}
+
+// LDS of one k_step wave (cars + LiDAR pool of G agents), or 0 when the fused
+// kernel does not apply.  At 4 waves per SIMD (128 VGPRs) a CU holds 16 waves,
+// so a wave may take 160 KB / 16 = 10 KB.
+static int fused_lds_bytes(const SimParams& p, int G) {
+    return (int)lds_al(cars_lds_bytes(p.N, cars_k(p))) + lidar_layout(G, p.R, lidar_cand_max(p)).bytes;
+}
+
+static int fused_group(const SimParams& p) {
+    if (p.traffic) return 0;  // the NPC phase's LDS leaves no room for a LiDAR pool
+    static const int g_env = [] { const char* v = getenv("MEV_FUSED_G"); return v ? atoi(v) : 0; }();
+    if (g_env > 0) return fused_lds_bytes(p, g_env) <= 10 * 1024 ? g_env : 0;  // experiments
+    // the largest pool of <= 512 beams that fits (one pool of the env's 8 agents at R = 64)
+    for (int G = p.N; G >= 1; --G)
+        if (G * p.R <= 512 && fused_lds_bytes(p, G) <= 10 * 1024) return G;
+    return 0;
+}
+
+int step_kernel_for(const SimParams& p) {
+    const bool fusable = fused_group(p) > 0;
+    if (p.step_kernel == 1) return 1;
+    if (p.step_kernel == 2) return fusable ? 2 : 0;
+    // auto: fused once the batch fills the chip with one wave per env (>= 4 per CU);
+    // smaller batches keep the LiDAR's finer per-group waves
+    return (fusable && p.E >= 1024) ? 2 : 1;
+}
+
+hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
+                       const hipEvent_t* ev) {
+    const int kind = step_kernel_for(p);
+    if (kind == 0) return hipErrorInvalidValue;
+    if (kind == 2) {
+        const int G = fused_group(p);
+        if (ev) (void)hipEventRecord(ev[0], s);
+        const unsigned lds = (unsigned)fused_lds_bytes(p, G);
+        if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true>), dim3(p.E), dim3(WAVE), lds, s, p, in, out, G);
+        else hipLaunchKernelGGL((k_step<false, false>), dim3(p.E), dim3(WAVE), lds, s, p, in, out, G);
+        hipError_t e = hipGetLastError();
+        if (ev && e == hipSuccess) { (void)hipEventRecord(ev[1], s); (void)hipEventRecord(ev[2], s); }
+        return e;
+    }
+    return launch_part(p, in, out, 0, p.E, s, ev);
 }
 
 hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s,

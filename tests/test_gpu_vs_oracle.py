@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import golden_replay as G
+from conftest import STEP_KERNELS, use_step_kernel
 import oracle_replay as R
 
 pytestmark = pytest.mark.gpu
@@ -124,8 +125,9 @@ def _oracle_from_state(cfg, st, e, troutes):
     return o
 
 
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
 @pytest.mark.parametrize("cfg", CONFIGS, ids=[c["name"] for c in CONFIGS])
-def test_random_states_match_oracle(mev, cfg):
+def test_random_states_match_oracle(mev, cfg, kernel):
     rng = np.random.default_rng(zlib.crc32(cfg["name"].encode()))
     E, T = 24, 50
     n, lanes = cfg["n"], cfg.get("lanes", 3)
@@ -136,6 +138,7 @@ def test_random_states_match_oracle(mev, cfg):
                    use_team_reward=int(cfg.get("use_team", False)), respawn_enabled=int(cfg.get("respawn", True)),
                    max_steps=cfg.get("max_steps", 2000), max_npcs=64,
                    reward=cfg.get("reward", [10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2]))
+    use_step_kernel(mev, h, kernel)
     table = ROUTES2 if lanes == 2 else ROUTES3
     st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table)
     h.set_traffic_routes(troutes)

@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 import golden_replay as G
+from conftest import STEP_KERNELS, use_step_kernel
 import oracle_replay as ORP
 
 CAR_DTYPE, OracleEnv = ORP.O.CAR_DTYPE, ORP.O.OracleEnv
@@ -87,14 +88,16 @@ def _oracle_obs(case, st, e, D):
     return r["obs"]
 
 
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
-def test_lidar_matches_oracle_on_dense_clusters(mev, case):
+def test_lidar_matches_oracle_on_dense_clusters(mev, case, kernel):
     rng = np.random.default_rng(zlib.crc32(case["name"].encode()))
     n, R_ = case["n"], case["rays"]
     D = 31 + R_
     E = 256 if R_ < 1024 else 64
     h = mev.Handle(num_envs=E, num_agents=n, num_lanes=case.get("lanes", 3), lidar_rays=R_, obs_dim=D,
                    lidar_fov_deg=case["fov"], lidar_max_dist=case["maxd"], lidar_step=case["step"], respawn_enabled=0)
+    use_step_kernel(mev, h, kernel)
     stops = 0
     for rnd in range(5):
         st = _cluster_state(rng, h, n)

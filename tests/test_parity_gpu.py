@@ -6,28 +6,39 @@ bit-exact requirement on crash/success flags."""
 import pytest
 
 import golden_replay as G
+from conftest import STEP_KERNELS
 
 pytestmark = pytest.mark.gpu
 
 SINGLE = [n for n in G.scenario_names() if not n.startswith("inject_egos")]
 
 
+def _replay(mev, names, kernel):
+    reps = G.replay(mev, names, kernel=kernel)
+    if reps is None:
+        pytest.skip(f"step kernel {kernel} does not apply to this configuration")
+    return reps
+
+
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
 @pytest.mark.parametrize("name", SINGLE)
-def test_golden_scenario(mev, name):
-    (rep,) = G.replay(mev, name)
+def test_golden_scenario(mev, name, kernel):
+    (rep,) = _replay(mev, name, kernel)
     assert rep.ok, f"{name}: {rep.mismatches[:5]} (steps checked {rep.steps})"
 
 
-def test_injected_states_batched(mev):
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
+def test_injected_states_batched(mev, kernel):
     # six different injected scenarios as six envs of ONE handle
-    reps = G.replay(mev, G.scenario_names("inject_egos"))
+    reps = _replay(mev, G.scenario_names("inject_egos"), kernel)
     bad = [(r.name, r.mismatches[:3]) for r in reps if not r.ok]
     assert not bad, bad
 
 
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
 @pytest.mark.parametrize("name", ["cfg3_team_policy", "traffic_d20"])
-def test_same_scenario_replicated_envs(mev, name):
+def test_same_scenario_replicated_envs(mev, name, kernel):
     # the same scenario in 37 envs of one handle: every env must match the reference
-    reps = G.replay(mev, [name] * 37)
+    reps = _replay(mev, [name] * 37, kernel)
     bad = [i for i, r in enumerate(reps) if not r.ok]
     assert not bad, reps[bad[0]].mismatches[:5]

@@ -45,6 +45,54 @@ def test_determinism_full_size(mev):
         assert np.array_equal(outs[0][1][k], outs[1][1][k]), k
 
 
+def test_fused_and_two_kernel_paths_agree_full_size(mev):
+    """The fused k_step (default at this size) and k_cars + k_lidar produce
+    identical outputs and state, step after step, with auto-reset on."""
+    st = _warm_state(mev, seed=6)
+    rng = np.random.default_rng(7)
+    acts = rng.uniform(-1, 1, (16, E, N, 2)).astype(np.float32)
+    hs = []
+    for kernel in (1, 2):
+        h = _handle(mev, max_steps=70)  # some envs truncate and auto-reset inside the window
+        h.set_step_kernel(kernel)
+        assert h.step_kernel() == kernel
+        h.set_state(st)
+        hs.append(h)
+    for a in acts:
+        o1 = hs[0].step(a, auto_reset=True)
+        o2 = hs[1].step(a, auto_reset=True)
+        for k in o1:
+            assert np.array_equal(o1[k], o2[k]), k
+    s1, s2 = hs[0].get_state(), hs[1].get_state()
+    for k in s1:
+        assert np.array_equal(s1[k], s2[k]), k
+    for h in hs:
+        h.close()
+
+
+def test_step_kernel_selection(mev):
+    h = _handle(mev)
+    assert h.step_kernel() == 2  # automatic: fused at 4096 envs
+    h.set_step_kernel(1)
+    assert h.step_kernel() == 1
+    with pytest.raises(mev.MevError):
+        h.set_step_kernel(3)
+    h.set_step_kernel(2)
+    with pytest.raises(mev.MevError):  # the fused kernel has no NPC phase
+        h.configure_traffic(1, 0.5)
+    h.set_step_kernel(0)
+    h.configure_traffic(1, 0.5)
+    assert h.step_kernel() == 1
+    with pytest.raises(mev.MevError):
+        h.set_step_kernel(2)
+    h.close()
+    small = _handle(mev, num_envs=64)
+    assert small.step_kernel() == 1  # automatic: finer LiDAR waves for small batches
+    small.set_step_kernel(2)
+    assert small.step_kernel() == 2
+    small.close()
+
+
 def test_env_permutation_equivariance(mev):
     st = _warm_state(mev, seed=2)
     rng = np.random.default_rng(3)

@@ -34,7 +34,7 @@ def _read(d, counter):
                 name = row["Kernel_Name"]
                 if "mev::" not in name:
                     continue            # the library's kernels only (not torch's input generation)
-                for short in ("k_lidar", "k_cars", "k_reset", "k_restore"):
+                for short in ("k_step", "k_lidar", "k_cars", "k_reset", "k_restore"):
                     if short in name:
                         name = short + name[name.find(short) + len(short):].split("(")[0]
                         break
