@@ -43,6 +43,11 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                # exact variants: probes per road-march step (product: 2)
                "npr1": ["-DMEV_LIDAR_NPR=1"], "npr3": ["-DMEV_LIDAR_NPR=3"],
+               # exact variants: k_step issue priorities of the car part / LiDAR part (product: 1 / 0)
+               "prio00": ["-DMEV_PRIO_CARS=0", "-DMEV_PRIO_LIDAR=0"], "prio01": ["-DMEV_PRIO_CARS=0", "-DMEV_PRIO_LIDAR=1"],
+               "prio20": ["-DMEV_PRIO_CARS=2", "-DMEV_PRIO_LIDAR=0"],
+               # exact variant: k_step stages every output in LDS and writes whole rows at the end
+               "staged": ["-DMEV_FUSED_STAGED=1"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
                "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 VARIANTS.update(EXPERIMENTS)

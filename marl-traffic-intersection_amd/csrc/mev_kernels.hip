@@ -133,8 +133,12 @@ __device__ inline int reset_route(const SimParams& p, uint64_t ctr, int e, int i
 // dist of march probe k: the reference accumulates `dist += step_size` in
 // float (Lidar.cpp:33); when that sum equals k*step exactly (checked on the
 // host, e.g. step 4) we multiply, otherwise read the host-accumulated table.
+// TAB: the handle's probe distances are not exactly k*step (they accumulate
+// dist += step like Lidar.cpp:33), read them from the table
+template <bool TAB>
 __device__ inline float march_dist(const SimParams& p, int k) {
-    return p.dist_tab ? p.dist_tab[k] : (float)k * p.lidar_step;
+    if constexpr (TAB) return p.dist_tab[k];
+    else return (float)k * p.lidar_step;
 }
 
 // Car::update_path_index (cpp/Car.cpp:47-74): argmin of squared distance over
@@ -510,7 +514,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
 // NPCs; stable by distance == libstdc++ insertion sort for <= 16 candidates).
 template <bool TRAFFIC, class EL>
 __device__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const NpcLDS* nl, int ncnt, float tx,
-                                  float ty, float* row) {
+                                  float ty, float* row, bool pad = true) {
     const float x = el.x[i], y = el.y[i], v = el.v[i], h = el.h[i];
     row[0] = x / float(WIDTH);
     row[1] = y / float(HEIGHT);
@@ -565,7 +569,8 @@ __device__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const
             o[0] = o[1] = o[2] = o[3] = o[4] = 0.0f;
         }
     }
-    for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
+    if (pad)
+        for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
 }
 
 template <bool TRAFFIC, class EL>
@@ -588,6 +593,13 @@ struct CarsLDS {
     int4* box;  // obstacle AABBs, integer pixels
     float *px, *py, *ph;
     unsigned long long* cand;  // [N][2]: boxes each agent's beams can reach
+    // k_step only (null in k_cars): the staged observation heads [N][31], the
+    // LiDAR beam offsets [R] and the env's flags (terminated, truncated,
+    // agents_alive, step, pending reset, reset this step), all written to HBM
+    // at the end of the kernel
+    float* head;
+    float* rel;
+    int32_t* envw;
 };
 
 __host__ __device__ inline size_t lds_al(size_t b) { return (b + 15) & ~size_t(15); }
@@ -625,8 +637,18 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
     L.py = reinterpret_cast<float*>(take(ob * 4));
     L.ph = reinterpret_cast<float*>(take(ob * 4));
     L.cand = reinterpret_cast<unsigned long long*>(take(n * 16));
+    L.head = nullptr;
+    L.rel = nullptr;
+    L.envw = nullptr;
     return L;
 }
+
+// k_step's output strategy: 0 = each part stores its outputs as it produces
+// them (the car part its rows' heads, the LiDAR part its blocks); 1 = staged in
+// LDS and written once at the end as whole coalesced rows (fused_store)
+#ifndef MEV_FUSED_STAGED
+#define MEV_FUSED_STAGED 0
+#endif
 
 // The per-env body of the step (k_cars, or the first half of k_step): el and
 // nl are this wave's LDS.  FUSED: the LiDAR runs in the same wave right after
@@ -644,35 +666,55 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
     // written once at the end.
     const int tid = threadIdx.x & (WAVE - 1);
     const int N = p.N;
+    // STAGE: every output and the state are written at the end of k_step (fused_store)
+    constexpr bool STAGE = FUSED && MEV_FUSED_STAGED;
 
     // ---- phase 0: ego state -> LDS (lane = agent).  An env whose previous
     // step ended starts from its spawns (vector auto-reset; reset +
     // add_car_with_route, :66-131).
-    const bool do_reset = in.auto_reset && p.pending_reset[e];
-    const int prev_step = do_reset ? 0 : p.step_count[e];
-    const int prev_npcs = TRAFFIC ? (do_reset ? 0 : p.npc.count[e]) : 0;
+    // Every load is issued up front (one round trip); only an env being reset
+    // waits a second round for its spawn poses.
+    const bool pending = p.pending_reset[e] != 0;
+    const int step_prev = p.step_count[e];
+    const int npcs_prev = TRAFFIC ? p.npc.count[e] : 0;
+    const bool do_reset = in.auto_reset && pending;
+    const int prev_step = do_reset ? 0 : step_prev;
+    const int prev_npcs = TRAFFIC ? (do_reset ? 0 : npcs_prev) : 0;
+    if constexpr (FUSED) {
+        for (int b = tid; b < p.R; b += WAVE) el.rel[b] = p.rel_angles[b];
+    }
     for (int i = tid; i < N; i += WAVE) {
         const int g = e * N + i;
-        const int rid = do_reset ? reset_route(p, in.rng_counter, e, i, p.ego.route[g]) : p.ego.route[g];
-        el.route[i] = rid;
-        el.a0[i] = in.actions[2 * g];
-        el.a1[i] = in.actions[2 * g + 1];
+        const int route_l = p.ego.route[g];
+        const float a0 = in.actions[2 * g], a1 = in.actions[2 * g + 1];
+        const float x = p.ego.x[g], y = p.ego.y[g], v = p.ego.v[g], h = p.ego.h[g];
+        const float acc = p.ego.acc[g], steer = p.ego.steer[g], pd = p.ego.prev_dist[g];
+        const float pa0 = p.ego.pa0[g], pa1 = p.ego.pa1[g];
+        const float sx = p.ego.sx[g], sy = p.ego.sy[g], sv = p.ego.sv[g], sh = p.ego.sh[g];
+        const int pidx = p.ego.pidx[g], intent = p.ego.intent[g];
+        const uint8_t alive = p.ego.alive[g];
+        el.a0[i] = a0;
+        el.a1[i] = a1;
         if (do_reset) {
-            const float sx = p.rt.spawn[3 * rid], sy = p.rt.spawn[3 * rid + 1], sh = p.rt.spawn[3 * rid + 2];
-            el.x[i] = sx; el.y[i] = sy; el.v[i] = 0.0f; el.h[i] = sh;
+            const int rid = reset_route(p, in.rng_counter, e, i, route_l);
+            const float rx = p.rt.spawn[3 * rid], ry = p.rt.spawn[3 * rid + 1], rh = p.rt.spawn[3 * rid + 2];
+            el.route[i] = rid;
+            el.x[i] = rx; el.y[i] = ry; el.v[i] = 0.0f; el.h[i] = rh;
             el.acc[i] = 0.0f; el.steer[i] = 0.0f; el.prev_dist[i] = 0.0f; el.pa0[i] = 0.0f; el.pa1[i] = 0.0f;
-            el.sx[i] = sx; el.sy[i] = sy; el.sv[i] = 0.0f; el.sh[i] = sh;
+            el.sx[i] = rx; el.sy[i] = ry; el.sv[i] = 0.0f; el.sh[i] = rh;
             el.pidx[i] = 0; el.intent[i] = p.rt.intent[rid]; el.alive[i] = 1;
         } else {
-            el.x[i] = p.ego.x[g]; el.y[i] = p.ego.y[g]; el.v[i] = p.ego.v[g]; el.h[i] = p.ego.h[g];
-            el.acc[i] = p.ego.acc[g]; el.steer[i] = p.ego.steer[g]; el.prev_dist[i] = p.ego.prev_dist[g];
-            el.pa0[i] = p.ego.pa0[g]; el.pa1[i] = p.ego.pa1[g];
-            el.sx[i] = p.ego.sx[g]; el.sy[i] = p.ego.sy[g]; el.sv[i] = p.ego.sv[g]; el.sh[i] = p.ego.sh[g];
-            el.pidx[i] = p.ego.pidx[g]; el.intent[i] = p.ego.intent[g]; el.alive[i] = p.ego.alive[g];
+            el.route[i] = route_l;
+            el.x[i] = x; el.y[i] = y; el.v[i] = v; el.h[i] = h;
+            el.acc[i] = acc; el.steer[i] = steer; el.prev_dist[i] = pd;
+            el.pa0[i] = pa0; el.pa1[i] = pa1;
+            el.sx[i] = sx; el.sy[i] = sy; el.sv[i] = sv; el.sh[i] = sh;
+            el.pidx[i] = pidx; el.intent[i] = intent; el.alive[i] = alive;
         }
     }
     const int step_no = prev_step + 1;  // res.step = ++step_count (:137)
-    if (tid == 0) p.step_count[e] = step_no;
+    // p.step_count[e] = step_no is stored with the other env flags (a store this
+    // early would be drained by the vmcnt waits of every later load)
     wave_lds_sync();
 
     STAMP(0);
@@ -888,11 +930,21 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
         const bool truncated = p.max_steps > 0 && step_no >= p.max_steps;
         if (in_env) { el.done[i] = done_i; el.status[i] = st_i; el.rew[i] = rew_i; }
         if (tid == 0) {
-            out.term[e] = terminated;
-            out.trunc[e] = truncated;
-            out.alive_cnt[e] = alive_cnt;
-            out.step[e] = step_no;
-            p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
+            if constexpr (STAGE) {
+                el.envw[0] = terminated;
+                el.envw[1] = truncated;
+                el.envw[2] = alive_cnt;
+                el.envw[3] = step_no;
+                el.envw[4] = (terminated || truncated) ? 1 : 0;
+                el.envw[5] = do_reset;
+            } else {
+                p.step_count[e] = step_no;
+                out.term[e] = terminated;
+                out.trunc[e] = truncated;
+                out.alive_cnt[e] = alive_cnt;
+                out.step[e] = step_no;
+                p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
+            }
         }
     }
     wave_lds_sync();
@@ -901,9 +953,11 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
     // final ego state back (lane = agent)
     for (int i = tid; i < N; i += WAVE) {
         const int g = e * N + i;
-        out.rew[g] = el.rew[i];
-        out.done[g] = el.done[i];
-        out.status[g] = el.status[i];
+        if (!STAGE) {
+            out.rew[g] = el.rew[i];
+            out.done[g] = el.done[i];
+            out.status[g] = el.status[i];
+        }
         const uint8_t st = el.status[i];
         if (p.respawn && el.alive[i] && el.done[i] && (st == ST_CRASH_CAR || st == ST_CRASH_WALL || st == ST_CRASH_LINE)) {
             const float sh = el.sh[i];
@@ -914,6 +968,7 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
             el.acc[i] = 0.0f; el.steer[i] = 0.0f;
             el.tgx[i] = el.t10x[i]; el.tgy[i] = el.t10y[i];  // path[min(0 + 10, 159)]
         }
+        if (STAGE) continue;  // k_step writes the state back at its end (fused_store)
         p.ego.x[g] = el.x[i]; p.ego.y[g] = el.y[i]; p.ego.v[g] = el.v[i]; p.ego.h[g] = el.h[i];
         p.ego.acc[g] = el.acc[i]; p.ego.steer[g] = el.steer[i]; p.ego.pidx[g] = el.pidx[i];
         p.ego.prev_dist[g] = el.prev_dist[i]; p.ego.pa0[g] = el.pa0[i]; p.ego.pa1[g] = el.pa1[i];
@@ -1009,7 +1064,8 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
             const int nb = __builtin_popcountll(ballot(valid) & gmask);
             STAMPY(5);
             if (act) {
-                float* row = out.obs + (size_t)(e * N + i) * p.D;
+                // k_step stages the head in LDS (written with the LiDAR block by fused_store)
+                float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)(e * N + i) * p.D;
                 if (!alv) {
                     for (int cc = sub; cc < OBS_HEAD; cc += 8) row[cc] = 0.0f;
                 } else {
@@ -1036,19 +1092,21 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
                         o[0] = o[1] = o[2] = o[3] = o[4] = 0.0f;
                     }
                 }
-                for (int cc = OBS_HEAD + p.lidar_slots + sub; cc < p.D; cc += 8) row[cc] = 0.0f;
+                if (!STAGE)
+                    for (int cc = OBS_HEAD + p.lidar_slots + sub; cc < p.D; cc += 8) row[cc] = 0.0f;
             }
         }
     } else {
         for (int i = tid; i < N; i += WAVE) {
             const int g = e * N + i;
-            float* row = out.obs + (size_t)g * p.D;
+            float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)g * p.D;
             if (!el.alive[i]) {
                 for (int c = 0; c < OBS_HEAD; ++c) row[c] = 0.0f;
-                for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
+                if (!STAGE)
+                    for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
                 continue;
             }
-            write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row);
+            write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row, !STAGE);
         }
     }
     STAMP(6);
@@ -1184,7 +1242,9 @@ struct LidarLayout {
 
 __host__ __device__ inline int lidar_cand_max(const SimParams& p) { return p.N - 1 + (p.traffic ? p.K : 0); }
 
-__host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax) {
+// with_bx: a per-segment copy of the obstacle box (k_lidar, whose boxes are in
+// HBM); k_step reads them from its own LDS obstacle table instead.
+__host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax, bool with_bx = true) {
     LidarLayout L;
     const int C = G * cmax;
     int off = 0;
@@ -1193,7 +1253,7 @@ __host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax) {
     L.res = off; off += G * R * 4;
     off = (off + 15) & ~15;
     L.seg_rg = off; off += C * 16;
-    L.seg_bx = off; off += C * 16;
+    L.seg_bx = off; off += with_bx ? C * 16 : 0;
     L.seg_jo = off; off += C * 4;
     L.queue = L.seg_rg;
     if (off < L.queue + G * R * 2) off = L.queue + G * R * 2;
@@ -1211,7 +1271,10 @@ int lidar_group(int R) {
 // HBM as k_cars published it (k_lidar), or the LDS of the same wave's
 // cars_body (k_step).
 struct LidarSrcHbm {
+    static constexpr bool kStaged = false;  // writes the LiDAR block (and dead rows) itself
+    static constexpr bool kBoxLds = false;  // boxes come from HBM: cache one per segment in LDS
     const SimParams& p;
+    __device__ float rel(int b) const { return p.rel_angles[b]; }
     __device__ bool alive(int g) const { return p.ego.alive[g] != 0; }
     __device__ float4 pose(int g) const { return make_float4(p.ego.x[g], p.ego.y[g], p.ego.h[g], __int_as_float(g)); }
     __device__ void cand(int g, unsigned long long& c0, unsigned long long& c1) const {
@@ -1221,8 +1284,11 @@ struct LidarSrcHbm {
     __device__ int4 box(int g, int o) const { return p.ob_box[(size_t)(g / p.N) * p.ob_stride + o]; }
 };
 struct LidarSrcLds {
+    static constexpr bool kStaged = MEV_FUSED_STAGED;  // leave the results in LDS for fused_store
+    static constexpr bool kBoxLds = true;  // the obstacle table is in this wave's LDS
     const CarsLDS& el;
     int g0;  // global index of the env's agent 0
+    __device__ float rel(int b) const { return el.rel[b]; }
     __device__ bool alive(int g) const { return el.alive[g - g0] != 0; }
     __device__ float4 pose(int g) const {
         const int i = g - g0;
@@ -1243,7 +1309,7 @@ struct LidarSrcLds {
 // longest beam of its agent is done (lockstep cost = max over the agent's
 // beams, pooled cost ~ their mean); phase 3 resolves the cars as packed
 // (agent, box, beam) pairs and writes the observation's LiDAR block.
-template <bool TAB, class Src>
+template <bool TAB, int ILP, class Src>
 __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& out, const Src& src, const int G,
                                            const int a0, const int na, const int lane, unsigned char* base,
                                            const LidarLayout& lay) {
@@ -1265,7 +1331,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const int g = a0 + lane;
         ag[lane_rank(am)] = src.pose(g);
     }
-    if (__popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
+    if (!Src::kStaged && __popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
         for (int j = 0; j < na; ++j) {
             if ((am >> j) & 1ull) continue;
             float* row = out.obs + (size_t)(a0 + j) * p.D + OBS_HEAD;
@@ -1324,42 +1390,67 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     int qn = 0;
     // beam offsets rel[b] of the first two chunks of 64 beams, loaded once:
     // a global load inside the loop would expose its latency every iteration
-    const float rel_c0 = lane < R ? p.rel_angles[lane] : 0.0f;
-    const float rel_c1 = lane + WAVE < R ? p.rel_angles[lane + WAVE] : 0.0f;
-    for (int j = 0; j < nal; ++j) {
-        const float4 a = ag[j];
+    const float rel_c0 = lane < R ? src.rel(lane) : 0.0f;
+    const float rel_c1 = lane + WAVE < R ? src.rel(lane + WAVE) : 0.0f;
+    // one beam: direction (Lidar.cpp:24-26) and the first probes; returns the
+    // beam's result (>= 0) or -(next probe to test) - 1
+    auto setup = [&](const float4& a, float rel_b, auto small, float2& d) -> int {
+        float sn, cs;
+        if constexpr (decltype(small)::value) sincosf_below120(a.z + rel_b, &sn, &cs);
+        else sincosf(a.z + rel_b, &sn, &cs);
+        const float dx = cs, dy = -sn;
+        d = make_float2(dx, dy);
+#ifdef MEV_EXP_NOROAD
+        return S << 1;
+#else
         const int px = (int)a.x, py = (int)a.y;
         const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
-        for (int b0 = 0; b0 < R; b0 += WAVE) {
-            const int b = b0 + lane;
-            bool pend = false;
-            if (b < R) {
-                float sn, cs;
-                const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : p.rel_angles[b]);
-                sincosf(a.z + rel_b, &sn, &cs);  // Lidar.cpp:24-26
-                const float dx = cs, dy = -sn;
-                dir[j * R + b] = make_float2(dx, dy);
-                int k1 = 0;
-                if (pmax < (unsigned)WIDTH) {
-                    const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
-                    const float safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
-                    // probes 1 .. j lie within j*step <= safe of the centre
-                    k1 = 1 + ((safe >= stp) ? (int)(safe * inv_stp) : 0);
-                }
-#ifdef MEV_EXP_NOROAD
-                res[j * R + b] = S << 1;
-#else
-                float fx, fy;
-                const int r = probes(a.x, a.y, dx, dy, k1, fx, fy);
-                res[j * R + b] = r >= 0 ? r : k1 + LIDAR_NPR;  // result, or the next probe to test
-                pend = r < 0;
+        const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
+        const float safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
+        // probes 1 .. j lie within j*step <= safe of the centre (car centre on screen)
+        const int k1 = pmax < (unsigned)WIDTH ? 1 + ((safe >= stp) ? (int)(safe * inv_stp) : 0) : 0;
+        float fx, fy;
+        const int r = probes(a.x, a.y, dx, dy, k1, fx, fy);
+        return r >= 0 ? r : -(k1 + LIDAR_NPR) - 1;
 #endif
+    };
+    // ILP = 2: two agents per pass, two independent dependency chains (sincosf's
+    // double polynomial, the safe distance, the probes) the compiler interleaves
+    // (k_step, 128 VGPRs); ILP = 1 in k_lidar, whose 64-VGPR budget would spill
+    auto phase1 = [&](auto small) {
+        for (int j = 0; j < nal; j += ILP) {
+            const bool two = ILP == 2 && j + 1 < nal;
+            const float4 aA = ag[j], aB = ag[two ? j + 1 : j];
+            for (int b0 = 0; b0 < R; b0 += WAVE) {
+                const int b = b0 + lane;
+                const bool vb = b < R;
+                const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : (vb ? src.rel(b) : 0.0f));
+                float2 dA, dB = make_float2(0.0f, 0.0f);
+                const int rA = setup(aA, rel_b, small, dA);
+                int rB = 0;
+                if constexpr (ILP == 2) rB = setup(aB, rel_b, small, dB);
+                if (vb) {
+                    dir[j * R + b] = dA;
+                    res[j * R + b] = rA >= 0 ? rA : -rA - 1;  // result, or the next probe to test
+                    if (two) {
+                        dir[(j + 1) * R + b] = dB;
+                        res[(j + 1) * R + b] = rB >= 0 ? rB : -rB - 1;
+                    }
+                }
+                const bool pA = vb && rA < 0, pB = vb && two && rB < 0;
+                const unsigned long long mA = ballot(pA), mB = ballot(pB);
+                const int nA = __popcll(mA);
+                if (pA) queue[qn + lane_rank(mA)] = (unsigned short)(j * R + b);
+                if (pB) queue[qn + nA + lane_rank(mB)] = (unsigned short)((j + 1) * R + b);
+                qn += nA + __popcll(mB);
             }
-            const unsigned long long pm = ballot(pend);
-            if (pend) queue[qn + lane_rank(pm)] = (unsigned short)(j * R + b);
-            qn += __popcll(pm);
         }
-    }
+    };
+    // |heading| < 100 for every agent (always, unless set_state() planted a
+    // wild heading): |h + rel| < 120, the range of the branch-free sincosf
+    const bool hsmall = ballot(lane < nal && !(fabs_f(ag[lane < nal ? lane : 0].z) < 100.0f)) == 0ull;
+    if (ILP == 2 && hsmall) phase1(std::true_type{});  // k_lidar: one instantiation (64 VGPRs)
+    else phase1(std::false_type{});
     wave_lds_sync();
 #if defined(MEV_STAMPS_R)  // one pool per env: slot 4 = end of phase 1
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 4] = __builtin_amdgcn_s_memrealtime();
@@ -1451,15 +1542,15 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // the range covers the angular span of the box's real slab (box_lo/box_hi):
     // a ray outside it never meets the slab, so none of its probes can land in
     // the box.
-    const float rel0 = p.rel_angles[0];
-    const float dphi = R > 1 ? (p.rel_angles[R - 1] - rel0) / (float)(R - 1) : 1.0f;
+    const float rel0 = src.rel(0);
+    const float dphi = R > 1 ? (src.rel(R - 1) - rel0) / (float)(R - 1) : 1.0f;
     const float idphi = 1.0f / dphi;
     const float period = 6.28318531f * idphi;  // beam indices per revolution
     for (int m = lane; m < M; m += WAVE) {
         const int jo = seg_jo[m];
         const float4 a = ag[jo >> 8];
         const int4 bx = src.box(__float_as_int(a.w), jo & 255);
-        seg_bx[m] = bx;
+        if (!Src::kBoxLds) seg_bx[m] = bx;
         const float ex0 = box_lo(bx.x), ex1 = box_hi(bx.y);
         const float ey0 = box_lo(bx.z), ey1 = box_hi(bx.w);
         int4 rg;
@@ -1528,7 +1619,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 const int j = seg_jo[m] >> 8;
                 const float4 a = ag[j];
                 const int4 rg = seg_rg[m];
-                const int4 bx = seg_bx[m];
+                const int4 bx = Src::kBoxLds ? src.box(0, seg_jo[m] & 255) : seg_bx[m];
                 const int cA = rg.x >> 16, cB = rg.y >> 16;
                 const int b = r < cA ? (rg.x & 0xffff) + r
                                      : (r < cA + cB ? (rg.y & 0xffff) + r - cA : (rg.z & 0xffff) + r - cA - cB);
@@ -1555,7 +1646,10 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 if (lo > hi) kb = 0;
                 // ... resolved by exact probes in march order
                 for (int kk = ka; kk <= kb; ++kk) {
-                    const float d = march_dist(p, kk);
+                    // a runtime table test here, not march_dist<TAB>: measured 4 us per
+                    // step faster in k_step, and without it k_lidar's 64-VGPR
+                    // allocation spills ~180 registers
+                    const float d = p.dist_tab ? p.dist_tab[kk] : (float)kk * p.lidar_step;
                     const int px = (int)(a.x + dd.x * d), py = (int)(a.y + dd.y * d);
                     if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) {
                         atomicMin(&res[slot], (kk << 1) | 1);
@@ -1569,12 +1663,13 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
 #if defined(MEV_STAMPS_R)
     if (lane == 0) p.debug[se_ * 8 + 5 + sp_] = __builtin_amdgcn_s_memrealtime();
 #endif
+    if (Src::kStaged) return;  // k_step: fused_store writes the block from res
     for (int j = 0; j < nal; ++j) {  // 3d: Lidar::normalized (:92-98)
         const int g = __float_as_int(ag[j].w);
         float* row = out.obs + (size_t)g * p.D + OBS_HEAD;
         for (int b = lane; b < p.lidar_slots; b += WAVE) {
             const int r = res[j * R + b];
-            const float final_dist = (r & 1) ? march_dist(p, r >> 1) : p.lidar_max;
+            const float final_dist = (r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max;
             row[b] = final_dist * p.lidar_inv;
         }
     }
@@ -1590,34 +1685,124 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     if (a0 >= a_end) return;  // wave-uniform exit: the kernel has no block-level barrier
     const int na = a_end - a0 < G ? a_end - a0 : G;
     const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p));
-    lidar_body<TAB>(p, out, LidarSrcHbm{p}, G, a0, na, lane, lds_raw + (size_t)wv * (size_t)lay.bytes, lay);
+    lidar_body<TAB, 1>(p, out, LidarSrcHbm{p}, G, a0, na, lane, lds_raw + (size_t)wv * (size_t)lay.bytes, lay);
 }
 
+// End of k_step: every output of the env and its state, written once from LDS.
+// The env's observation rows [N][D] are one contiguous block of HBM, written
+// with 16-byte stores: head (staged by cars_body), LiDAR (Lidar::normalized,
+// :92-98, from the beam results res) and zero padding; a dead agent's row is zero.
+template <bool TAB>
+__device__ __forceinline__ void fused_store(const SimParams& p, const Outputs& out, const int e, const CarsLDS& el,
+                                            const int* res, const int lane) {
+    const int N = p.N, D = p.D, R = p.R, slots = p.lidar_slots;
+    const unsigned long long am = ballot(lane < N && el.alive[lane < N ? lane : 0] != 0);
+    const int total = N * D;
+    const float invD = 1.0f / (float)D;
+    // branch-free: both LDS reads are issued with clamped indices, then selected
+    auto value = [&](int idx) -> float {
+        int i = (int)((float)idx * invD);  // idx / D, corrected for the reciprocal's rounding
+        i -= i * D > idx ? 1 : 0;
+        i += (i + 1) * D <= idx ? 1 : 0;
+        const int c = idx - i * D;
+        const int b = c - OBS_HEAD;
+        const int j = __popcll(am & ((1ull << i) - 1ull));  // compacted LiDAR slot of agent i
+        const float hv = el.head[i * OBS_HEAD + (c < OBS_HEAD ? c : 0)];
+        const int r = res[j * R + (b >= 0 && b < slots ? b : 0)];
+        const float lv = ((r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max) * p.lidar_inv;
+        const float v = c < OBS_HEAD ? hv : (b < slots ? lv : 0.0f);
+        return ((am >> i) & 1ull) ? v : 0.0f;
+    };
+    float* blk = out.obs + (size_t)e * (size_t)total;
+    if ((total & 3) == 0) {
+        float4* b4 = reinterpret_cast<float4*>(blk);
+        for (int q = lane; q < total / 4; q += WAVE)
+            b4[q] = make_float4(value(4 * q), value(4 * q + 1), value(4 * q + 2), value(4 * q + 3));
+    } else {
+        for (int idx = lane; idx < total; idx += WAVE) blk[idx] = value(idx);
+    }
+    const bool do_reset = el.envw[5] != 0;
+    for (int i = lane; i < N; i += WAVE) {
+        const int g = e * N + i;
+        out.rew[g] = el.rew[i];
+        out.done[g] = el.done[i];
+        out.status[g] = el.status[i];
+        p.ego.x[g] = el.x[i]; p.ego.y[g] = el.y[i]; p.ego.v[g] = el.v[i]; p.ego.h[g] = el.h[i];
+        p.ego.acc[g] = el.acc[i]; p.ego.steer[g] = el.steer[i]; p.ego.pidx[g] = el.pidx[i];
+        p.ego.prev_dist[g] = el.prev_dist[i]; p.ego.pa0[g] = el.pa0[i]; p.ego.pa1[g] = el.pa1[i];
+        if (do_reset) {
+            p.ego.sx[g] = el.sx[i]; p.ego.sy[g] = el.sy[i]; p.ego.sv[g] = el.sv[i]; p.ego.sh[g] = el.sh[i];
+            p.ego.intent[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; p.ego.route[g] = el.route[i];
+        }
+    }
+    if (lane == 0) {
+        out.term[e] = el.envw[0];
+        out.trunc[e] = el.envw[1];
+        out.alive_cnt[e] = el.envw[2];
+        out.step[e] = el.envw[3];
+        p.step_count[e] = el.envw[3];
+        p.pending_reset[e] = el.envw[4];
+    }
+}
+
+// LDS of one k_step wave: cars LDS, the staged heads [N][31], the beam offsets
+// [R], the env flags [8], then the LiDAR pool of the env's N agents.
+struct StepLayout {
+    int head, rel, envw, lidar, bytes;
+};
+__host__ __device__ inline StepLayout step_layout(const SimParams& p) {
+    StepLayout L;
+    int off = (int)lds_al(cars_lds_bytes(p.N, cars_k(p)));
+    L.head = off; off += MEV_FUSED_STAGED ? (int)lds_al((size_t)p.N * OBS_HEAD * 4) : 0;
+    L.rel = off; off += (int)lds_al((size_t)p.R * 4);
+    L.envw = off; off += 32;
+    L.lidar = off; off += lidar_layout(p.N, p.R, lidar_cand_max(p), false).bytes;
+    L.bytes = off;
+    return L;
+}
+
+// Issue priorities of k_step's two parts (s_setprio; experiments: tools/kernel_time.py)
+#ifndef MEV_PRIO_CARS
+#define MEV_PRIO_CARS 1
+#endif
+#ifndef MEV_PRIO_LIDAR
+#define MEV_PRIO_LIDAR 0
+#endif
+
 // The whole step in one wave per env: cars_body, then the LiDAR of the env's
-// N agents in pools of G from the same wave's LDS (no HBM hand-off, no second
-// launch; a wave whose env finishes its car logic early starts its LiDAR
-// while other waves on the SIMD are still in theirs).
+// N agents as one pool, from the same wave's LDS, then every output written
+// once (fused_store).  No HBM hand-off, no second launch, and no global store
+// before the last phase (a later load's vmcnt wait would drain them); a wave
+// whose env finishes its car logic early starts its LiDAR while other waves
+// on the SIMD are still in theirs.  The car part runs at a higher issue
+// priority: it is the latency-bound critical path of each wave.
 template <bool TRAFFIC, bool TAB>
-__global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Outputs out, int G) {
+__global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Outputs out) {
     extern __shared__ __align__(16) unsigned char step_lds[];
     const int e = blockIdx.x;
 #if defined(MEV_STAMPS_R)
     STAMP_RAW(0);
 #endif
-    const CarsLDS el = carve_cars_lds(step_lds, p.N, cars_k(p));
+    const StepLayout sl = step_layout(p);
+    CarsLDS el = carve_cars_lds(step_lds, p.N, cars_k(p));
+    el.head = reinterpret_cast<float*>(step_lds + sl.head);
+    el.rel = reinterpret_cast<float*>(step_lds + sl.rel);
+    el.envw = reinterpret_cast<int32_t*>(step_lds + sl.envw);
     __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
     NpcLDS* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
+    if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
     cars_body<TRAFFIC, true>(p, in, out, e, el, nl);
     wave_lds_sync();
-    const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p));
-    unsigned char* lbase = step_lds + lds_al(cars_lds_bytes(p.N, cars_k(p)));
+    if (MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
+    const LidarLayout lay = lidar_layout(p.N, p.R, lidar_cand_max(p), false);
+    unsigned char* lbase = step_lds + sl.lidar;
     const int lane = threadIdx.x & (WAVE - 1);
     const int g0 = e * p.N;
-    for (int j0 = 0; j0 < p.N; j0 += G) {
-        const int na = p.N - j0 < G ? p.N - j0 : G;
-        lidar_body<TAB>(p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
+    lidar_body<TAB, 2>(p, out, LidarSrcLds{el, g0}, p.N, g0, p.N, lane, lbase, lay);
+    if (MEV_FUSED_STAGED) {
         wave_lds_sync();
+        fused_store<TAB>(p, out, e, el, reinterpret_cast<const int*>(lbase + lay.res), lane);
     }
 }
 
@@ -1714,25 +1899,16 @@ static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Ou
     return e;
 }
 
-// LDS of one k_step wave (cars + LiDAR pool of G agents), or 0 when the fused
-// kernel does not apply.  At 4 waves per SIMD (128 VGPRs) a CU holds 16 waves,
-// so a wave may take 160 KB / 16 = 10 KB.
-static int fused_lds_bytes(const SimParams& p, int G) {
-    return (int)lds_al(cars_lds_bytes(p.N, cars_k(p))) + lidar_layout(G, p.R, lidar_cand_max(p)).bytes;
-}
-
-static int fused_group(const SimParams& p) {
-    if (p.traffic) return 0;  // the NPC phase's LDS leaves no room for a LiDAR pool
-    static const int g_env = [] { const char* v = getenv("MEV_FUSED_G"); return v ? atoi(v) : 0; }();
-    if (g_env > 0) return fused_lds_bytes(p, g_env) <= 10 * 1024 ? g_env : 0;  // experiments
-    // the largest pool of <= 512 beams that fits (one pool of the env's 8 agents at R = 64)
-    for (int G = p.N; G >= 1; --G)
-        if (G * p.R <= 512 && fused_lds_bytes(p, G) <= 10 * 1024) return G;
-    return 0;
+// k_step applies without traffic when the env's N*R beams form one pool of at
+// most 512 beams and its LDS fits a wave's share: at 4 waves per SIMD (128
+// VGPRs) a CU holds 16 waves, so a wave may take 160 KB / 16 = 10 KB.
+static bool fused_fits(const SimParams& p) {
+    if (p.traffic) return false;  // the NPC phase's LDS leaves no room for a LiDAR pool
+    return p.N * p.R <= 512 && step_layout(p).bytes <= 10 * 1024;
 }
 
 int step_kernel_for(const SimParams& p) {
-    const bool fusable = fused_group(p) > 0;
+    const bool fusable = fused_fits(p);
     if (p.step_kernel == 1) return 1;
     if (p.step_kernel == 2) return fusable ? 2 : 0;
     // auto: fused once the batch fills the chip with one wave per env (>= 4 per CU);
@@ -1745,11 +1921,10 @@ hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& 
     const int kind = step_kernel_for(p);
     if (kind == 0) return hipErrorInvalidValue;
     if (kind == 2) {
-        const int G = fused_group(p);
         if (ev) (void)hipEventRecord(ev[0], s);
-        const unsigned lds = (unsigned)fused_lds_bytes(p, G);
-        if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true>), dim3(p.E), dim3(WAVE), lds, s, p, in, out, G);
-        else hipLaunchKernelGGL((k_step<false, false>), dim3(p.E), dim3(WAVE), lds, s, p, in, out, G);
+        const unsigned lds = (unsigned)step_layout(p).bytes;
+        if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
+        else hipLaunchKernelGGL((k_step<false, false>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
         hipError_t e = hipGetLastError();
         if (ev && e == hipSuccess) { (void)hipEventRecord(ev[1], s); (void)hipEventRecord(ev[2], s); }
         return e;

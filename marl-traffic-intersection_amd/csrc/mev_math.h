@@ -124,6 +124,33 @@ MEV_HD double reduce_large(uint32_t xi, int* np) {
     return x * 0x1.921fb54442d18p-62;
 }
 
+// glibc's polynomial step after a reduction to x (double) and n: with the
+// table selector q (n, or n + sign in the large path) sign[q & 3] = {1, -1, -1, 1}
+// multiplies x by +-1 (an exact negation) and kSinCos[1] is kSinCos[0] with
+// the cosine coefficients c0..c4 negated, so its cosine polynomial -- and the
+// rounded float -- is exactly the negation of kSinCos[0]'s; no per-lane table
+// loads.  Returns (sin, cos) before the |y| < 2^-12 shortcut.
+template <bool FMA>
+MEV_HD void sincos_tail(double x, int n, int q, float* so, float* co) {
+    const double xs = ((q + 1) & 2) ? -x : x;
+    const SinCosTab& p = kSinCos[0];
+    const double x2 = x * x;
+    const double x4 = x2 * x2;
+    const double x3 = x2 * xs;
+    const double c2 = madd<FMA>(p.c3, x2, p.c4);
+    const double s1 = madd<FMA>(p.s2, x2, p.s3);
+    const double c1 = madd<FMA>(p.c0, x2, p.c1);
+    const double x5 = x3 * x2;
+    const double x6 = x4 * x2;
+    const double sp = madd<FMA>(xs, x3, p.s1);
+    const double cp = madd<FMA>(c1, x4, p.c2);
+    const float sv = (float)madd<FMA>(sp, x5, s1);
+    float cv = (float)madd<FMA>(cp, x6, c2);
+    cv = (q & 2) ? -cv : cv;
+    *so = (n & 1) ? cv : sv;
+    *co = (n & 1) ? sv : cv;
+}
+
 template <bool FMA>
 MEV_HD void sincosf_impl(float y, float* sinp, float* cosp) {
     double x = y;
@@ -139,16 +166,12 @@ MEV_HD void sincosf_impl(float y, float* sinp, float* cosp) {
         sincosf_poly<FMA>(x, x2, *p, 0, sinp, cosp);
     } else if (abstop12(y) < abstop12(120.0f)) {
         x = reduce_fast<FMA>(x, *p, &n);
-        const double s = p->sign[n & 3];
-        if (n & 2) p = &kSinCos[1];
-        sincosf_poly<FMA>(x * s, x * x, *p, n, sinp, cosp);
+        sincos_tail<FMA>(x, n, n, sinp, cosp);
     } else if (abstop12(y) < abstop12(__builtin_inff())) {
         const uint32_t xi = f2u(y);
         const int sign = xi >> 31;
         x = reduce_large(xi, &n);
-        const double s = p->sign[(n + sign) & 3];
-        if ((n + sign) & 2) p = &kSinCos[1];
-        sincosf_poly<FMA>(x * s, x * x, *p, n, sinp, cosp);
+        sincos_tail<FMA>(x, n, n + sign, sinp, cosp);
     } else {
         *sinp = *cosp = y - y;  // NaN for inf / NaN input
     }
@@ -161,40 +184,30 @@ MEV_HD void sincosf_impl(float y, float* sinp, float* cosp) {
 // checked for every float |y| <= 8 by tests/native/devmath_check.cpp.  A wave
 // of beams then does not evaluate the polynomial twice.
 template <bool FMA>
+MEV_HD void sincosf_below120_impl(float y, float* sinp, float* cosp) {
+    int n;
+    const double x = reduce_fast<FMA>((double)y, kSinCos[0], &n);
+    float so, co;
+    sincos_tail<FMA>(x, n, n, &so, &co);
+    const bool tiny = abstop12(y) < abstop12(0x1p-12f);  // glibc's shortcut (keeps the sign of -0)
+    *sinp = tiny ? y : so;
+    *cosp = tiny ? 1.0f : co;
+}
+
+template <bool FMA>
 MEV_HD void sincosf_reduced_impl(float y, float* sinp, float* cosp) {
     if (!(abstop12(y) < abstop12(120.0f))) {
         sincosf_impl<FMA>(y, sinp, cosp);
         return;
     }
-    int n;
-    const double x = reduce_fast<FMA>((double)y, kSinCos[0], &n);
-    // no per-lane table loads: sign[n & 3] = {1, -1, -1, 1} multiplies x by +-1
-    // (an exact negation), and kSinCos[1] is kSinCos[0] with the cosine
-    // coefficients c0..c4 negated, so its cosine polynomial -- and the rounded
-    // float -- is exactly the negation of kSinCos[0]'s
-    const double xs = ((n + 1) & 2) ? -x : x;
-    const SinCosTab& p = kSinCos[0];
-    const double x2 = x * x;
-    const double x4 = x2 * x2;
-    const double x3 = x2 * xs;
-    const double c2 = madd<FMA>(p.c3, x2, p.c4);
-    const double s1 = madd<FMA>(p.s2, x2, p.s3);
-    const double c1 = madd<FMA>(p.c0, x2, p.c1);
-    const double x5 = x3 * x2;
-    const double x6 = x4 * x2;
-    const double sp = madd<FMA>(xs, x3, p.s1);
-    const double cp = madd<FMA>(c1, x4, p.c2);
-    const float sv = (float)madd<FMA>(sp, x5, s1);
-    float cv = (float)madd<FMA>(cp, x6, c2);
-    cv = (n & 2) ? -cv : cv;
-    const bool tiny = abstop12(y) < abstop12(0x1p-12f);  // glibc's shortcut (keeps the sign of -0)
-    const float so = (n & 1) ? cv : sv, co = (n & 1) ? sv : cv;
-    *sinp = tiny ? y : so;
-    *cosp = tiny ? 1.0f : co;
+    sincosf_below120_impl<FMA>(y, sinp, cosp);
 }
 
 // the simulator's sincosf (glibc results; single path below 120)
 MEV_HD void sincosf(float y, float* s, float* c) { sincosf_reduced_impl<MEV_SINCOS_FMA != 0>(y, s, c); }
+// the same for a caller that guarantees |y| < 120 (no branch: straight-line code
+// the compiler can interleave with other independent work)
+MEV_HD void sincosf_below120(float y, float* s, float* c) { sincosf_below120_impl<MEV_SINCOS_FMA != 0>(y, s, c); }
 
 // ------------------------------------------------------------------ tanf ---
 MEV_HD float kernel_tanf(float x, float y, int iy) {
