@@ -219,12 +219,29 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     hipError_t err = hipSuccess;
     auto A = [&](auto** ptr, size_t n) { if (err == hipSuccess) err = h->alloc(ptr, n); };
     // state
-    A(&p.ego.x, EN); A(&p.ego.y, EN); A(&p.ego.v, EN); A(&p.ego.h, EN); A(&p.ego.acc, EN); A(&p.ego.steer, EN);
-    A(&p.ego.prev_dist, EN); A(&p.ego.pa0, EN); A(&p.ego.pa1, EN);
-    A(&p.ego.sx, EN); A(&p.ego.sy, EN); A(&p.ego.sv, EN); A(&p.ego.sh, EN);
-    A(&p.ego.pidx, EN); A(&p.ego.route, EN); A(&p.ego.intent, EN); A(&p.ego.alive, EN);
-    A(&p.npc.x, EK); A(&p.npc.y, EK); A(&p.npc.v, EK); A(&p.npc.h, EK); A(&p.npc.acc, EK); A(&p.npc.steer, EK);
-    A(&p.npc.pidx, EK); A(&p.npc.route, EK); A(&p.npc.intent, EK); A(&p.npc.alive, EK); A(&p.npc.count, size_t(E));
+    // the 4-byte fields of each SoA in one block, field k at k * stride (mev_kernels.h)
+    const size_t ens = (EN + 63) & ~size_t(63), eks = (EK + 63) & ~size_t(63);
+    float* eblk = nullptr;
+    float* nblk = nullptr;
+    A(&eblk, ens * mev::EF_COUNT);
+    A(&nblk, eks * mev::NF_COUNT);
+    if (err == hipSuccess) {
+        float** ef[] = {&p.ego.x, &p.ego.y, &p.ego.v, &p.ego.h, &p.ego.acc, &p.ego.steer, &p.ego.prev_dist,
+                        &p.ego.pa0, &p.ego.pa1, &p.ego.sx, &p.ego.sy, &p.ego.sv, &p.ego.sh};
+        for (int k = 0; k < mev::EF_PIDX; ++k) *ef[k] = eblk + size_t(k) * ens;
+        p.ego.pidx = reinterpret_cast<int32_t*>(eblk + size_t(mev::EF_PIDX) * ens);
+        p.ego.route = reinterpret_cast<int32_t*>(eblk + size_t(mev::EF_ROUTE) * ens);
+        p.ego.intent = reinterpret_cast<int32_t*>(eblk + size_t(mev::EF_INTENT) * ens);
+        p.ego.stride = int64_t(ens);
+        float** nf[] = {&p.npc.x, &p.npc.y, &p.npc.v, &p.npc.h, &p.npc.acc, &p.npc.steer};
+        for (int k = 0; k < mev::NF_PIDX; ++k) *nf[k] = nblk + size_t(k) * eks;
+        p.npc.pidx = reinterpret_cast<int32_t*>(nblk + size_t(mev::NF_PIDX) * eks);
+        p.npc.route = reinterpret_cast<int32_t*>(nblk + size_t(mev::NF_ROUTE) * eks);
+        p.npc.intent = reinterpret_cast<int32_t*>(nblk + size_t(mev::NF_INTENT) * eks);
+        p.npc.stride = int64_t(eks);
+    }
+    A(&p.ego.alive, EN);
+    A(&p.npc.alive, EK); A(&p.npc.count, size_t(E));
     A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 1); A(&p.debug, size_t(E) * 8);
     A(&p.ob_box, size_t(E) * size_t(N + c.max_npcs)); A(&p.ob_cand, EN * 2);
     // outputs

@@ -19,18 +19,26 @@
 
 namespace mev {
 
+// The 4-byte fields of each SoA live in ONE allocation, field k at base +
+// k * stride (x first): kernels address them from the x pointer and the stride
+// so they hold one base address in SGPRs instead of one pointer per field.
 struct EgoSoA {
     float *x, *y, *v, *h, *acc, *steer, *prev_dist, *pa0, *pa1, *sx, *sy, *sv, *sh;
     int32_t *pidx, *route, *intent;
     uint8_t* alive;
+    int64_t stride;  // elements between consecutive fields (>= E*N)
 };
+enum EgoField { EF_X, EF_Y, EF_V, EF_H, EF_ACC, EF_STEER, EF_PREV_DIST, EF_PA0, EF_PA1, EF_SX, EF_SY, EF_SV, EF_SH,
+                EF_PIDX, EF_ROUTE, EF_INTENT, EF_COUNT };
 
 struct NpcSoA {
     float *x, *y, *v, *h, *acc, *steer;
     int32_t *pidx, *route, *intent;
     uint8_t* alive;
     int32_t* count;
+    int64_t stride;  // elements between consecutive fields (>= E*K)
 };
+enum NpcField { NF_X, NF_Y, NF_V, NF_H, NF_ACC, NF_STEER, NF_PIDX, NF_ROUTE, NF_INTENT, NF_COUNT };
 
 struct RouteTab {
     const float* path;      // [nroutes][160][2]

@@ -64,6 +64,15 @@ constexpr int MAXK = 64;
 constexpr int MAXOB = MAXN + MAXK;
 
 // --------------------------------------------------------------- helpers ---
+// SoA field k of the ego / NPC blocks (one base pointer + stride, see EgoSoA)
+__device__ inline float* egof(const SimParams& p, int k) { return p.ego.x + p.ego.stride * k; }
+__device__ inline int32_t* egoi(const SimParams& p, int k) {
+    return reinterpret_cast<int32_t*>(p.ego.x + p.ego.stride * k);
+}
+__device__ inline float* npcf(const SimParams& p, int k) { return p.npc.x + p.npc.stride * k; }
+__device__ inline int32_t* npci(const SimParams& p, int k) {
+    return reinterpret_cast<int32_t*>(p.npc.x + p.npc.stride * k);
+}
 __device__ inline unsigned long long ballot(bool p) { return __ballot(p); }
 
 // LDS visibility between the lanes of one wave.  k_cars, k_reset and the NPC
@@ -189,15 +198,15 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // load
     if (lane < cnt) {
         const int g = e * K + lane;
-        nl.x[lane] = p.npc.x[g];
-        nl.y[lane] = p.npc.y[g];
-        nl.v[lane] = p.npc.v[g];
-        nl.h[lane] = p.npc.h[g];
-        nl.acc[lane] = p.npc.acc[g];
-        nl.steer[lane] = p.npc.steer[g];
-        nl.pidx[lane] = p.npc.pidx[g];
-        nl.route[lane] = p.npc.route[g];
-        nl.intent[lane] = p.npc.intent[g];
+        nl.x[lane] = npcf(p, NF_X)[g];
+        nl.y[lane] = npcf(p, NF_Y)[g];
+        nl.v[lane] = npcf(p, NF_V)[g];
+        nl.h[lane] = npcf(p, NF_H)[g];
+        nl.acc[lane] = npcf(p, NF_ACC)[g];
+        nl.steer[lane] = npcf(p, NF_STEER)[g];
+        nl.pidx[lane] = npci(p, NF_PIDX)[g];
+        nl.route[lane] = npci(p, NF_ROUTE)[g];
+        nl.intent[lane] = npci(p, NF_INTENT)[g];
         nl.alive[lane] = p.npc.alive[g];
     }
     // -- spawn (TrafficFlow.cpp:320-329, try_spawn_traffic_car :275-315)
@@ -498,9 +507,9 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // store back + corners of the survivors (for ego-NPC SAT)
     if (lane < newcnt) {
         const int g = e * K + lane;
-        p.npc.x[g] = nl.x[lane]; p.npc.y[g] = nl.y[lane]; p.npc.v[g] = nl.v[lane]; p.npc.h[g] = nl.h[lane];
-        p.npc.acc[g] = nl.acc[lane]; p.npc.steer[g] = nl.steer[lane]; p.npc.pidx[g] = nl.pidx[lane];
-        p.npc.route[g] = nl.route[lane]; p.npc.intent[g] = nl.intent[lane]; p.npc.alive[g] = 1;
+        npcf(p, NF_X)[g] = nl.x[lane]; npcf(p, NF_Y)[g] = nl.y[lane]; npcf(p, NF_V)[g] = nl.v[lane]; npcf(p, NF_H)[g] = nl.h[lane];
+        npcf(p, NF_ACC)[g] = nl.acc[lane]; npcf(p, NF_STEER)[g] = nl.steer[lane]; npci(p, NF_PIDX)[g] = nl.pidx[lane];
+        npci(p, NF_ROUTE)[g] = nl.route[lane]; npci(p, NF_INTENT)[g] = nl.intent[lane]; p.npc.alive[g] = 1;
         car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
     }
     if (lane == 0) p.npc.count[e] = newcnt;
@@ -685,13 +694,13 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
     }
     for (int i = tid; i < N; i += WAVE) {
         const int g = e * N + i;
-        const int route_l = p.ego.route[g];
+        const int route_l = egoi(p, EF_ROUTE)[g];
         const float a0 = in.actions[2 * g], a1 = in.actions[2 * g + 1];
-        const float x = p.ego.x[g], y = p.ego.y[g], v = p.ego.v[g], h = p.ego.h[g];
-        const float acc = p.ego.acc[g], steer = p.ego.steer[g], pd = p.ego.prev_dist[g];
-        const float pa0 = p.ego.pa0[g], pa1 = p.ego.pa1[g];
-        const float sx = p.ego.sx[g], sy = p.ego.sy[g], sv = p.ego.sv[g], sh = p.ego.sh[g];
-        const int pidx = p.ego.pidx[g], intent = p.ego.intent[g];
+        const float x = egof(p, EF_X)[g], y = egof(p, EF_Y)[g], v = egof(p, EF_V)[g], h = egof(p, EF_H)[g];
+        const float acc = egof(p, EF_ACC)[g], steer = egof(p, EF_STEER)[g], pd = egof(p, EF_PREV_DIST)[g];
+        const float pa0 = egof(p, EF_PA0)[g], pa1 = egof(p, EF_PA1)[g];
+        const float sx = egof(p, EF_SX)[g], sy = egof(p, EF_SY)[g], sv = egof(p, EF_SV)[g], sh = egof(p, EF_SH)[g];
+        const int pidx = egoi(p, EF_PIDX)[g], intent = egoi(p, EF_INTENT)[g];
         const uint8_t alive = p.ego.alive[g];
         el.a0[i] = a0;
         el.a1[i] = a1;
@@ -969,12 +978,12 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
             el.tgx[i] = el.t10x[i]; el.tgy[i] = el.t10y[i];  // path[min(0 + 10, 159)]
         }
         if (STAGE) continue;  // k_step writes the state back at its end (fused_store)
-        p.ego.x[g] = el.x[i]; p.ego.y[g] = el.y[i]; p.ego.v[g] = el.v[i]; p.ego.h[g] = el.h[i];
-        p.ego.acc[g] = el.acc[i]; p.ego.steer[g] = el.steer[i]; p.ego.pidx[g] = el.pidx[i];
-        p.ego.prev_dist[g] = el.prev_dist[i]; p.ego.pa0[g] = el.pa0[i]; p.ego.pa1[g] = el.pa1[i];
+        egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
+        egof(p, EF_ACC)[g] = el.acc[i]; egof(p, EF_STEER)[g] = el.steer[i]; egoi(p, EF_PIDX)[g] = el.pidx[i];
+        egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
         if (do_reset) {
-            p.ego.sx[g] = el.sx[i]; p.ego.sy[g] = el.sy[i]; p.ego.sv[g] = el.sv[i]; p.ego.sh[g] = el.sh[i];
-            p.ego.intent[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; p.ego.route[g] = el.route[i];
+            egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
+            egoi(p, EF_INTENT)[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
         }
     }
     wave_lds_sync();
@@ -1276,7 +1285,7 @@ struct LidarSrcHbm {
     const SimParams& p;
     __device__ float rel(int b) const { return p.rel_angles[b]; }
     __device__ bool alive(int g) const { return p.ego.alive[g] != 0; }
-    __device__ float4 pose(int g) const { return make_float4(p.ego.x[g], p.ego.y[g], p.ego.h[g], __int_as_float(g)); }
+    __device__ float4 pose(int g) const { return make_float4(egof(p, EF_X)[g], egof(p, EF_Y)[g], egof(p, EF_H)[g], __int_as_float(g)); }
     __device__ void cand(int g, unsigned long long& c0, unsigned long long& c1) const {
         c0 = p.ob_cand[2 * g];
         c1 = p.ob_cand[2 * g + 1];
@@ -1727,12 +1736,12 @@ __device__ __forceinline__ void fused_store(const SimParams& p, const Outputs& o
         out.rew[g] = el.rew[i];
         out.done[g] = el.done[i];
         out.status[g] = el.status[i];
-        p.ego.x[g] = el.x[i]; p.ego.y[g] = el.y[i]; p.ego.v[g] = el.v[i]; p.ego.h[g] = el.h[i];
-        p.ego.acc[g] = el.acc[i]; p.ego.steer[g] = el.steer[i]; p.ego.pidx[g] = el.pidx[i];
-        p.ego.prev_dist[g] = el.prev_dist[i]; p.ego.pa0[g] = el.pa0[i]; p.ego.pa1[g] = el.pa1[i];
+        egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
+        egof(p, EF_ACC)[g] = el.acc[i]; egof(p, EF_STEER)[g] = el.steer[i]; egoi(p, EF_PIDX)[g] = el.pidx[i];
+        egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
         if (do_reset) {
-            p.ego.sx[g] = el.sx[i]; p.ego.sy[g] = el.sy[i]; p.ego.sv[g] = el.sv[i]; p.ego.sh[g] = el.sh[i];
-            p.ego.intent[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; p.ego.route[g] = el.route[i];
+            egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
+            egoi(p, EF_INTENT)[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
         }
     }
     if (lane == 0) {
@@ -1823,19 +1832,19 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
     for (int i = lane; i < N; i += WAVE) {
         const int g = e * N + i;
         if (do_reset) {
-            const int rid = reset_route(p, rng_counter, e, i, p.ego.route[g]);
-            p.ego.route[g] = rid;
-            p.ego.x[g] = p.rt.spawn[3 * rid];
-            p.ego.y[g] = p.rt.spawn[3 * rid + 1];
-            p.ego.v[g] = 0.0f;
-            p.ego.h[g] = p.rt.spawn[3 * rid + 2];
-            p.ego.sx[g] = p.ego.x[g]; p.ego.sy[g] = p.ego.y[g]; p.ego.sv[g] = 0.0f; p.ego.sh[g] = p.ego.h[g];
-            p.ego.acc[g] = 0.0f; p.ego.steer[g] = 0.0f; p.ego.prev_dist[g] = 0.0f;
-            p.ego.pa0[g] = 0.0f; p.ego.pa1[g] = 0.0f; p.ego.pidx[g] = 0;
-            p.ego.intent[g] = p.rt.intent[rid]; p.ego.alive[g] = 1;
+            const int rid = reset_route(p, rng_counter, e, i, egoi(p, EF_ROUTE)[g]);
+            egoi(p, EF_ROUTE)[g] = rid;
+            egof(p, EF_X)[g] = p.rt.spawn[3 * rid];
+            egof(p, EF_Y)[g] = p.rt.spawn[3 * rid + 1];
+            egof(p, EF_V)[g] = 0.0f;
+            egof(p, EF_H)[g] = p.rt.spawn[3 * rid + 2];
+            egof(p, EF_SX)[g] = egof(p, EF_X)[g]; egof(p, EF_SY)[g] = egof(p, EF_Y)[g]; egof(p, EF_SV)[g] = 0.0f; egof(p, EF_SH)[g] = egof(p, EF_H)[g];
+            egof(p, EF_ACC)[g] = 0.0f; egof(p, EF_STEER)[g] = 0.0f; egof(p, EF_PREV_DIST)[g] = 0.0f;
+            egof(p, EF_PA0)[g] = 0.0f; egof(p, EF_PA1)[g] = 0.0f; egoi(p, EF_PIDX)[g] = 0;
+            egoi(p, EF_INTENT)[g] = p.rt.intent[rid]; p.ego.alive[g] = 1;
         }
-        el.x[i] = p.ego.x[g]; el.y[i] = p.ego.y[g]; el.v[i] = p.ego.v[g]; el.h[i] = p.ego.h[g];
-        el.alive[i] = p.ego.alive[g]; el.intent[i] = p.ego.intent[g]; el.pidx[i] = p.ego.pidx[g];
+        el.x[i] = egof(p, EF_X)[g]; el.y[i] = egof(p, EF_Y)[g]; el.v[i] = egof(p, EF_V)[g]; el.h[i] = egof(p, EF_H)[g];
+        el.alive[i] = p.ego.alive[g]; el.intent[i] = egoi(p, EF_INTENT)[g]; el.pidx[i] = egoi(p, EF_PIDX)[g];
     }
     int ncnt = 0;
     if (do_reset) {
@@ -1848,8 +1857,8 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
         ncnt = p.npc.count[e];
         if (lane < ncnt) {
             const int g = e * p.K + lane;
-            nl->x[lane] = p.npc.x[g]; nl->y[lane] = p.npc.y[g]; nl->v[lane] = p.npc.v[g]; nl->h[lane] = p.npc.h[g];
-            nl->intent[lane] = p.npc.intent[g]; nl->alive[lane] = p.npc.alive[g];
+            nl->x[lane] = npcf(p, NF_X)[g]; nl->y[lane] = npcf(p, NF_Y)[g]; nl->v[lane] = npcf(p, NF_V)[g]; nl->h[lane] = npcf(p, NF_H)[g];
+            nl->intent[lane] = npci(p, NF_INTENT)[g]; nl->alive[lane] = p.npc.alive[g];
         }
     }
     wave_lds_sync();
@@ -1860,7 +1869,7 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
             for (int c = 0; c < p.D; ++c) row[c] = 0.0f;
             continue;
         }
-        const float* path = p.rt.path + (size_t)p.ego.route[g] * (2 * PATH_LEN);
+        const float* path = p.rt.path + (size_t)egoi(p, EF_ROUTE)[g] * (2 * PATH_LEN);
         write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row);
         for (int b = 0; b < p.lidar_slots; ++b) row[OBS_HEAD + b] = p.lidar_max * p.lidar_inv;
     }
