@@ -85,6 +85,29 @@ __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Inclusive add / max scans over the 64 lanes with DPP row shifts and row
+// broadcasts (VALU only, no LDS permute round trips).  wave_scan_max assumes
+// values >= 0 (0 is the identity the shifted-in lanes read).
+template <class Op>
+__device__ inline int wave_scan_dpp(int v, Op op) {
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));  // row_shr:1
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));  // row_shr:2
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));  // row_shr:4
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));  // row_shr:8
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));  // row_bcast:15 -> rows 1, 3
+    v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+// one DPP lane move of a float (ctrl: quad_perm / row_half_mirror ...; every lane reads a valid lane)
+#define dpp_f(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xf, 0xf, false))
+
+__device__ inline int wave_scan_add(int v) {
+    return wave_scan_dpp(v, [](int a, int b) { return a + b; });
+}
+__device__ inline int wave_scan_max(int v) {
+    return wave_scan_dpp(v, [](int a, int b) { return a > b ? a : b; });
+}
+
 __device__ inline float wave_min(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -769,12 +792,14 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
                 if (d < bd) { bd = d; bi = start_i + off; }
             }
         }
-#pragma unroll
-        for (int o = 1; o < 8; o <<= 1) {
-            const float od = __shfl_xor(bd, o);
-            const int oi = __shfl_xor(bi, o);
+        // minimum over the 8 lanes of the group (first index on ties): DPP swaps
+        // within quads, then the mirror within each half-row (VALU, no LDS)
+        auto take = [&](float od, int oi) {
             if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
-        }
+        };
+        take(dpp_f(bd, 0xB1), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xf, 0xf, false));    // quad_perm [1,0,3,2]
+        take(dpp_f(bd, 0x4E), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xf, 0xf, false));    // quad_perm [2,3,0,1]
+        take(dpp_f(bd, 0x141), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xf, 0xf, false));  // row_half_mirror
         const int pidx = alive ? (bi == 0x7fffffff ? start_i : bi) : pidx0;
         // look-ahead point of the observation (:444-452), picked from the window
         {
@@ -1246,7 +1271,7 @@ __device__ inline int lane_rank(unsigned long long mask) {
 constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
 
 struct LidarLayout {
-    int ag, dir, res, seg_jo, seg_rg, seg_bx, queue, bytes;
+    int ag, dir, res, seg_jo, seg_rg, seg_bx, queue, scr, bytes;
 };
 
 __host__ __device__ inline int lidar_cand_max(const SimParams& p) { return p.N - 1 + (p.traffic ? p.K : 0); }
@@ -1266,6 +1291,8 @@ __host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax, bool
     L.seg_jo = off; off += C * 4;
     L.queue = L.seg_rg;
     if (off < L.queue + G * R * 2) off = L.queue + G * R * 2;
+    off = (off + 15) & ~15;
+    L.scr = off; off += WAVE * 4;  // the car phase's segment lookup (3c)
     L.bytes = (off + 15) & ~15;
     return L;
 }
@@ -1532,6 +1559,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     int* seg_jo = reinterpret_cast<int*>(base + lay.seg_jo);
     int4* seg_rg = reinterpret_cast<int4*>(base + lay.seg_rg);
     int4* seg_bx = reinterpret_cast<int4*>(base + lay.seg_bx);
+    int* scr = reinterpret_cast<int*>(base + lay.scr);
     int M = 0;
     for (int j = 0; j < nal; ++j) {  // 3a
         const int g = __builtin_amdgcn_readfirstlane(__float_as_int(ag[j].w));
@@ -1604,25 +1632,28 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     for (int cb = 0; cb < M; cb += WAVE) {
         const int nseg = M - cb < WAVE ? M - cb : WAVE;
         const int cnt = lane < nseg ? seg_rg[cb + lane].w : 0;
-        int incl = cnt;
-#pragma unroll
-        for (int off = 1; off < WAVE; off <<= 1) {
-            const int t = __shfl_up(incl, off);
-            if (lane >= off) incl += t;
-        }
+        const int incl = wave_scan_add(cnt);  // DPP, no LDS round trips
         const int excl = incl - cnt;
         const int T = __builtin_amdgcn_readlane(incl, WAVE - 1);
+        int carry = 0;  // (start << 8 | segment) of the segment running into this chunk
         for (int q0 = 0; q0 < T; q0 += WAVE) {
             const int q = q0 + lane;
-            // segment of pair q: the last m < nseg with excl[m] <= q (binary search)
-            int sm = 0;
-#pragma unroll
-            for (int st = WAVE / 2; st > 0; st >>= 1) {
-                const int c = sm + st;
-                const int ec = __shfl(excl, c < nseg ? c : 0);
-                sm = (c < nseg && ec <= q) ? c : sm;
-            }
-            const int r = q - __shfl(excl, sm);
+            // segment of pair q: the last m with excl[m] <= q.  Each segment that
+            // starts in this chunk writes (start << 8 | m) + 1 to the LDS slot of
+            // its start; a max-scan spreads it over the segment's lanes (starts
+            // increase with m, so the max is the latest); one LDS round trip
+            // instead of a chain of lane shuffles.
+            const bool starts = cnt > 0 && excl >= q0 && excl < q0 + WAVE;
+            scr[lane] = 0;
+            wave_lds_sync();  // lanes' writes to the same slot: the zeroing must not sink past the scatter
+            if (starts) scr[excl - q0] = ((excl << 8) | lane) + 1;
+            wave_lds_sync();
+            const int got = wave_scan_max(scr[lane]);
+            wave_lds_sync();  // the next chunk rewrites scr
+            const int cur = got > 0 ? got - 1 : carry;
+            carry = __builtin_amdgcn_readlane(cur, WAVE - 1);
+            const int sm = cur & 255;
+            const int r = q - (cur >> 8);
             if (q < T) {
                 const int m = cb + sm;
                 const int j = seg_jo[m] >> 8;

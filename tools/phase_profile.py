@@ -33,10 +33,12 @@ def main():
     ap.add_argument("--traffic", type=int, default=0)
     ap.add_argument("--density", type=float, default=0.5)
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--step-kernel", type=int, default=0, help="0 auto, 1 k_cars + k_lidar, 2 fused k_step")
     args = ap.parse_args()
     mev = pkgload.load()
     h = mev.Handle(num_envs=args.envs, num_agents=args.agents, lidar_rays=args.rays, use_team_reward=1,
                    traffic_flow=args.traffic, traffic_density=args.density)
+    h.set_step_kernel(args.step_kernel)
     rng = np.random.default_rng(0)
     acc = []
     for t in range(args.steps):
