@@ -1455,37 +1455,36 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // (k_step, 128 VGPRs); ILP = 1 in k_lidar, whose 64-VGPR budget would spill
     auto phase1 = [&](auto small) {
         for (int j = 0; j < nal; j += ILP) {
-            const bool two = ILP == 2 && j + 1 < nal;
-            const float4 aA = ag[j], aB = ag[two ? j + 1 : j];
+            float4 a[ILP];
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) a[u] = ag[j + u < nal ? j + u : j];
             for (int b0 = 0; b0 < R; b0 += WAVE) {
                 const int b = b0 + lane;
                 const bool vb = b < R;
                 const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : (vb ? src.rel(b) : 0.0f));
-                float2 dA, dB = make_float2(0.0f, 0.0f);
-                const int rA = setup(aA, rel_b, small, dA);
-                int rB = 0;
-                if constexpr (ILP == 2) rB = setup(aB, rel_b, small, dB);
-                if (vb) {
-                    dir[j * R + b] = dA;
-                    res[j * R + b] = rA >= 0 ? rA : -rA - 1;  // result, or the next probe to test
-                    if (two) {
-                        dir[(j + 1) * R + b] = dB;
-                        res[(j + 1) * R + b] = rB >= 0 ? rB : -rB - 1;
+                float2 d[ILP];
+                int r[ILP];
+#pragma unroll
+                for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rel_b, small, d[u]);
+#pragma unroll
+                for (int u = 0; u < ILP; ++u) {
+                    const bool in = j + u < nal;  // wave-uniform
+                    if (vb && in) {
+                        dir[(j + u) * R + b] = d[u];
+                        res[(j + u) * R + b] = r[u] >= 0 ? r[u] : -r[u] - 1;  // result, or the next probe to test
                     }
+                    const bool pend = vb && in && r[u] < 0;
+                    const unsigned long long m = ballot(pend);
+                    if (pend) queue[qn + lane_rank(m)] = (unsigned short)((j + u) * R + b);
+                    qn += __popcll(m);
                 }
-                const bool pA = vb && rA < 0, pB = vb && two && rB < 0;
-                const unsigned long long mA = ballot(pA), mB = ballot(pB);
-                const int nA = __popcll(mA);
-                if (pA) queue[qn + lane_rank(mA)] = (unsigned short)(j * R + b);
-                if (pB) queue[qn + nA + lane_rank(mB)] = (unsigned short)((j + 1) * R + b);
-                qn += nA + __popcll(mB);
             }
         }
     };
     // |heading| < 100 for every agent (always, unless set_state() planted a
     // wild heading): |h + rel| < 120, the range of the branch-free sincosf
     const bool hsmall = ballot(lane < nal && !(fabs_f(ag[lane < nal ? lane : 0].z) < 100.0f)) == 0ull;
-    if (ILP == 2 && hsmall) phase1(std::true_type{});  // k_lidar: one instantiation (64 VGPRs)
+    if (ILP > 1 && hsmall) phase1(std::true_type{});  // k_lidar: one instantiation (64 VGPRs)
     else phase1(std::false_type{});
     wave_lds_sync();
 #if defined(MEV_STAMPS_R)  // one pool per env: slot 4 = end of phase 1
@@ -1801,6 +1800,11 @@ __host__ __device__ inline StepLayout step_layout(const SimParams& p) {
     return L;
 }
 
+// agents per phase-1 pass in k_step (independent dependency chains interleaved)
+#ifndef MEV_PHASE1_ILP
+#define MEV_PHASE1_ILP 2
+#endif
+
 // Issue priorities of k_step's two parts (s_setprio; experiments: tools/kernel_time.py)
 #ifndef MEV_PRIO_CARS
 #define MEV_PRIO_CARS 1
@@ -1839,7 +1843,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Ou
     unsigned char* lbase = step_lds + sl.lidar;
     const int lane = threadIdx.x & (WAVE - 1);
     const int g0 = e * p.N;
-    lidar_body<TAB, 2>(p, out, LidarSrcLds{el, g0}, p.N, g0, p.N, lane, lbase, lay);
+    lidar_body<TAB, MEV_PHASE1_ILP>(p, out, LidarSrcLds{el, g0}, p.N, g0, p.N, lane, lbase, lay);
     if (MEV_FUSED_STAGED) {
         wave_lds_sync();
         fused_store<TAB>(p, out, e, el, reinterpret_cast<const int*>(lbase + lay.res), lane);
