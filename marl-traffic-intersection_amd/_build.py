@@ -46,6 +46,9 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # exact variants: k_step issue priorities of the car part / LiDAR part (product: 1 / 0)
                "prio00": ["-DMEV_PRIO_CARS=0", "-DMEV_PRIO_LIDAR=0"], "prio01": ["-DMEV_PRIO_CARS=0", "-DMEV_PRIO_LIDAR=1"],
                "prio20": ["-DMEV_PRIO_CARS=2", "-DMEV_PRIO_LIDAR=0"],
+               # timing-only: k_step stopped after the car part / LiDAR phase 1 / 2 / 3 (instruction budgets)
+               "stop1": ["-DMEV_EXP_STOP=1"], "stop2": ["-DMEV_EXP_STOP=2"], "stop3": ["-DMEV_EXP_STOP=3"],
+               "stop4": ["-DMEV_EXP_STOP=4"],
                # exact variant: k_step stages every output in LDS and writes whole rows at the end
                "staged": ["-DMEV_FUSED_STAGED=1"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it

@@ -98,6 +98,12 @@ __device__ inline int wave_scan_dpp(int v, Op op) {
     v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));  // row_bcast:31 -> rows 2, 3
     return v;
 }
+// a 64-bit value of lane l (wave-uniform result)
+__device__ inline unsigned long long readlane64(unsigned long long v, int l) {
+    return ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+           (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+}
+
 // one DPP lane move of a float (ctrl: quad_perm / row_half_mirror ...; every lane reads a valid lane)
 #define dpp_f(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xf, 0xf, false))
 
@@ -933,15 +939,16 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
         unsigned long long donem = ballot(in_env && (done_i || !alive_i));
         const unsigned long long npcm = ballot(colnpc_i);
         unsigned long long crash = 0ull;
-        const unsigned col_lo = (unsigned)col_i, col_hi = (unsigned)(col_i >> 32);
-        for (int a = 0; a < N; ++a) {
-            if ((donem >> a) & 1ull) continue;
-            const unsigned long long ca = ((unsigned long long)__builtin_amdgcn_readlane(col_hi, a) << 32) |
-                                          (unsigned)__builtin_amdgcn_readlane(col_lo, a);
-            const unsigned long long higher = (a == 63) ? 0ull : (~0ull << (a + 1));
-            const unsigned long long hits = ca & ~donem & higher;
-            if (hits) { donem |= hits | (1ull << a); crash |= hits | (1ull << a); }
-            if (TRAFFIC && ((npcm >> a) & 1ull)) { donem |= 1ull << a; crash |= 1ull << a; }
+        // (most steps have no car-car contact at all: the scan is skipped)
+        if (ballot(col_i != 0ull) != 0ull || npcm != 0ull) {
+            for (int a = 0; a < N; ++a) {
+                if ((donem >> a) & 1ull) continue;
+                const unsigned long long ca = readlane64(col_i, a);
+                const unsigned long long higher = (a == 63) ? 0ull : (~0ull << (a + 1));
+                const unsigned long long hits = ca & ~donem & higher;
+                if (hits) { donem |= hits | (1ull << a); crash |= hits | (1ull << a); }
+                if (TRAFFIC && ((npcm >> a) & 1ull)) { donem |= 1ull << a; crash |= 1ull << a; }
+            }
         }
         STAMPY(1);
         if ((crash >> i) & 1ull) { done_i = 1; st_i = ST_CRASH_CAR; }
@@ -1487,6 +1494,9 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (ILP > 1 && hsmall) phase1(std::true_type{});  // k_lidar: one instantiation (64 VGPRs)
     else phase1(std::false_type{});
     wave_lds_sync();
+#if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 2  // timing-only: stop after phase 1
+    if (Src::kBoxLds) return;
+#endif
 #if defined(MEV_STAMPS_R)  // one pool per env: slot 4 = end of phase 1
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 4] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1494,6 +1504,8 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // ---- phase 2: pooled road + screen march of the queued beams
     // (Lidar.cpp:31-48, first stop wins): LIDAR_NPR exact probes, then a jump
     // over the provably safe stretch after the last one
+    // (one beam per lane: measured, a second interleaved beam per lane doubles
+    // the per-iteration cost while the long beams still set the trip count)
     const float invR = 1.0f / (float)R;
     int next = qn < WAVE ? qn : WAVE;
     int slot = lane < qn ? (int)queue[lane] : -1;
@@ -1543,6 +1555,9 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (lane == 0 && a0 / G < p.E * 8) p.debug[a0 / G] = (unsigned long long)iters;
 #endif
     wave_lds_sync();
+#if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 3  // timing-only: stop after phase 2
+    if (Src::kBoxLds) return;
+#endif
 #if defined(MEV_STAMPS_R)  // one pool per env: slot 6 = end of phase 2
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1560,14 +1575,14 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     int4* seg_bx = reinterpret_cast<int4*>(base + lay.seg_bx);
     int* scr = reinterpret_cast<int*>(base + lay.scr);
     int M = 0;
-    for (int j = 0; j < nal; ++j) {  // 3a
-        const int g = __builtin_amdgcn_readfirstlane(__float_as_int(ag[j].w));
-#ifdef MEV_EXP_NOCARS
-        const unsigned long long c0 = 0, c1 = 0;
-#else
-        unsigned long long c0, c1;
-        src.cand(g, c0, c1);
+    // 3a: lane j < nal fetches agent j's candidate masks once; the loop then
+    // reads them with readlane instead of two dependent LDS round trips per agent
+    unsigned long long cl0 = 0ull, cl1 = 0ull;
+#ifndef MEV_EXP_NOCARS
+    if (lane < nal) src.cand(__float_as_int(ag[lane].w), cl0, cl1);
 #endif
+    for (int j = 0; j < nal; ++j) {
+        const unsigned long long c0 = readlane64(cl0, j), c1 = readlane64(cl1, j);
         const int n0 = __popcll(c0);
         if ((c0 >> lane) & 1ull) seg_jo[M + lane_rank(c0)] = (j << 8) | lane;
         if ((c1 >> lane) & 1ull) seg_jo[M + n0 + lane_rank(c1)] = (j << 8) | (lane + WAVE);
@@ -1701,6 +1716,9 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     wave_lds_sync();
 #if defined(MEV_STAMPS_R)
     if (lane == 0) p.debug[se_ * 8 + 5 + sp_] = __builtin_amdgcn_s_memrealtime();
+#endif
+#if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 4  // timing-only: stop after phase 3 (no LiDAR block writes)
+    if (Src::kBoxLds) return;
 #endif
     if (Src::kStaged) return;  // k_step: fused_store writes the block from res
     for (int j = 0; j < nal; ++j) {  // 3d: Lidar::normalized (:92-98)
@@ -1838,6 +1856,9 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Ou
     if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
     cars_body<TRAFFIC, true>(p, in, out, e, el, nl);
     wave_lds_sync();
+#if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 1  // timing-only: the car part alone
+    return;
+#endif
     if (MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
     const LidarLayout lay = lidar_layout(p.N, p.R, lidar_cand_max(p), false);
     unsigned char* lbase = step_lds + sl.lidar;

@@ -24,6 +24,10 @@ if [ "$what" = bench ] || [ "$what" = all ]; then
       python3 bench.py --no-kernel-events --no-cpu-baseline --steps 200 > $OUT/pmc_fetch.log 2>&1
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- \
       python3 bench.py --no-kernel-events --no-cpu-baseline --steps 200 > $OUT/pmc_write.log 2>&1
+  rm -rf $OUT/sq1
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU \
+      -d $OUT/sq1 -o run --output-format csv -- python3 bench.py --no-kernel-events --no-cpu-baseline --steps 200 > $OUT/sq1.log 2>&1
+  python tools/pmc_sq.py $OUT/sq1 > $OUT/sq_counters.txt
   find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
   cat $OUT/kernel_stats.csv | cut -c1-200
 fi
