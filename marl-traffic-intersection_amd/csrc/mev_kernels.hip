@@ -1525,9 +1525,13 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     };
     if (slot >= 0) load_beam(slot);
 #ifdef MEV_ITERS
-    int iters = 0;
+    int iters = 0, drained = -1, lanes_busy = 0;
 #endif
     while (ballot(slot >= 0) != 0ull) {
+#ifdef MEV_ITERS
+        lanes_busy += __popcll(ballot(slot >= 0));
+        if (drained < 0 && next >= qn) drained = iters;
+#endif
         // branch-free body: every lane evaluates its probes; idle lanes only skip the store
         const bool act = slot >= 0;
         float fx, fy;
@@ -1551,8 +1555,13 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             next += __popcll(fm);
         }
     }
-#ifdef MEV_ITERS
-    if (lane == 0 && a0 / G < p.E * 8) p.debug[a0 / G] = (unsigned long long)iters;
+#ifdef MEV_ITERS  // per pool: iterations, queued beams, iteration at which the queue ran dry, busy lane-iterations
+    if (lane == 0 && a0 / G < p.E) {
+        p.debug[(a0 / G) * 8 + 0] = (unsigned long long)iters;
+        p.debug[(a0 / G) * 8 + 1] = (unsigned long long)qn;
+        p.debug[(a0 / G) * 8 + 2] = (unsigned long long)(drained < 0 ? iters : drained);
+        p.debug[(a0 / G) * 8 + 3] = (unsigned long long)lanes_busy;
+    }
 #endif
     wave_lds_sync();
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 3  // timing-only: stop after phase 2
@@ -1802,8 +1811,16 @@ __device__ __forceinline__ void fused_store(const SimParams& p, const Outputs& o
     }
 }
 
+// Agents per LiDAR pool in k_step: the env's N agents in pools of at most 512
+// beams (all N in one pool at config 3; the staged variant needs one pool).
+__host__ __device__ inline int step_pool(const SimParams& p) {
+    if (MEV_FUSED_STAGED) return p.N;
+    const int g = 512 / (p.R > 0 ? p.R : 1);
+    return g < 1 ? 1 : (g < p.N ? g : p.N);
+}
+
 // LDS of one k_step wave: cars LDS, the staged heads [N][31], the beam offsets
-// [R], the env flags [8], then the LiDAR pool of the env's N agents.
+// [R], the env flags [8], then the LiDAR pool of step_pool(p) agents.
 struct StepLayout {
     int head, rel, envw, lidar, bytes;
 };
@@ -1813,7 +1830,7 @@ __host__ __device__ inline StepLayout step_layout(const SimParams& p) {
     L.head = off; off += MEV_FUSED_STAGED ? (int)lds_al((size_t)p.N * OBS_HEAD * 4) : 0;
     L.rel = off; off += (int)lds_al((size_t)p.R * 4);
     L.envw = off; off += 32;
-    L.lidar = off; off += lidar_layout(p.N, p.R, lidar_cand_max(p), false).bytes;
+    L.lidar = off; off += lidar_layout(step_pool(p), p.R, lidar_cand_max(p), false).bytes;
     L.bytes = off;
     return L;
 }
@@ -1860,11 +1877,16 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Ou
     return;
 #endif
     if (MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
-    const LidarLayout lay = lidar_layout(p.N, p.R, lidar_cand_max(p), false);
+    const int G = step_pool(p);
+    const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p), false);
     unsigned char* lbase = step_lds + sl.lidar;
     const int lane = threadIdx.x & (WAVE - 1);
     const int g0 = e * p.N;
-    lidar_body<TAB, MEV_PHASE1_ILP>(p, out, LidarSrcLds{el, g0}, p.N, g0, p.N, lane, lbase, lay);
+    for (int j0 = 0; j0 < p.N; j0 += G) {  // pools of G agents (one at config 3)
+        if (j0 > 0) wave_lds_sync();
+        const int na = p.N - j0 < G ? p.N - j0 : G;
+        lidar_body<TAB, MEV_PHASE1_ILP>(p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
+    }
     if (MEV_FUSED_STAGED) {
         wave_lds_sync();
         fused_store<TAB>(p, out, e, el, reinterpret_cast<const int*>(lbase + lay.res), lane);
@@ -1964,12 +1986,13 @@ static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Ou
     return e;
 }
 
-// k_step applies without traffic when the env's N*R beams form one pool of at
-// most 512 beams and its LDS fits a wave's share: at 4 waves per SIMD (128
-// VGPRs) a CU holds 16 waves, so a wave may take 160 KB / 16 = 10 KB.
+// k_step applies without traffic when its LDS (cars + one LiDAR pool of
+// step_pool(p) agents) fits a wave's share: at 4 waves per SIMD (128 VGPRs) a
+// CU holds 16 waves, so a wave may take 160 KB / 16 = 10 KB.
 static bool fused_fits(const SimParams& p) {
     if (p.traffic) return false;  // the NPC phase's LDS leaves no room for a LiDAR pool
-    return p.N * p.R <= 512 && step_layout(p).bytes <= 10 * 1024;
+    if (MEV_FUSED_STAGED && p.N * p.R > 512) return false;
+    return step_layout(p).bytes <= 10 * 1024;
 }
 
 int step_kernel_for(const SimParams& p) {

@@ -16,9 +16,9 @@ def _handle(mev, **kw):
     return mev.Handle(**cfg)
 
 
-def _warm_state(mev, steps=60, seed=0):
+def _warm_state(mev, steps=60, seed=0, **kw):
     """A diverse state: run random actions from reset."""
-    h = _handle(mev)
+    h = _handle(mev, **kw)
     rng = np.random.default_rng(seed)
     for _ in range(steps):
         h.step(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32))
@@ -45,15 +45,17 @@ def test_determinism_full_size(mev):
         assert np.array_equal(outs[0][1][k], outs[1][1][k]), k
 
 
-def test_fused_and_two_kernel_paths_agree_full_size(mev):
-    """The fused k_step (default at this size) and k_cars + k_lidar produce
-    identical outputs and state, step after step, with auto-reset on."""
-    st = _warm_state(mev, seed=6)
+@pytest.mark.parametrize("rays", [64, 128])
+def test_fused_and_two_kernel_paths_agree_full_size(mev, rays):
+    """The fused k_step (default at this size; at 128 beams it runs the env's
+    LiDAR as two pools of 4 agents) and k_cars + k_lidar produce identical
+    outputs and state, step after step, with auto-reset on."""
+    st = _warm_state(mev, seed=6, lidar_rays=rays)
     rng = np.random.default_rng(7)
     acts = rng.uniform(-1, 1, (16, E, N, 2)).astype(np.float32)
     hs = []
     for kernel in (1, 2):
-        h = _handle(mev, max_steps=70)  # some envs truncate and auto-reset inside the window
+        h = _handle(mev, max_steps=70, lidar_rays=rays)  # some envs truncate and auto-reset inside the window
         h.set_step_kernel(kernel)
         assert h.step_kernel() == kernel
         h.set_state(st)

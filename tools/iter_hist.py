@@ -1,4 +1,9 @@
-"""Diagnostic: per-wave road-march iteration counts (exp_iters build)."""
+"""Diagnostic: road-march (LiDAR phase 2) statistics per beam pool, exp_iters build.
+    python tools/iter_hist.py [--step-kernel 2]
+Per pool (k_step: one per env): wave iterations, queued beams after phase 1, the
+iteration at which the queue ran dry (after it only the tail of running beams
+remains) and the lane utilisation (busy lane-iterations / 64 x iterations)."""
+import argparse
 import os
 import sys
 
@@ -7,14 +12,34 @@ import numpy as np  # noqa: E402
 
 import pkgload  # noqa: E402
 
-mev = pkgload.load()
-mev._capi.VARIANT = "exp_iters"
-h = mev.Handle(num_envs=4096, num_agents=8, lidar_rays=64, use_team_reward=1)
-rng = np.random.default_rng(0)
-for t in range(300):
-    h.step(rng.uniform(-1, 1, (4096, 8, 2)).astype(np.float32), auto_reset=True)
-it = h.debug_stamps().reshape(-1).astype(np.int64)
-it = it[: 4096 * 8 // int(os.environ.get("MEV_LIDAR_G", "4"))]  # one entry per k_lidar wave
-print("wave iterations: mean %.2f median %d p90 %d p99 %d max %d" % (it.mean(), np.median(it), np.percentile(it, 90),
-                                                                   np.percentile(it, 99), it.max()))
-print(np.bincount(it)[:80])
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--step-kernel", type=int, default=2)
+    ap.add_argument("--envs", type=int, default=4096)
+    a = ap.parse_args()
+    mev = pkgload.load()
+    mev._capi.VARIANT = "exp_iters"
+    h = mev.Handle(num_envs=a.envs, num_agents=8, lidar_rays=64, use_team_reward=1)
+    h.set_step_kernel(a.step_kernel)
+    rng = np.random.default_rng(0)
+    for t in range(300):
+        h.step(rng.uniform(-1, 1, (a.envs, 8, 2)).astype(np.float32), auto_reset=True)
+    d = h.debug_stamps().reshape(a.envs, 8).astype(np.int64)
+    it, qn, dry, busy = d[:, 0], d[:, 1], d[:, 2], d[:, 3]
+    ok = it > 0
+
+    def stat(name, v):
+        print(f"  {name:28s} mean {v.mean():7.2f}  p10 {np.percentile(v, 10):6.1f}  p50 {np.percentile(v, 50):6.1f}"
+              f"  p90 {np.percentile(v, 90):6.1f}  max {v.max():6.1f}")
+
+    print(f"pools: {ok.sum()} of {a.envs}")
+    stat("iterations", it[ok])
+    stat("queued beams", qn[ok])
+    stat("iteration queue ran dry", dry[ok])
+    stat("tail iterations", (it - dry)[ok])
+    stat("lane utilisation %", 100.0 * busy[ok] / (64.0 * it[ok]))
+
+
+if __name__ == "__main__":
+    main()
