@@ -1730,13 +1730,32 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (Src::kBoxLds) return;
 #endif
     if (Src::kStaged) return;  // k_step: fused_store writes the block from res
-    for (int j = 0; j < nal; ++j) {  // 3d: Lidar::normalized (:92-98)
-        const int g = __float_as_int(ag[j].w);
-        float* row = out.obs + (size_t)g * p.D + OBS_HEAD;
-        for (int b = lane; b < p.lidar_slots; b += WAVE) {
-            const int r = res[j * R + b];
-            const float final_dist = (r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max;
-            row[b] = final_dist * p.lidar_inv;
+    // 3d: Lidar::normalized (:92-98), the LiDAR block of each alive agent's row
+    auto lidar_value = [&](int r) {
+        return ((r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max) * p.lidar_inv;
+    };
+    if (p.lidar_slots <= WAVE) {
+        // lane = beam: the agents' global indices come from one LDS read (readlane per
+        // row) and 8 rows' results are read before any is stored (one LDS wait per 8 rows)
+        const int gl = lane < nal ? __float_as_int(ag[lane].w) : 0;
+        const bool beam = lane < p.lidar_slots;
+        for (int j0 = 0; j0 < nal; j0 += 8) {
+            int rr[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) rr[u] = (j0 + u < nal && beam) ? res[(j0 + u) * R + lane] : 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (j0 + u < nal && beam) {
+                    const int g = __builtin_amdgcn_readlane(gl, j0 + u);
+                    out.obs[(size_t)g * p.D + OBS_HEAD + lane] = lidar_value(rr[u]);
+                }
+            }
+        }
+    } else {
+        for (int j = 0; j < nal; ++j) {
+            const int g = __float_as_int(ag[j].w);
+            float* row = out.obs + (size_t)g * p.D + OBS_HEAD;
+            for (int b = lane; b < p.lidar_slots; b += WAVE) row[b] = lidar_value(res[j * R + b]);
         }
     }
 }
