@@ -43,9 +43,12 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                # exact variants: probes per road-march step (product: 2)
                "npr1": ["-DMEV_LIDAR_NPR=1"], "npr3": ["-DMEV_LIDAR_NPR=3"],
-               # exact variants: k_step issue priorities of the car part / LiDAR part (product: 1 / 0)
-               "prio00": ["-DMEV_PRIO_CARS=0", "-DMEV_PRIO_LIDAR=0"], "prio01": ["-DMEV_PRIO_CARS=0", "-DMEV_PRIO_LIDAR=1"],
-               "prio20": ["-DMEV_PRIO_CARS=2", "-DMEV_PRIO_LIDAR=0"],
+               # exact variants: k_step issue priorities (product: cars 3, LiDAR phase 1 3 -> 2 after a
+               # quarter of its agents, phase 2 1, phase 3 0); prio10 = the earlier cars 1 / LiDAR 0
+               "prio10": ["-DMEV_PRIO_CARS=1", "-DMEV_PRIO_LIDAR=0", "-DMEV_PRIO_P1B=-1", "-DMEV_PRIO_P2=-1",
+                          "-DMEV_PRIO_P3=-1"],
+               "prio3210": ["-DMEV_PRIO_CARS=3", "-DMEV_PRIO_LIDAR=2", "-DMEV_PRIO_P1B=-1"],
+               "prio_half": ["-DMEV_PRIO_P1B_AT=2"],
                # timing-only: k_step stopped after the car part / LiDAR phase 1 / 2 / 3 (instruction budgets)
                "stop1": ["-DMEV_EXP_STOP=1"], "stop2": ["-DMEV_EXP_STOP=2"], "stop3": ["-DMEV_EXP_STOP=3"],
                "stop4": ["-DMEV_EXP_STOP=4"],

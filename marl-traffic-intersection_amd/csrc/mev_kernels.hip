@@ -63,6 +63,38 @@ constexpr int MAXN = 64;
 constexpr int MAXK = 64;
 constexpr int MAXOB = MAXN + MAXK;
 
+// k_step's issue priorities (s_setprio), falling as a wave's remaining work
+// shrinks: the four waves of a SIMD start together and the hardware otherwise
+// favours the oldest, so the wave with the most work left -- the one that sets
+// the SIMD's finish -- would be served last.  Cars and the first quarter of
+// LiDAR phase 1: 3, the rest of phase 1: 2, phase 2 (march): 1, phase 3 and the
+// block writes: 0 (measured +11 % over cars 1 / LiDAR 0).
+// -1 keeps the previous level.  The two-kernel path runs at the default.
+#ifndef MEV_PRIO_CARS
+#define MEV_PRIO_CARS 3
+#endif
+#ifndef MEV_PRIO_LIDAR
+#define MEV_PRIO_LIDAR 3
+#endif
+#ifndef MEV_PRIO_HEAD  // the car part's observation head
+#define MEV_PRIO_HEAD -1
+#endif
+#ifndef MEV_PRIO_P1B  // LiDAR phase 1 from MEV_PRIO_P1B_AT quarters of its agents on
+#define MEV_PRIO_P1B 2
+#endif
+#ifndef MEV_PRIO_P1B_AT
+#define MEV_PRIO_P1B_AT 1
+#endif
+#ifndef MEV_PRIO_P2
+#define MEV_PRIO_P2 1
+#endif
+#ifndef MEV_PRIO_P3
+#define MEV_PRIO_P3 0
+#endif
+#ifndef MEV_PRIO_P4  // the LiDAR block writes
+#define MEV_PRIO_P4 -1
+#endif
+
 // --------------------------------------------------------------- helpers ---
 // SoA field k of the ego / NPC blocks (one base pointer + stride, see EgoSoA)
 __device__ inline float* egof(const SimParams& p, int k) { return p.ego.x + p.ego.stride * k; }
@@ -1067,6 +1099,7 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
 
     STAMP(5);
     STAMPY(4);
+    if (FUSED && MEV_PRIO_HEAD >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_HEAD < 0 ? 0 : MEV_PRIO_HEAD);
     // ---- observation head (:418-520)
     const int C = N + (TRAFFIC ? ncnt : 0);
     if (C <= 8) {
@@ -1462,6 +1495,8 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // (k_step, 128 VGPRs); ILP = 1 in k_lidar, whose 64-VGPR budget would spill
     auto phase1 = [&](auto small) {
         for (int j = 0; j < nal; j += ILP) {
+            if (Src::kBoxLds && MEV_PRIO_P1B >= 0 && 4 * j >= MEV_PRIO_P1B_AT * nal)
+                __builtin_amdgcn_s_setprio(MEV_PRIO_P1B < 0 ? 0 : MEV_PRIO_P1B);
             float4 a[ILP];
 #pragma unroll
             for (int u = 0; u < ILP; ++u) a[u] = ag[j + u < nal ? j + u : j];
@@ -1501,6 +1536,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 4] = __builtin_amdgcn_s_memrealtime();
 #endif
 
+    if (Src::kBoxLds && MEV_PRIO_P2 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P2 < 0 ? 0 : MEV_PRIO_P2);
     // ---- phase 2: pooled road + screen march of the queued beams
     // (Lidar.cpp:31-48, first stop wins): LIDAR_NPR exact probes, then a jump
     // over the provably safe stretch after the last one
@@ -1571,6 +1607,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
 
+    if (Src::kBoxLds && MEV_PRIO_P3 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P3 < 0 ? 0 : MEV_PRIO_P3);
     // ---- phase 3: cars (Lidar.cpp:50-80) as a list of (agent, box, beam) pairs.
     // A box can only stop the beams whose ray enters its slab box, i.e. the
     // beams inside the angular span of its real slab box seen from the agent:
@@ -1651,6 +1688,9 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         seg_rg[m] = rg;
     }
     wave_lds_sync();
+#ifdef MEV_ITERS
+    int p3_pairs = 0, p3_chunks = 0, p3_kk = 0;
+#endif
     // 3c: the pairs of all the group's agents packed into the 64 lanes
     for (int cb = 0; cb < M; cb += WAVE) {
         const int nseg = M - cb < WAVE ? M - cb : WAVE;
@@ -1659,7 +1699,13 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const int excl = incl - cnt;
         const int T = __builtin_amdgcn_readlane(incl, WAVE - 1);
         int carry = 0;  // (start << 8 | segment) of the segment running into this chunk
+#ifdef MEV_ITERS
+        p3_pairs += T;
+#endif
         for (int q0 = 0; q0 < T; q0 += WAVE) {
+#ifdef MEV_ITERS
+            ++p3_chunks;
+#endif
             const int q = q0 + lane;
             // segment of pair q: the last m with excl[m] <= q.  Each segment that
             // starts in this chunk writes (start << 8 | m) + 1 to the LDS slot of
@@ -1708,6 +1754,20 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 kb = kb < kr - 1 ? kb : kr - 1;
                 if (lo > hi) kb = 0;
                 // ... resolved by exact probes in march order
+#ifdef MEV_ITERS
+                {
+                    int tk = 0;
+                    for (int kk = ka; kk <= kb; ++kk) {
+                        ++tk;
+                        const float d = (float)kk * p.lidar_step;
+                        const int px = (int)(a.x + dd.x * d), py = (int)(a.y + dd.y * d);
+                        if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) break;
+                    }
+                    int mx = tk;
+                    for (int o = 32; o >= 1; o >>= 1) { const int t2 = __shfl_xor(mx, o); mx = mx > t2 ? mx : t2; }
+                    p3_kk += mx;
+                }
+#endif
                 for (int kk = ka; kk <= kb; ++kk) {
                     // a runtime table test here, not march_dist<TAB>: measured 4 us per
                     // step faster in k_step, and without it k_lidar's 64-VGPR
@@ -1723,6 +1783,14 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         }
     }
     wave_lds_sync();
+#ifdef MEV_ITERS  // per pool: segments, pairs, 64-pair chunks, probe-loop trips (wave max per chunk)
+    if (lane == 0 && a0 / G < p.E) {
+        p.debug[(a0 / G) * 8 + 4] = (unsigned long long)M;
+        p.debug[(a0 / G) * 8 + 5] = (unsigned long long)p3_pairs;
+        p.debug[(a0 / G) * 8 + 6] = (unsigned long long)p3_chunks;
+        p.debug[(a0 / G) * 8 + 7] = (unsigned long long)p3_kk;
+    }
+#endif
 #if defined(MEV_STAMPS_R)
     if (lane == 0) p.debug[se_ * 8 + 5 + sp_] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1730,6 +1798,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (Src::kBoxLds) return;
 #endif
     if (Src::kStaged) return;  // k_step: fused_store writes the block from res
+    if (Src::kBoxLds && MEV_PRIO_P4 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P4 < 0 ? 0 : MEV_PRIO_P4);
     // 3d: Lidar::normalized (:92-98), the LiDAR block of each alive agent's row
     auto lidar_value = [&](int r) {
         return ((r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max) * p.lidar_inv;
@@ -1859,13 +1928,6 @@ __host__ __device__ inline StepLayout step_layout(const SimParams& p) {
 #define MEV_PHASE1_ILP 2
 #endif
 
-// Issue priorities of k_step's two parts (s_setprio; experiments: tools/kernel_time.py)
-#ifndef MEV_PRIO_CARS
-#define MEV_PRIO_CARS 1
-#endif
-#ifndef MEV_PRIO_LIDAR
-#define MEV_PRIO_LIDAR 0
-#endif
 
 // The whole step in one wave per env: cars_body, then the LiDAR of the env's
 // N agents as one pool, from the same wave's LDS, then every output written
@@ -1895,7 +1957,6 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Ou
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 1  // timing-only: the car part alone
     return;
 #endif
-    if (MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
     const int G = step_pool(p);
     const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p), false);
     unsigned char* lbase = step_lds + sl.lidar;
@@ -1903,6 +1964,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Ou
     const int g0 = e * p.N;
     for (int j0 = 0; j0 < p.N; j0 += G) {  // pools of G agents (one at config 3)
         if (j0 > 0) wave_lds_sync();
+        if (j0 > 0 || MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);  // each pool
         const int na = p.N - j0 < G ? p.N - j0 : G;
         lidar_body<TAB, MEV_PHASE1_ILP>(p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
     }
@@ -1910,6 +1972,14 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Ou
         wave_lds_sync();
         fused_store<TAB>(p, out, e, el, reinterpret_cast<const int*>(lbase + lay.res), lane);
     }
+#if defined(MEV_STAMPS_R)  // slot 7: end of the wave (low 40 bits) | where it ran (HW_ID[15:0], XCC_ID[2:0]) << 40
+    {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime() & ((1ull << 40) - 1);
+        const unsigned hw = __builtin_amdgcn_s_getreg((15 << 11) | 4) & 0xffffu;
+        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
+        if (lane == 0) p.debug[e * 8 + 7] = t | ((unsigned long long)(hw | (xcc << 16)) << 40);
+    }
+#endif
 }
 
 // ------------------------------------------------- reset / re-observe ---

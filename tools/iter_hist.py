@@ -39,6 +39,11 @@ def main():
     stat("iteration queue ran dry", dry[ok])
     stat("tail iterations", (it - dry)[ok])
     stat("lane utilisation %", 100.0 * busy[ok] / (64.0 * it[ok]))
+    print("phase 3 (car pairs):")
+    stat("segments (agent, box)", d[ok, 4])
+    stat("pairs (beam, box)", d[ok, 5])
+    stat("64-pair chunks", d[ok, 6])
+    stat("probe-loop trips", d[ok, 7])
 
 
 if __name__ == "__main__":
