@@ -69,7 +69,7 @@ constexpr int MAXOB = MAXN + MAXK;
 // the SIMD's finish -- would be served last.  Cars and the first quarter of
 // LiDAR phase 1: 3, the rest of phase 1: 2, phase 2 (march): 1, phase 3 and the
 // block writes: 0 (measured +11 % over cars 1 / LiDAR 0).
-// -1 keeps the previous level.  The two-kernel path runs at the default.
+// -1 keeps the previous level.
 #ifndef MEV_PRIO_CARS
 #define MEV_PRIO_CARS 3
 #endif
@@ -93,6 +93,9 @@ constexpr int MAXOB = MAXN + MAXK;
 #endif
 #ifndef MEV_PRIO_P4  // the LiDAR block writes
 #define MEV_PRIO_P4 -1
+#endif
+#ifndef MEV_PRIO_HBM  // the LiDAR phases' schedule in k_lidar too (two-kernel path: 54.4 -> 50.7 us/step)
+#define MEV_PRIO_HBM 1
 #endif
 
 // --------------------------------------------------------------- helpers ---
@@ -1495,7 +1498,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // (k_step, 128 VGPRs); ILP = 1 in k_lidar, whose 64-VGPR budget would spill
     auto phase1 = [&](auto small) {
         for (int j = 0; j < nal; j += ILP) {
-            if (Src::kBoxLds && MEV_PRIO_P1B >= 0 && 4 * j >= MEV_PRIO_P1B_AT * nal)
+            if ((Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P1B >= 0 && 4 * j >= MEV_PRIO_P1B_AT * nal)
                 __builtin_amdgcn_s_setprio(MEV_PRIO_P1B < 0 ? 0 : MEV_PRIO_P1B);
             float4 a[ILP];
 #pragma unroll
@@ -1536,7 +1539,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 4] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    if (Src::kBoxLds && MEV_PRIO_P2 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P2 < 0 ? 0 : MEV_PRIO_P2);
+    if ((Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P2 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P2 < 0 ? 0 : MEV_PRIO_P2);
     // ---- phase 2: pooled road + screen march of the queued beams
     // (Lidar.cpp:31-48, first stop wins): LIDAR_NPR exact probes, then a jump
     // over the provably safe stretch after the last one
@@ -1607,7 +1610,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    if (Src::kBoxLds && MEV_PRIO_P3 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P3 < 0 ? 0 : MEV_PRIO_P3);
+    if ((Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P3 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P3 < 0 ? 0 : MEV_PRIO_P3);
     // ---- phase 3: cars (Lidar.cpp:50-80) as a list of (agent, box, beam) pairs.
     // A box can only stop the beams whose ray enters its slab box, i.e. the
     // beams inside the angular span of its real slab box seen from the agent:
@@ -1798,7 +1801,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (Src::kBoxLds) return;
 #endif
     if (Src::kStaged) return;  // k_step: fused_store writes the block from res
-    if (Src::kBoxLds && MEV_PRIO_P4 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P4 < 0 ? 0 : MEV_PRIO_P4);
+    if ((Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P4 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P4 < 0 ? 0 : MEV_PRIO_P4);
     // 3d: Lidar::normalized (:92-98), the LiDAR block of each alive agent's row
     auto lidar_value = [&](int r) {
         return ((r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max) * p.lidar_inv;
@@ -1838,6 +1841,7 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     const int a0 = __builtin_amdgcn_readfirstlane(a_begin + (int)(blockIdx.x * (blockDim.x / WAVE) + wv) * G);
     if (a0 >= a_end) return;  // wave-uniform exit: the kernel has no block-level barrier
     const int na = a_end - a0 < G ? a_end - a0 : G;
+    if (MEV_PRIO_HBM) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
     const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p));
     lidar_body<TAB, 1>(p, out, LidarSrcHbm{p}, G, a0, na, lane, lds_raw + (size_t)wv * (size_t)lay.bytes, lay);
 }

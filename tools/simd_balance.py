@@ -34,7 +34,7 @@ def main():
     h = mev.Handle(num_envs=a.envs, num_agents=8, lidar_rays=64, use_team_reward=1)
     h.set_step_kernel(2)
     rng = np.random.default_rng(0)
-    ph, spans, fin, life, simd_sum, simd_max, simd_mean, nw, first_end = [], [], [], [], [], [], [], Counter(), []
+    slots, entries, ph, spans, fin, life, simd_sum, simd_max, simd_mean, nw, first_end = [], [], [], [], [], [], [], [], [], Counter(), []
     for t in range(a.steps):
         h.step(rng.uniform(-1, 1, (a.envs, 8, 2)).astype(np.float32), auto_reset=True)
         if t < a.steps // 2:
@@ -49,6 +49,8 @@ def main():
         lt = (t_out - t_in) / 100.0
         life.append(lt)
         first_end.append((t_out.min() - t0) / 100.0)
+        slots.append(where & 0xF)
+        entries.append((t_in - t0) / 100.0)
         tt = (r.astype(np.int64) & M40)
         tt[:, 7] = t_out
         ph.append(np.stack([(tt[:, j] - tt[:, i]) / 100.0 for i, j in PHASES], 1))
@@ -75,6 +77,12 @@ def main():
     print("  per-wave phase time: all p50 | mean of the 10 % shortest waves | of the 10 % longest")
     for k, n in enumerate(PH_NAMES):
         print(f"    {n:22s} {np.percentile(P[:, k], 50):7.2f} | {P[lo, k].mean():7.2f} | {P[hi, k].mean():7.2f}")
+    S = np.concatenate(slots)
+    E = np.concatenate(entries)
+    print("  by wave slot on the SIMD (HW_ID wave_id): slot: waves, mean entry, mean lifetime, mean end")
+    for k in np.unique(S):
+        m = S == k
+        print(f"    {k:2d}: {m.sum():7d} {E[m].mean():7.2f} {L[m].mean():7.2f} {(E[m] + L[m]).mean():7.2f}")
     c = np.corrcoef(simd_sum, fin)[0, 1]
     print(f"  corr(SIMD sum of lifetimes, SIMD finish) = {c:.3f}")
 
