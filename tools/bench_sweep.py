@@ -2,7 +2,7 @@
 contract and measures config 3).  Same method as bench.py: actions resident
 in HBM, outputs to HBM, auto-reset, warm-up then timed steps; per-kernel
 device time from the library's events (every 4th step).
-    python tools/bench_sweep.py [--steps 500] [--out profiles/r1_sweep.json]"""
+    python tools/bench_sweep.py [--steps 500] [--only cfg4] [--out profiles/r1_sweep.json]"""
 import argparse
 import json
 import os
@@ -66,9 +66,12 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default=None, help="comma-separated config names (e.g. cfg4)")
     a = ap.parse_args()
     res = []
     for cfg in CONFIGS:
+        if a.only and cfg["name"] not in a.only.split(","):
+            continue
         r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup)
         print(json.dumps(r), flush=True)
         res.append(r)
