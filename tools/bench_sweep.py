@@ -24,7 +24,7 @@ CONFIGS = [
 ]
 
 
-def run(cfg, steps, warmup):
+def run(cfg, steps, warmup, step_kernel=0):
     import torch
     import pkgload
     mev = pkgload.load()
@@ -33,6 +33,8 @@ def run(cfg, steps, warmup):
     h = mev.Handle(num_envs=E, num_agents=N, lidar_rays=R, obs_dim=cfg.get("D", 0),
                    use_team_reward=cfg.get("team", 0), traffic_flow=cfg.get("traffic", 0), traffic_density=0.5,
                    max_npcs=32)
+    if step_kernel:
+        h.set_step_kernel(step_kernel)
     st = torch.cuda.Stream(dev)
     torch.cuda.set_stream(st)
     h.set_stream(st.cuda_stream)
@@ -67,12 +69,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="comma-separated config names (e.g. cfg4)")
+    ap.add_argument("--step-kernel", type=int, default=0, help="0 auto, 1 k_cars + k_lidar, 2 fused k_step")
     a = ap.parse_args()
     res = []
     for cfg in CONFIGS:
         if a.only and cfg["name"] not in a.only.split(","):
             continue
-        r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup)
+        r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup, a.step_kernel)
         print(json.dumps(r), flush=True)
         res.append(r)
     if a.out:
