@@ -6,27 +6,32 @@ One "step" = IntersectionEnv::step + get_observations for all of the GPU's
 4096 envs: one launch of the fused k_step kernel (one wave per env: physics,
 status, collisions, rewards, respawn, observation head, then the 64-beam LiDAR
 of the env's 8 agents as one pooled beam queue, all from the wave's LDS), with
-the actions already resident in HBM (pre-generated
-uniform [-1, 1) f32) and obs [E, 8, 95] / reward / done / status /
-terminated / truncated written to HBM.
+the actions already resident in HBM (pre-generated uniform [-1, 1) f32) and
+obs [E, 8, 95] / reward / done / status / terminated / truncated written to HBM.
 
---gpus N > 1 (one process per GPU, torchrun): every rank steps its own 4096
-envs (weak scaling: envs are independent, so the step has no data-path
-collective; a barrier and a max-over-ranks reduction bracket the timed
-region).  --gather adds the optional output collection of sharding.py: each
-step's packed outputs gathered to rank 0 with one RCCL gather over xGMI,
-overlapped with the next step (double buffered).
+--gpus N > 1: one process per GPU.  Run directly, bench.py starts the N rank
+processes itself (children, before any GPU call); under torchrun it reads
+RANK / LOCAL_RANK / WORLD_SIZE.  Every rank steps its own 4096 envs (weak
+scaling: envs are independent, so the step has no data-path collective; a
+barrier and a max-over-ranks reduction bracket the timed region): "value".
+A second timed phase ("gather_to_root") repeats the steps with the
+north star's per-step RCCL gather of every rank's packed outputs to rank 0,
+issued from the C ABI (MEV_GATHER_TO_ROOT) on a communication stream that
+overlaps the next step; --no-gather skips it.
 
 Prints ONE JSON line on rank 0, including "roofline" for the dominant kernel
-(k_step, the only kernel of a step; device durations from HIP events the
-library records on its stream around it during the timed region) and "cpu_baseline" (the
-reference's own C++ simulator, compiled from its sources, on this host).
+(k_step, the only kernel of a step; HBM fraction from HIP events on its stream,
+VALU-issue fraction from the committed SQ counter pass) and "cpu_baseline" (the
+pinned C restatement on every host core, with the reference's survey-container
+numbers quoted beside it).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -56,29 +61,151 @@ def cars_bytes_per_agent_step(rays: int) -> int:
     return 8 + 80 + 4 * 31 + 4 + 2
 
 
-def cpu_baseline(seconds_budget: float = 20.0):
-    """The reference's C++ simulator (oracle/_ref: its unmodified sources compiled
-    with g++ -O2 by oracle/build_ref.sh) on this host's cores; falls back to the
-    C restatement (oracle/marl_oracle.c, single thread) when _ref is absent."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+# The reference's own C++ simulator timed in the survey container (8 vCPU Xeon, env.py
+# driver, one env per process): it cannot run on the GPU box, which
+# receives only this repository.  Quoted beside the live port timing.
+REFERENCE_SURVEY_CPU = {
+    "value_1_process": 6668, "value_8_processes": 37362, "unit": "agent-steps/s", "cores": 8,
+    "host": "survey container, Intel Xeon (family 6, model 0xCF), 8 vCPUs",
+    "config": "reference cpp/ (g++ -O2) through env.py, 8 agents, team reward, 64 beams",
+    "source": "BASELINE.md (measured during the survey, not published by the reference)",
+}
+
+
+def host_cores() -> int:
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU quota if one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     try:
-        import refharness
-    except Exception:
-        refharness = None
-    threads = min(16, os.cpu_count() or 1)
-    if refharness is not None and refharness.available():
-        # ~1 ms per 8-agent env-step per core => steps sized for ~seconds_budget CPU-seconds in total
-        steps = max(50, int(seconds_budget / threads / 1.1e-3))
-        v = refharness.bench(N_AGENTS, RAYS, True, False, 0.5, 1, steps, threads, 0)
-        return {"value": round(v, 1), "unit": "agent-steps/s", "cores": threads, "kind": "reference",
-                "sample": f"reference cpp/ simulator (unmodified sources, g++ -O2), {threads} threads x 1 env x "
-                          f"{steps} steps, 8 agents, 64 beams, team reward, uniform random actions, auto-reset"}
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_baseline(seconds_budget: float = 20.0):
+    """The pinned C restatement of the step (oracle/marl_oracle.c, bit-exact against the
+    reference's golden vectors; test infrastructure used here only as the baseline), one
+    thread per host core on every core this process may use, each thread its own env
+    (the ctypes call releases the GIL, so the threads run in parallel)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    steps = int(seconds_budget / 1.2e-3)
-    v = oracle.bench(N_AGENTS, RAYS, True, steps, 0)
-    return {"value": round(v, 1), "unit": "agent-steps/s", "cores": 1, "kind": "port",
-            "sample": f"C restatement (oracle/marl_oracle.c, gcc -O2), 1 thread x 1 env x {steps} steps, 8 agents, "
-                      f"64 beams, team reward, uniform random actions, auto-reset"}
+
+    oracle.lib()
+    threads = host_cores()
+    # ~1.2 ms per 8-agent env-step on one core: ~seconds_budget CPU-seconds in total
+    steps = max(100, int(seconds_budget / threads / 1.2e-3))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda t: oracle.bench(N_AGENTS, RAYS, True, steps, t), range(threads)))
+    wall = time.perf_counter() - t0
+    v = threads * steps * N_AGENTS / wall
+    return {"value": round(v, 1), "unit": "agent-steps/s", "cores": threads, "kind": "port",
+            "sample": f"C restatement of the step (oracle/marl_oracle.c, gcc -O2, bit-exact vs the reference "
+                      f"goldens), {threads} threads (every host core available to this process) x 1 env x {steps} "
+                      f"steps each, 8 agents, 64 beams, team reward, uniform random actions, auto-reset; "
+                      f"wall {wall:.1f} s",
+            "reference_survey": REFERENCE_SURVEY_CPU}
+
+
+def dist_table_needed(max_dist: float = 250.0, step: float = 4.0) -> bool:
+    """Whether the handle reads accumulated probe distances (k_step<_, true>): the float sum
+    dist += step of Lidar.cpp:33 differs from k*step (mirrors mev_create)."""
+    import numpy as np
+    d, k = np.float32(0.0), 0
+    while d < np.float32(max_dist):
+        if d != np.float32(k) * np.float32(step):
+            return True
+        d = np.float32(d + np.float32(step))
+        k += 1
+    return False
+
+
+VALU_PEAK_G = 1024 * 2.4e9 / 2 / 1e9  # wave64 VALU instructions/s: 1024 SIMD-32 x 2.4 GHz / 2 cycles
+
+
+def valu_roofline(kernel_ms: float, envs: int):
+    """VALU issue fraction of k_step: SQ_INSTS_VALU per launch (committed rocprofv3 pass,
+    profiles/valu_counters.json) / the live kernel time, against 1024 SIMDs issuing one wave64
+    VALU instruction per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md, Wave scheduling)."""
+    f = os.path.join(ROOT, "profiles", "valu_counters.json")
+    if not os.path.exists(f):
+        return None
+    pm = json.load(open(f))
+    k = pm.get("k_step")
+    if not k or pm.get("envs") != envs or pm.get("agents") != N_AGENTS or pm.get("rays") != RAYS:
+        return None
+    inst = float(k["SQ_INSTS_VALU_per_launch"])
+    achieved = inst / (kernel_ms * 1e-3) / 1e9
+    return {"achieved": round(achieved, 2), "peak": VALU_PEAK_G, "unit": "G wave-instr/s",
+            "frac": round(achieved / VALU_PEAK_G, 4), "SQ_INSTS_VALU_per_launch": inst,
+            "source": "profiles/valu_counters.json (rocprofv3 --pmc pass of this bench) / live kernel_ms"}
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int) -> int:
+    """--gpus N without a launcher: start N rank processes of this script (one per GPU) and
+    supervise them.  No GPU call happens in this process; the children are started, not
+    exec'd.  If a rank fails, the others are stopped (by PID) and its exit code returned."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for pr in list(live):
+            code = pr.poll()
+            if code is None:
+                continue
+            live.remove(pr)
+            if code != 0 and rc == 0:
+                rc = code
+                for other in live:
+                    other.kill()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args):
+    """The rank-side control plane of main() without a GPU (tests/test_bench_launcher.py)."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if os.environ.get("MEV_DRYRUN_FAIL_RANK") == str(rank):
+        sys.exit(3)  # test hook: a rank that dies before the rendezvous (the launcher must stop the rest)
+    if world > 1:
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("mev_comm_id", bytes(range(128)))  # stands in for mev_comm_unique_id()
+        uid = bytes(store.get("mev_comm_id"))
+        assert uid == bytes(range(128))
+        dist.barrier()
+    t = torch.tensor([float(rank + 1), float(os.getpid())], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "max_over_ranks": t[0].item(),
+                          "steps": args.steps, "warmup": args.warmup}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
@@ -87,39 +214,62 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--envs", type=int, default=E_PER_GPU, help="envs per GPU")
-    ap.add_argument("--gather", action="store_true",
-                    help="also gather every step's packed outputs to rank 0 (one RCCL gather over xGMI)")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="skip the second timed phase (every step's outputs gathered to rank 0 over RCCL)")
+    ap.add_argument("--gather-timeout", type=float, default=120.0, help="seconds before a stuck gather is aborted")
     ap.add_argument("--no-kernel-events", action="store_true", help="do not record per-kernel HIP events")
     ap.add_argument("--event-every", type=int, default=50, help="record the per-kernel events on every n-th step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--step-kernel", type=int, default=0,
                     help="0 automatic (fused k_step at this size), 1 k_cars + k_lidar, 2 fused")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank plumbing: launcher, gloo control plane, RCCL-id "
+                         "exchange through the store, max over ranks; no GPU work, no metric")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args.gpus))  # one child process per GPU; this process never touches the GPU
+    if args.dry_run:
+        return dry_run(args)
 
     import torch
     import pkgload
 
     mev = pkgload.load()
-    from marl_traffic_intersection_amd import sharding
+    from marl_traffic_intersection_amd import _capi
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
     torch.cuda.set_device(local_rank)
     if world > 1:
+        # control plane only (barriers, max over ranks, the RCCL id): gloo on the host; the
+        # data-path collective is the library's own RCCL gather (mev_comm_init)
+        import datetime
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(60.0, args.gather_timeout + 60.0)))
     dev = torch.device("cuda", local_rank)
     E, N, D = args.envs, N_AGENTS, OBS_DIM
     K, W = args.steps, args.warmup
 
+    def max_over_ranks(vals):
+        if dist is None:
+            return vals
+        t = torch.tensor(vals, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(x) for x in t.tolist()]
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
     env = mev.Handle(num_envs=E, num_agents=N, lidar_rays=RAYS, use_team_reward=1, respawn_enabled=1,
                      max_steps=2000, seed=rank, device=local_rank)
     env.set_step_kernel(args.step_kernel)
-    stream = torch.cuda.Stream(dev)  # the env kernels, the events and the gather are all ordered on it
+    stream = torch.cuda.Stream(dev)  # the env kernels and the events are all ordered on it
     torch.cuda.set_stream(stream)
     env.set_stream(stream.cuda_stream)
 
@@ -127,44 +277,27 @@ def main():
     g.manual_seed(1234 + rank)
     actions = torch.rand((W + K, E, N, 2), device=dev, generator=g, dtype=torch.float32) * 2.0 - 1.0
 
-    layout = sharding.PackedOutputs(E, N, D)  # every rank steps E envs: the gather needs no padding
-    bufs = [torch.zeros(layout.nbytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-    ptrs = [layout.pointers(b.data_ptr()) for b in bufs]
-    gather_on = world > 1 and args.gather
-    stacked = torch.empty((world, layout.nbytes), dtype=torch.uint8, device=dev) if gather_on and rank == 0 else None
-    works = [None, None]
+    # ---- phase 1 (the metric): every rank steps its own envs, outputs stay in its HBM
+    outs = [{k: torch.zeros_like(torch.as_tensor(v), device=dev) for k, v in env.alloc_outputs().items()}
+            for _ in range(2)]
     env.reset(device=True)
 
     def step(t):
-        slot = t & 1
-        if works[slot] is not None:
-            works[slot].wait()  # stream-ordered: the gather reading this buffer is done
-            works[slot] = None
-        env.step(actions[t].data_ptr(), 1.0 / 60.0, out=ptrs[slot], auto_reset=True, device=True)
-        if gather_on:
-            works[slot] = sharding.gather_to_root(bufs[slot], stacked, async_op=True)
+        env.step(actions[t].data_ptr(), 1.0 / 60.0, out=outs[t & 1], auto_reset=True, device=True)
 
     for t in range(W):
         step(t)
     torch.cuda.synchronize(dev)
     if not args.no_kernel_events:
         env.kernel_timing(args.event_every)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
     for k in range(K):
         step(W + k)
     ev1.record(stream)
-    for w in works:
-        if w is not None:
-            w.wait()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    barrier()
     elapsed = time.perf_counter() - t0
     stream_ms = ev0.elapsed_time(ev1) / K
     cars_ms = lidar_ms = None
@@ -173,16 +306,72 @@ def main():
         c_sum, l_sum, n_steps = env.kernel_times()
         assert n_steps == (K + args.event_every - 1) // args.event_every, (n_steps, K)
         cars_ms, lidar_ms = c_sum / n_steps, l_sum / n_steps
-    if dist is not None:
-        vals = torch.tensor([elapsed, cars_ms or 0.0, lidar_ms or 0.0, stream_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
-        elapsed, c_, l_, stream_ms = (float(x) for x in vals.tolist())
-        if cars_ms is not None:
-            cars_ms, lidar_ms = c_, l_
-
+        env.kernel_timing(0)
+    elapsed, c_, l_, stream_ms = max_over_ranks([elapsed, cars_ms or 0.0, lidar_ms or 0.0, stream_ms])
+    if cars_ms is not None:
+        cars_ms, lidar_ms = c_, l_
     # sanity: outputs are finite and the sim advanced
-    last = layout.unpack(bufs[(W + K - 1) & 1])
+    last = outs[(W + K - 1) & 1]
     assert torch.isfinite(last["obs"]).all().item(), "non-finite observations"
+
+    # ---- phase 2: the same steps with every step's outputs gathered to rank 0 (RCCL, xGMI)
+    gather = None
+    if not args.no_gather:
+        gather = {}
+        try:
+            if world > 1:
+                store = dist.distributed_c10d._get_default_store()
+                if rank == 0:
+                    store.set("mev_comm_id", _capi.comm_unique_id())
+                uid = bytes(store.get("mev_comm_id"))
+            else:
+                uid = _capi.comm_unique_id()
+            env.comm_init(uid, world, rank, root=0, slots=E)
+            env.reset(device=True)
+            for t in range(W):
+                env.step(actions[t].data_ptr(), 1.0 / 60.0, auto_reset=True, device=True, gather=True)
+            env.gather_wait(int(args.gather_timeout * 1000))
+            ok = 1.0
+        except Exception as exc:  # reported in the line; never lose the phase-1 result
+            gather["error"] = f"rank {rank}: {exc}"[:300]
+            ok = 0.0
+        if dist is not None:
+            t = torch.tensor([ok], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = float(t.item())
+        if ok > 0:
+            barrier()
+            t0 = time.perf_counter()
+            try:
+                for k in range(K):
+                    env.step(actions[W + k].data_ptr(), 1.0 / 60.0, auto_reset=True, device=True, gather=True)
+                env.gather_wait(int(args.gather_timeout * 1000))
+                ok = 1.0
+            except Exception as exc:
+                gather["error"] = f"rank {rank}: {exc}"[:300]
+                ok = 0.0
+            torch.cuda.synchronize(dev)
+            g_elapsed = time.perf_counter() - t0
+            if dist is not None:
+                dist.barrier()
+            g_elapsed, bad = max_over_ranks([g_elapsed, 1.0 - ok])
+            if bad == 0.0:
+                per = _capi.packed_layout(E, N, D)[1]  # bytes per rank per step
+                gather.update({
+                    "value": round(world * E * N * K / g_elapsed, 1), "unit": "agent-steps/s",
+                    "ms_per_step": round(g_elapsed / K * 1e3, 5), "bytes_per_rank_per_step": per,
+                    "root_ingress_GBs": round(per * (world - 1) / (g_elapsed / K) / 1e9, 2),
+                    "what": "phase 1's steps with every step's packed outputs (obs|reward|done|status|"
+                            "terminated|truncated) gathered to rank 0: one grouped ncclSend/ncclRecv per step "
+                            "from the C ABI (MEV_GATHER_TO_ROOT), on a communication stream overlapping the next step"})
+                if rank == 0:
+                    ptr, per_rank, w = env.gather_result()
+                    torch.cuda.synchronize(dev)
+                    gather["verified"] = "gather buffer present" if ptr else "missing"
+            elif "error" not in gather:
+                gather["error"] = "another rank failed in the gather phase"
+        elif "error" not in gather:
+            gather["error"] = "another rank failed to set up the gather"
 
     if rank == 0:
         total_agent_steps = world * E * N * K
@@ -204,12 +393,15 @@ def main():
             # in profiles/ is the same quantity without the gap)
             pb = algorithmic_bytes_per_agent_step(RAYS) * E * N
             achieved = pb / (stream_ms * 1e-3) / 1e9
+            kname = f"mev::k_step<false, {'true' if dist_table_needed() else 'false'}>"
             roofline = {
                 "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic_of.get("k_step"),
-                "kernel": "mev::k_step<false, false>", "kernel_ms": round(stream_ms, 5),
+                "kernel": kname, "kernel_ms": round(stream_ms, 5),
                 "kernel_ms_source": "stream HIP events around the timed region / steps (one launch per step)",
                 "algorithmic_bytes_per_agent_step": algorithmic_bytes_per_agent_step(RAYS), "bytes_per_launch": pb,
+                "valu": valu_roofline(stream_ms, E),
+                "binding_bound": "VALU issue (the working set is MALL/L2-resident; see valu.frac)",
             }
             if cars_ms is not None:
                 roofline["kernel_ms_library_events"] = round(cars_ms, 5)
@@ -247,8 +439,9 @@ def main():
             "config": {"workload": f"config 3: {E} envs/GPU x {N} agents x {RAYS}-beam lidar, team reward, "
                                    f"respawn on, max_steps 2000, per-env auto-reset",
                        "envs_per_gpu": E, "agents": N, "rays": RAYS, "obs_dim": D,
-                       "parallelism": f"env-sharded x{world}" + (" + RCCL gather to rank 0 per step" if gather_on else "")},
+                       "parallelism": f"env-sharded x{world} (one process per GPU, no data-path collective)"},
             "roofline": roofline,
+            "gather_to_root": gather,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:

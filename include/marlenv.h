@@ -50,6 +50,7 @@ enum { MEV_ALIVE = 0, MEV_DEAD = 1, MEV_SUCCESS = 2, MEV_CRASH_WALL = 3, MEV_CRA
 #define MEV_DEVICE_PTRS 0x1u /* all pointers in this call are device pointers; no host sync */
 #define MEV_AUTO_RESET 0x2u  /* an env whose previous step ended (terminated|truncated) is reset
                                 before this step (gym-style vector auto-reset) */
+/* MEV_GATHER_TO_ROOT (0x4) is declared with the multi-GPU entry points below */
 
 typedef struct mev_handle mev_handle;
 
@@ -222,6 +223,84 @@ int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* 
  * step is one sequential loop, cpp/IntersectionEnv.cpp:133-392). */
 int mev_set_step_kernel(mev_handle* h, int32_t kernel);
 int mev_get_step_kernel(const mev_handle* h, int32_t* kernel);
+
+/* ---- Multi-GPU: the per-step RCCL gather of the stacked outputs ----------
+ * envs are sharded over the GPUs of a node, one process and
+ * one handle per GPU, with no communication inside a step; the one collective
+ * is a gather of every rank's step outputs to a root rank over xGMI.  The
+ * reference has no counterpart (each IntersectionEnv is a single instance,
+ * cpp/IntersectionEnv.h:23-105).
+ *
+ * Packed layout of one rank's outputs (slots = envs per rank, the largest
+ * shard; a smaller shard leaves the tail of its slots unused), one contiguous
+ * message per rank:
+ *   obs f32 [slots][N][D] | reward f32 [slots][N] | done u8 [slots][N] |
+ *   status u8 [slots][N] | terminated u8 [slots] | truncated u8 [slots]
+ * each field 256-B aligned, the total padded to 256 B.  Host-only (no device). */
+#define MEV_GATHER_TO_ROOT 0x4u /* mev_step: write the outputs packed and gather them to the root rank */
+#define MEV_COMM_ID_BYTES 128   /* == NCCL_UNIQUE_ID_BYTES */
+enum { MEV_PK_OBS = 0, MEV_PK_REWARD, MEV_PK_DONE, MEV_PK_STATUS, MEV_PK_TERMINATED, MEV_PK_TRUNCATED, MEV_PK_COUNT };
+int mev_packed_layout(int32_t slots, int32_t num_agents, int32_t obs_dim, uint64_t* offsets /*[MEV_PK_COUNT]*/,
+                      uint64_t* bytes);
+/* ncclGetUniqueId: called by ONE process (any), then shared with every rank
+ * out of band (e.g. a TCP store); id is MEV_COMM_ID_BYTES bytes. */
+int mev_comm_unique_id(uint8_t* id);
+/* Join the communicator of `world` ranks (ncclCommInitRank on the handle's
+ * device; collective: every rank calls it) and allocate the double-buffered
+ * packed buffers: two send buffers on a non-root rank, two [world][bytes]
+ * gather buffers on the root.  slots = envs per rank of the largest shard
+ * (0 = num_envs). */
+int mev_comm_init(mev_handle* h, const uint8_t* id, int32_t world, int32_t rank, int32_t root, int32_t slots);
+int mev_comm_destroy(mev_handle* h);
+/* mev_step with MEV_GATHER_TO_ROOT (the args' obs/reward/done/status/
+ * terminated/truncated pointers must be NULL): the step kernel writes this
+ * rank's outputs straight into its packed slot (on the root: its row of the
+ * gather buffer, no copy), then one grouped ncclSend (non-root) / ncclRecv
+ * from every peer (root) runs on the handle's communication stream, ordered
+ * after the step by an event, so it overlaps the next step.  Step t and t+2
+ * share a buffer: step t+2 waits for gather t.  agents_alive / step still go
+ * to the args' pointers (or the handle's own buffers).
+ *
+ * mev_gather_result (root): the gather buffer of the last gathered step,
+ * [world][bytes] in rank order, and makes the handle's stream wait for that
+ * gather (stream-ordered consumers on that stream then see every rank's rows).
+ * mev_gather_wait: host wait for every gather issued so far, at most
+ * timeout_ms (<= 0: no limit); on timeout the communicator is aborted and
+ * MEV_E_HIP returned, so a lost peer cannot hang the caller forever. */
+int mev_gather_result(mev_handle* h, void** stacked, uint64_t* bytes_per_rank, int32_t* world);
+int mev_gather_wait(mev_handle* h, int32_t timeout_ms);
+
+/* ---- Zero-copy export (DLPack) -----------------------------------------
+ * the handle's device output buffers as DLPack tensors for
+ * torch-free consumers (and torch.from_dlpack).  The structs below are the
+ * DLPack v0.8 ABI (dlpack.h: DLDevice, DLDataType, DLTensor, DLManagedTensor),
+ * restated so this header stays self-contained.  The tensor views memory the
+ * handle owns: it is valid until mev_destroy; call its deleter when done (it
+ * frees only the descriptor). */
+typedef struct { int32_t device_type; int32_t device_id; } mev_dl_device; /* kDLROCM = 10 */
+typedef struct { uint8_t code; uint8_t bits; uint16_t lanes; } mev_dl_dtype; /* kDLInt 0, kDLUInt 1, kDLFloat 2 */
+typedef struct {
+    void* data;
+    mev_dl_device device;
+    int32_t ndim;
+    mev_dl_dtype dtype;
+    int64_t* shape;
+    int64_t* strides; /* NULL = compact row-major */
+    uint64_t byte_offset;
+} mev_dl_tensor;
+typedef struct mev_dl_managed {
+    mev_dl_tensor dl_tensor;
+    void* manager_ctx;
+    void (*deleter)(struct mev_dl_managed* self);
+} mev_dl_managed;
+enum { MEV_OUT_OBS = 0, MEV_OUT_REWARD, MEV_OUT_DONE, MEV_OUT_STATUS, MEV_OUT_TERMINATED, MEV_OUT_TRUNCATED,
+       MEV_OUT_AGENTS_ALIVE, MEV_OUT_STEP, MEV_OUT_GATHERED /* root: [world][bytes] u8 of the last gather */,
+       MEV_OUT_COUNT };
+/* The handle's internal output buffer `which` (what steps without output
+ * pointers write, and what mev_device_outputs returns) as a DLPack tensor:
+ * obs [E][N][D] f32, reward [E][N] f32, done/status [E][N] u8,
+ * terminated/truncated [E] u8, agents_alive/step [E] i32. */
+int mev_output_dlpack(mev_handle* h, int32_t which, mev_dl_managed** out);
 
 #ifdef __cplusplus
 }

@@ -88,7 +88,10 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC] + sched + VARIANTS[variant]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
-    cmd += ["-o", tmp]
+    # RCCL for the multi-GPU gather (mev_comm_*); when torch is imported first its
+    # bundled librccl.so (same SONAME librccl.so.1) satisfies this dependency,
+    # as its libamdhip64.so satisfies libamdhip64.so.7: one runtime per process
+    cmd += ["-L", "/opt/rocm/lib", "-lrccl", "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -20,6 +20,11 @@ LIB_PATH = _build.LIB_PATH
 
 MEV_DEVICE_PTRS = 0x1
 MEV_AUTO_RESET = 0x2
+MEV_GATHER_TO_ROOT = 0x4
+MEV_COMM_ID_BYTES = 128
+# packed-output fields (mev_packed_layout) and DLPack outputs (mev_output_dlpack), include/marlenv.h order
+PACKED_FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated")
+DLPACK_OUTPUTS = ("obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step", "gathered")
 
 STATUS_NAMES = ("ALIVE", "DEAD", "SUCCESS", "CRASH_WALL", "CRASH_LINE", "CRASH_CAR")
 PATH_LEN = 160
@@ -34,6 +39,8 @@ EXPORTED = (
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
     "mev_kernel_timing", "mev_kernel_times", "mev_set_reset_routes", "mev_snapshot_size", "mev_snapshot",
     "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel",
+    "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
+    "mev_gather_wait", "mev_output_dlpack",
 )
 
 
@@ -140,6 +147,14 @@ def load_library(variant: str = None):
     L.mev_set_reward.argtypes = [_vp, f32p]
     L.mev_car_update.argtypes = [f32p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
     L.mev_car_check_collision.argtypes = [f32p, f32p, i32p]
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    L.mev_packed_layout.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, u64p, u64p]
+    L.mev_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.mev_comm_init.argtypes = [_vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
+    L.mev_comm_destroy.argtypes = [_vp]
+    L.mev_gather_result.argtypes = [_vp, ctypes.POINTER(_vp), u64p, i32p]
+    L.mev_gather_wait.argtypes = [_vp, ctypes.c_int32]
+    L.mev_output_dlpack.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(_vp)]
     _libs[variant] = L
     return L
 
@@ -319,16 +334,19 @@ class Handle:
                     agents_alive=np.zeros(E, np.int32), step=np.zeros(E, np.int32))
 
     def step(self, actions, dt: float = 1.0 / 60.0, out: Optional[dict] = None, spawn_route=None,
-             auto_reset: bool = False, device: bool = False):
+             auto_reset: bool = False, device: bool = False, gather: bool = False):
         """Host mode (default): numpy in/out, synchronous.  device=True: every
-        array is a device tensor/pointer on this handle's device; asynchronous."""
+        array is a device tensor/pointer on this handle's device; asynchronous.
+        gather=True (needs comm_init): the outputs are written packed and
+        gathered to the root rank over RCCL (gather_result); `out` may then
+        only hold agents_alive / step."""
         if not device:
             actions = np.ascontiguousarray(actions, np.float32)
             if actions.size != self.E * self.N * 2:
                 raise ValueError(f"actions must have {self.E}x{self.N}x2 elements, got {actions.shape}")
             if spawn_route is not None:
                 spawn_route = np.ascontiguousarray(np.broadcast_to(np.asarray(spawn_route, np.int32), (self.E,)))
-            if out is None:
+            if out is None and not gather:
                 out = self.alloc_outputs()
         a = MevStepArgs()
         a.actions = _ptr(actions)
@@ -337,9 +355,50 @@ class Handle:
         out = out or {}
         for k in ("obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step"):
             setattr(a, k, _ptr(out.get(k)))
-        a.flags = (MEV_DEVICE_PTRS if device else 0) | (MEV_AUTO_RESET if auto_reset else 0)
+        a.flags = ((MEV_DEVICE_PTRS if device else 0) | (MEV_AUTO_RESET if auto_reset else 0) |
+                   (MEV_GATHER_TO_ROOT if gather else 0))
         _check(self._lib.mev_step(self._h, ctypes.byref(a)))
         return out
+
+    # -- multi-GPU gather (mev_comm_*) -------------------------------------
+    def comm_init(self, unique_id: bytes, world: int, rank: int, root: int = 0, slots: int = 0):
+        """Join the RCCL communicator (collective over all ranks); slots = envs of the largest shard."""
+        if len(unique_id) != MEV_COMM_ID_BYTES:
+            raise ValueError("unique_id must be MEV_COMM_ID_BYTES bytes")
+        _check(self._lib.mev_comm_init(self._h, bytes(unique_id), int(world), int(rank), int(root), int(slots)))
+        self.comm = dict(world=int(world), rank=int(rank), root=int(root), slots=int(slots) or self.E)
+
+    def comm_destroy(self):
+        _check(self._lib.mev_comm_destroy(self._h))
+        self.comm = None
+
+    def gather_result(self):
+        """Root: (device pointer, bytes per rank, world) of the last gathered step's [world][bytes] buffer;
+        the handle's stream is made to wait for that gather."""
+        p, n, w = _vp(), ctypes.c_uint64(), ctypes.c_int32()
+        _check(self._lib.mev_gather_result(self._h, ctypes.byref(p), ctypes.byref(n), ctypes.byref(w)))
+        return p.value, n.value, w.value
+
+    def gather_wait(self, timeout_ms: int = 0):
+        """Host wait for every gather issued so far (timeout: the communicator is aborted, MevError)."""
+        _check(self._lib.mev_gather_wait(self._h, int(timeout_ms)))
+
+    # -- zero-copy export (DLPack) ----------------------------------------
+    def output_dlpack(self, which: str):
+        """PyCapsule ("dltensor") viewing the handle's internal output buffer `which` (DLPACK_OUTPUTS);
+        valid while the handle lives; torch.from_dlpack() consumes it."""
+        m = _vp()
+        _check(self._lib.mev_output_dlpack(self._h, DLPACK_OUTPUTS.index(which), ctypes.byref(m)))
+        new = ctypes.pythonapi.PyCapsule_New
+        new.restype = ctypes.py_object
+        new.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
+        return new(m.value, b"dltensor", None)
+
+    def output_tensors(self, names=("obs", "reward", "done", "status", "terminated", "truncated",
+                                    "agents_alive", "step")):
+        """The internal output buffers as torch tensors (zero copy, through DLPack)."""
+        import torch.utils.dlpack as tdl
+        return {k: tdl.from_dlpack(self.output_dlpack(k)) for k in names}
 
     def get_outputs(self, out: Optional[dict] = None, device: bool = False):
         """Outputs of the last step/reset/restore; device=True: `out` holds device buffers (D2D copies)."""
@@ -460,6 +519,22 @@ def car_check_collision(box_a, box_b) -> bool:
     _check(load_library().mev_car_check_collision(a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                                                   b.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(r)))
     return bool(r.value)
+
+
+def packed_layout(slots: int, agents: int, obs_dim: int):
+    """(offsets by field, total bytes) of one rank's packed outputs (mev_packed_layout; host-only, no GPU)."""
+    off = (ctypes.c_uint64 * len(PACKED_FIELDS))()
+    n = ctypes.c_uint64()
+    _check(load_library().mev_packed_layout(int(slots), int(agents), int(obs_dim), off, ctypes.byref(n)))
+    return dict(zip(PACKED_FIELDS, (int(x) for x in off))), int(n.value)
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId (call on ONE rank, share the bytes with all)."""
+    _torch_runtime_first()
+    buf = ctypes.create_string_buffer(MEV_COMM_ID_BYTES)
+    _check(load_library().mev_comm_unique_id(buf))
+    return buf.raw
 
 
 def device_count() -> int:

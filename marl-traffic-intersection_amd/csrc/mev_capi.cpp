@@ -6,10 +6,13 @@
 
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <rccl/rccl.h>
 #include <string.h>
 
+#include <chrono>
 #include <cstdio>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mev_kernels.h"
@@ -75,6 +78,16 @@ struct mev_handle {
     int64_t t_phase = 0;   // steps since timing was enabled
     double t_cars_ms = 0.0, t_lidar_ms = 0.0;
     int64_t t_steps = 0;
+    // multi-GPU gather (mev_comm_init): packed outputs, double buffered by step parity
+    ncclComm_t comm = nullptr;
+    int world = 1, rank = 0, root = 0, slots = 0;
+    uint64_t pk_off[MEV_PK_COUNT] = {};
+    uint64_t pk_bytes = 0;
+    uint8_t* pk_buf[2] = {nullptr, nullptr};  // root: [world][pk_bytes]; other ranks: [pk_bytes]
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_step[2] = {nullptr, nullptr}, ev_gather[2] = {nullptr, nullptr};
+    bool gather_pending[2] = {false, false};
+    int64_t gathers = 0;  // gathered steps so far; the last one used buffer (gathers - 1) & 1
 
     template <class T>
     hipError_t alloc(T** p, size_t n) {
@@ -105,7 +118,24 @@ struct mev_handle {
         tev.clear();
         tn = 0;
     }
+    void free_comm() {
+        if (comm) (void)ncclCommDestroy(comm);
+        comm = nullptr;
+        for (int b = 0; b < 2; ++b) {
+            if (pk_buf[b]) (void)hipFree(pk_buf[b]);
+            if (ev_step[b]) (void)hipEventDestroy(ev_step[b]);
+            if (ev_gather[b]) (void)hipEventDestroy(ev_gather[b]);
+            pk_buf[b] = nullptr;
+            ev_step[b] = ev_gather[b] = nullptr;
+            gather_pending[b] = false;
+        }
+        if (comm_stream) (void)hipStreamDestroy(comm_stream);
+        comm_stream = nullptr;
+        world = 1; rank = root = 0; gathers = 0;
+    }
     ~mev_handle() {
+        if (comm_stream) (void)hipStreamSynchronize(comm_stream);
+        free_comm();
         free_timing();
         if (d_snap_stage) (void)hipFree(d_snap_stage);
         for (void* p : allocs) (void)hipFree(p);
@@ -166,6 +196,15 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(MEV_E_HIP, "no HIP device available");
     if (c.device < 0 || c.device >= ndev) return fail(MEV_E_INVALID, "device ordinal out of range");
     HIP_TRY(hipSetDevice(c.device));
+    // LiDAR probe distances exactly as Lidar.cpp:33 accumulates them (validated
+    // before any allocation: this error path owns nothing)
+    std::vector<float> dists;
+    bool dist_mul_exact = true;
+    for (float dist = 0.0f; dist < c.lidar_max_dist; dist += c.lidar_step) {
+        if (dist != float(dists.size()) * c.lidar_step) dist_mul_exact = false;
+        dists.push_back(dist);
+        if (dists.size() > (1u << 20)) return fail(MEV_E_INVALID, "lidar_max_dist / lidar_step too large");
+    }
 
     auto* h = new mev_handle();
     h->cfg = c;
@@ -199,14 +238,6 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
         }
     }
     h->h_traffic = mev::default_traffic_routes(c.num_lanes);
-    // LiDAR probe distances exactly as Lidar.cpp:33 accumulates them
-    std::vector<float> dists;
-    bool dist_mul_exact = true;
-    for (float dist = 0.0f; dist < c.lidar_max_dist; dist += c.lidar_step) {
-        if (dist != float(dists.size()) * c.lidar_step) dist_mul_exact = false;
-        dists.push_back(dist);
-        if (dists.size() > (1u << 20)) return fail(MEV_E_INVALID, "lidar_max_dist / lidar_step too large");
-    }
 
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
@@ -320,9 +351,16 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     p.n_traffic_routes = int(h->h_traffic.size());
     p.reset_routes = h->d_reset_routes;
     p.n_reset_routes = 0;
-    *out = h;
     // initial state = a reset (the reference env.py constructor ends with reset(), env.py:136)
-    return mev_reset(h, nullptr, nullptr, 0);
+    const int rc = mev_reset(h, nullptr, nullptr, 0);
+    if (rc != MEV_OK) {
+        const std::string m = g_err;
+        delete h;
+        *out = nullptr;
+        return fail(rc, m);
+    }
+    *out = h;
+    return MEV_OK;
 }
 
 int mev_destroy(mev_handle* h) {
@@ -561,6 +599,12 @@ int mev_reset(mev_handle* h, const uint8_t* env_mask, float* obs, uint32_t flags
 int mev_step(mev_handle* h, const mev_step_args* a) {
     if (!h || !a) return fail(MEV_E_INVALID, "null argument");
     if (!a->actions) return fail(MEV_E_INVALID, "actions required");
+    const bool gather = (a->flags & MEV_GATHER_TO_ROOT) != 0;
+    if (gather) {
+        if (!h->comm) return fail(MEV_E_INVALID, "MEV_GATHER_TO_ROOT needs a communicator (mev_comm_init)");
+        if (a->obs || a->reward || a->done || a->status || a->terminated || a->truncated)
+            return fail(MEV_E_INVALID, "MEV_GATHER_TO_ROOT writes the outputs packed: pass NULL output pointers");
+    }
     HIP_TRY(hipSetDevice(h->cfg.device));
     const bool dev = (a->flags & MEV_DEVICE_PTRS) != 0;
     const size_t E = size_t(h->cfg.num_envs), EN = E * size_t(h->cfg.num_agents);
@@ -581,8 +625,21 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     }
     // spawn probability, TrafficFlow.cpp:321-322 (host glibc expf, bit-identical to the reference)
     h->sp.spawn_prob = 1.0f - expf(-h->cfg.traffic_density * a->dt);
-    const mev::Outputs o = resolve_outputs(h, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated,
-                                           a->agents_alive, a->step, dev);
+    mev::Outputs o = resolve_outputs(h, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated,
+                                     a->agents_alive, a->step, dev);
+    const int slot = int(h->gathers & 1);
+    if (gather) {
+        // this rank's packed slot: on the root its own row of the gather buffer
+        // (no copy), elsewhere the send buffer; step t and t+2 share a buffer
+        if (h->gather_pending[slot]) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gather[slot], 0));
+        uint8_t* base = h->pk_buf[slot] + (h->rank == h->root ? size_t(h->root) * h->pk_bytes : 0);
+        o.obs = reinterpret_cast<float*>(base + h->pk_off[MEV_PK_OBS]);
+        o.rew = reinterpret_cast<float*>(base + h->pk_off[MEV_PK_REWARD]);
+        o.done = base + h->pk_off[MEV_PK_DONE];
+        o.status = base + h->pk_off[MEV_PK_STATUS];
+        o.term = base + h->pk_off[MEV_PK_TERMINATED];
+        o.trunc = base + h->pk_off[MEV_PK_TRUNCATED];
+    }
     const hipEvent_t* ev = nullptr;
     if (!h->tev.empty() && (h->t_phase++ % h->t_every) == 0) {
         if (size_t(3 * (h->tn + 1)) > h->tev.size()) HIP_TRY(h->fold_timing());
@@ -591,6 +648,30 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     }
     HIP_TRY(mev::launch_step(h->sp, in, o, h->stream, ev));
     h->last = o;
+    if (gather && h->world == 1) {
+        ++h->gathers;  // a world of one: the root's row is written in place, nothing to move
+    } else if (gather) {
+        // one grouped send/recv on the communication stream, after the step
+        HIP_TRY(hipEventRecord(h->ev_step[slot], h->stream));
+        HIP_TRY(hipStreamWaitEvent(h->comm_stream, h->ev_step[slot], 0));
+        {
+            ncclResult_t nr = ncclGroupStart();
+            if (h->rank == h->root) {
+                for (int r = 0; r < h->world && nr == ncclSuccess; ++r)
+                    if (r != h->root)
+                        nr = ncclRecv(h->pk_buf[slot] + size_t(r) * h->pk_bytes, h->pk_bytes, ncclUint8, r, h->comm,
+                                      h->comm_stream);
+            } else {
+                nr = ncclSend(h->pk_buf[slot], h->pk_bytes, ncclUint8, h->root, h->comm, h->comm_stream);
+            }
+            const ncclResult_t ne = ncclGroupEnd();
+            if (nr == ncclSuccess) nr = ne;
+            if (nr != ncclSuccess) return fail(MEV_E_HIP, std::string("RCCL gather: ") + ncclGetErrorString(nr));
+        }
+        HIP_TRY(hipEventRecord(h->ev_gather[slot], h->comm_stream));
+        h->gather_pending[slot] = true;
+        ++h->gathers;
+    }
     if (!dev) {
         int r = copy_out(h, o, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated, a->agents_alive,
                          a->step, hipMemcpyDeviceToHost);
@@ -835,6 +916,17 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
     } else {
         memcpy(&hd, src, sizeof(hd));
     }
+    {  // validate before touching the handle: a mismatched snapshot leaves it unchanged
+        const mev::Outputs save_last = h->last;
+        h->last = h->internal;  // the field table of a restore (its targets are the internal buffers)
+        const std::vector<SnapField> f0 = snap_fields(h);
+        h->last = save_last;
+        const size_t total0 = snap_offsets(f0, E, nullptr);
+        if (hd.magic != kSnapMagic || hd.version != 1 || hd.E != h->cfg.num_envs || hd.N != h->cfg.num_agents ||
+            hd.K != h->cfg.max_npcs || hd.D != h->D || hd.nfields != int32_t(f0.size()) || hd.total_bytes != total0)
+            return fail(MEV_E_INVALID, "snapshot does not match this handle");
+        if (env_mask && f0.size() > size_t(mev::kMaxRestoreFields)) return fail(MEV_E_INVALID, "too many snapshot fields");
+    }
     // the live outputs are restored into the handle's own buffers; envs a masked
     // restore leaves alone keep their current outputs, so bring those in first
     {
@@ -860,16 +952,12 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
     const std::vector<SnapField> f = snap_fields(h);
     std::vector<size_t> off;
     const size_t total = snap_offsets(f, E, &off);
-    if (hd.magic != kSnapMagic || hd.version != 1 || hd.E != h->cfg.num_envs || hd.N != h->cfg.num_agents ||
-        hd.K != h->cfg.max_npcs || hd.D != h->D || hd.nfields != int32_t(f.size()) || hd.total_bytes != total)
-        return fail(MEV_E_INVALID, "snapshot does not match this handle");
     const uint8_t* s = static_cast<const uint8_t*>(src);
     if (!env_mask) {
         const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
         for (size_t i = 0; i < f.size(); ++i) HIP_TRY(hipMemcpyAsync(f[i].restore, s + off[i], f[i].bpe * E, kind, h->stream));
         h->rng_counter = hd.rng_counter;
     } else {
-        if (f.size() > size_t(mev::kMaxRestoreFields)) return fail(MEV_E_INVALID, "too many snapshot fields");
         const uint8_t* dsrc = s;
         const uint8_t* dmask = env_mask;
         if (!dev) {  // stage the snapshot and the mask on the device
@@ -898,6 +986,168 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
         HIP_TRY(mev::launch_restore(tab, dsrc, dmask, h->cfg.num_envs, h->stream));
     }
     if (!dev) HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+// ---- multi-GPU gather (include/marlenv.h) ----------------
+int mev_packed_layout(int32_t slots, int32_t num_agents, int32_t obs_dim, uint64_t* offsets, uint64_t* bytes) {
+    if (!offsets || !bytes) return fail(MEV_E_INVALID, "null argument");
+    if (slots < 1 || num_agents < 1 || obs_dim < 1) return fail(MEV_E_INVALID, "slots, agents and obs_dim must be >= 1");
+    const uint64_t C = uint64_t(slots), N = uint64_t(num_agents), D = uint64_t(obs_dim);
+    const uint64_t sizes[MEV_PK_COUNT] = {C * N * D * 4, C * N * 4, C * N, C * N, C, C};
+    uint64_t off = 0;
+    for (int f = 0; f < MEV_PK_COUNT; ++f) {
+        off = (off + 255) & ~uint64_t(255);
+        offsets[f] = off;
+        off += sizes[f];
+    }
+    *bytes = (off + 255) & ~uint64_t(255);
+    return MEV_OK;
+}
+
+int mev_comm_unique_id(uint8_t* id) {
+    if (!id) return fail(MEV_E_INVALID, "null argument");
+    static_assert(sizeof(ncclUniqueId) == MEV_COMM_ID_BYTES, "unique id size");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return fail(MEV_E_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    memcpy(id, &u, sizeof(u));
+    return MEV_OK;
+}
+
+int mev_comm_init(mev_handle* h, const uint8_t* id, int32_t world, int32_t rank, int32_t root, int32_t slots) {
+    if (!h || !id) return fail(MEV_E_INVALID, "null argument");
+    if (h->comm) return fail(MEV_E_INVALID, "the handle already has a communicator");
+    if (world < 1 || rank < 0 || rank >= world || root < 0 || root >= world)
+        return fail(MEV_E_INVALID, "bad world / rank / root");
+    if (slots <= 0) slots = h->cfg.num_envs;
+    if (slots < h->cfg.num_envs) return fail(MEV_E_INVALID, "slots must be >= num_envs");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    int rc = mev_packed_layout(slots, h->cfg.num_agents, h->D, h->pk_off, &h->pk_bytes);
+    if (rc) return rc;
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t nr = ncclCommInitRank(&comm, world, u, rank);
+    if (nr != ncclSuccess) return fail(MEV_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+    h->comm = comm;
+    h->world = world; h->rank = rank; h->root = root; h->slots = slots; h->gathers = 0;
+    hipError_t e = hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking);
+    const size_t per = (rank == root) ? size_t(world) * h->pk_bytes : h->pk_bytes;
+    for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+        e = hipMalloc(reinterpret_cast<void**>(&h->pk_buf[b]), per);
+        if (e == hipSuccess) e = hipMemsetAsync(h->pk_buf[b], 0, per, h->stream);  // unused slot tails stay 0
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_step[b], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_gather[b], hipEventDisableTiming);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+        h->free_comm();
+        return fail(MEV_E_NOMEM, std::string("gather buffers: ") + hipGetErrorString(e));
+    }
+    return MEV_OK;
+}
+
+int mev_comm_destroy(mev_handle* h) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->comm_stream) HIP_TRY(hipStreamSynchronize(h->comm_stream));
+    h->free_comm();
+    return MEV_OK;
+}
+
+int mev_gather_result(mev_handle* h, void** stacked, uint64_t* bytes_per_rank, int32_t* world) {
+    if (!h || !stacked || !bytes_per_rank || !world) return fail(MEV_E_INVALID, "null argument");
+    if (!h->comm) return fail(MEV_E_INVALID, "no communicator (mev_comm_init)");
+    if (h->rank != h->root) return fail(MEV_E_INVALID, "the gather result lives on the root rank");
+    if (h->gathers == 0) return fail(MEV_E_INVALID, "no step has been gathered yet");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const int b = int((h->gathers - 1) & 1);
+    if (h->gather_pending[b]) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gather[b], 0));
+    *stacked = h->pk_buf[b];
+    *bytes_per_rank = h->pk_bytes;
+    *world = h->world;
+    return MEV_OK;
+}
+
+int mev_gather_wait(mev_handle* h, int32_t timeout_ms) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (!h->comm) return fail(MEV_E_INVALID, "no communicator (mev_comm_init)");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int b = 0; b < 2; ++b) {
+        if (!h->gather_pending[b]) continue;
+        for (;;) {
+            const hipError_t q = hipEventQuery(h->ev_gather[b]);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return fail(MEV_E_HIP, std::string("gather: ") + hipGetErrorString(q));
+            ncclResult_t ae = ncclSuccess;
+            if (ncclCommGetAsyncError(h->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                (void)ncclCommAbort(h->comm);
+                h->comm = nullptr;
+                return fail(MEV_E_HIP, std::string("RCCL gather failed: ") + ncclGetErrorString(ae));
+            }
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            if (timeout_ms > 0 && ms > double(timeout_ms)) {
+                (void)ncclCommAbort(h->comm);  // a lost peer must not hang the caller
+                h->comm = nullptr;
+                return fail(MEV_E_HIP, "RCCL gather timed out (communicator aborted)");
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        h->gather_pending[b] = false;
+    }
+    return MEV_OK;
+}
+
+// ---- DLPack export of the internal output buffers ---------------------------
+namespace {
+struct DlBox {
+    mev_dl_managed m;
+    int64_t shape[3];
+};
+void dl_delete(mev_dl_managed* m) { delete reinterpret_cast<DlBox*>(m); }
+}  // namespace
+
+int mev_output_dlpack(mev_handle* h, int32_t which, mev_dl_managed** out) {
+    if (!h || !out) return fail(MEV_E_INVALID, "null argument");
+    const int64_t E = h->cfg.num_envs, N = h->cfg.num_agents, D = h->D;
+    void* data = nullptr;
+    int nd = 1;
+    int64_t sh[3] = {E, 0, 0};
+    mev_dl_dtype dt{1, 8, 1};  // u8
+    const mev::Outputs& I = h->internal;
+    switch (which) {
+        case MEV_OUT_OBS: data = I.obs; nd = 3; sh[1] = N; sh[2] = D; dt = {2, 32, 1}; break;
+        case MEV_OUT_REWARD: data = I.rew; nd = 2; sh[1] = N; dt = {2, 32, 1}; break;
+        case MEV_OUT_DONE: data = I.done; nd = 2; sh[1] = N; break;
+        case MEV_OUT_STATUS: data = I.status; nd = 2; sh[1] = N; break;
+        case MEV_OUT_TERMINATED: data = I.term; break;
+        case MEV_OUT_TRUNCATED: data = I.trunc; break;
+        case MEV_OUT_AGENTS_ALIVE: data = I.alive_cnt; dt = {0, 32, 1}; break;
+        case MEV_OUT_STEP: data = I.step; dt = {0, 32, 1}; break;
+        case MEV_OUT_GATHERED:
+            if (!h->comm || h->rank != h->root) return fail(MEV_E_INVALID, "the gather buffer lives on the root rank");
+            data = h->pk_buf[h->gathers > 0 ? int((h->gathers - 1) & 1) : 0];
+            nd = 2; sh[0] = h->world; sh[1] = int64_t(h->pk_bytes);
+            break;
+        default: return fail(MEV_E_INVALID, "unknown output");
+    }
+    auto* box = new DlBox();
+    for (int k = 0; k < 3; ++k) box->shape[k] = sh[k];
+    mev_dl_tensor& t = box->m.dl_tensor;
+    t.data = data;
+    t.device = {10, h->cfg.device};  // kDLROCM
+    t.ndim = nd;
+    t.dtype = dt;
+    t.shape = box->shape;
+    t.strides = nullptr;
+    t.byte_offset = 0;
+    box->m.manager_ctx = nullptr;
+    box->m.deleter = dl_delete;
+    *out = &box->m;
     return MEV_OK;
 }
 

@@ -2,19 +2,23 @@
 
 Envs never interact, so a batch of E envs is split into contiguous blocks,
 env e -> rank floor(e * G / E), one process and one device handle per GPU,
-with no communication inside a step.  The only collective is one gather per
-step of the per-rank outputs to rank 0 (RCCL over xGMI on MI355X; gloo in
-the CPU tests), issued on the step's stream right after the step so it
-overlaps the next step's launch on the other ranks.
+with no communication inside a step.  The one collective is the gather of
+every rank's step outputs to a root rank, and it lives in the C ABI
+(mev_comm_init + the MEV_GATHER_TO_ROOT step flag: one grouped RCCL
+ncclSend/ncclRecv per step over xGMI, on a communication stream that
+overlaps the next step); the data path needs no torch.distributed.
 
 The outputs of one step are packed into ONE flat byte buffer per rank so the
-gather is a single message per peer:
+gather is a single message per peer (mev_packed_layout, include/marlenv.h):
 
     obs f32 [C, N, D] | reward f32 [C, N] | done u8 [C, N] | status u8 [C, N]
-    | terminated u8 [C] | truncated u8 [C]        (padded to 256 B)
+    | terminated u8 [C] | truncated u8 [C]     (fields 256-B aligned, total padded to 256 B)
 
 with C = ceil(E / G) slots per rank (ranks with fewer envs leave the tail of
-their slots unused).
+their slots unused).  This module holds the host-side pieces: the partition,
+the layout's typed views, the RCCL-id bootstrap through a key-value store, and
+a torch.distributed gather of packed buffers that the CPU tests use in place of
+RCCL (gloo has no device path).
 """
 from __future__ import annotations
 
@@ -35,21 +39,18 @@ def env_owner(env: int, total_envs: int, world: int) -> int:
 
 
 class PackedOutputs:
-    """Byte layout of one rank's step outputs (see module docstring)."""
+    """Byte layout of one rank's step outputs: the library's mev_packed_layout
+    (host-only, no device), so these views match what MEV_GATHER_TO_ROOT writes."""
 
     FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated")
 
     def __init__(self, slots: int, agents: int, obs_dim: int):
+        from . import _capi
+
         self.C, self.N, self.D = int(slots), int(agents), int(obs_dim)
-        C, N, D = self.C, self.N, self.D
-        sizes = [C * N * D * 4, C * N * 4, C * N, C * N, C, C]
-        self.offsets: Dict[str, int] = {}
-        off = 0
-        for name, sz in zip(self.FIELDS, sizes):
-            self.offsets[name] = off
-            off += sz
-        self.used = off
-        self.nbytes = (off + 255) // 256 * 256
+        self.offsets, self.nbytes = _capi.packed_layout(self.C, self.N, self.D)
+        self.offsets: Dict[str, int]
+        self.used = self.offsets["truncated"] + self.C
 
     def pointers(self, base: int) -> Dict[str, int]:
         """Field pointers (for mev_step's output arguments) inside a buffer at `base`."""
@@ -94,8 +95,25 @@ class PackedOutputs:
         return {k: np.concatenate([p[k] for p in parts]) for k in self.FIELDS}
 
 
+def comm_bootstrap(handle, store, world: int, rank: int, root: int = 0, slots: int = 0,
+                   key: str = "mev_comm_id") -> None:
+    """Join the handle's RCCL communicator: the root draws the unique id
+    (mev_comm_unique_id) and publishes it in `store` (any object with
+    set/get, e.g. torch.distributed's TCPStore); every rank then calls
+    mev_comm_init.  After this, handle.step(..., gather=True) gathers."""
+    from . import _capi
+
+    if rank == root:
+        uid = _capi.comm_unique_id()
+        store.set(key, uid)
+    else:
+        uid = bytes(store.get(key))
+    handle.comm_init(uid, world, rank, root, slots)
+
+
 def gather_to_root(buf, stacked: Optional[object], group=None, async_op: bool = True):
-    """One gather of every rank's packed buffer into `stacked` ([world, nbytes]) on rank 0."""
+    """One gather of every rank's packed buffer into `stacked` ([world, nbytes]) on rank 0,
+    through torch.distributed: the CPU tests' stand-in (gloo) for the library's RCCL gather."""
     import torch.distributed as dist
     gl = list(stacked.unbind(0)) if stacked is not None else None
     return dist.gather(buf, gather_list=gl, dst=0, group=group, async_op=async_op)
