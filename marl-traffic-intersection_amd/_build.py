@@ -59,7 +59,14 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "npcprio0": ["-DMEV_NPC_PRIO=0"], "npcprio1": ["-DMEV_NPC_PRIO=1"], "npcprio3": ["-DMEV_NPC_PRIO=3"],
                # timing-only: k_step stopped after the car part / LiDAR phase 1 / 2 / 3 (instruction budgets)
                "stop1": ["-DMEV_EXP_STOP=1"], "stop2": ["-DMEV_EXP_STOP=2"], "stop3": ["-DMEV_EXP_STOP=3"],
-               "stop4": ["-DMEV_EXP_STOP=4"],
+               "stop4": ["-DMEV_EXP_STOP=4"], "stop0": ["-DMEV_EXP_STOP=0"],
+               # timing-only: k_step without the observation head / the car-car SAT
+               "nohead": ["-DMEV_EXP_NOHEAD"], "nosat": ["-DMEV_EXP_NOSAT"],
+               # exact variants: k_step's cars_post after the LiDAR (product: before it), at the LiDAR's last
+               # issue priority or a fixed one
+               "postlate": ["-DMEV_POST_AFTER_LIDAR=1"],
+               "post1": ["-DMEV_POST_AFTER_LIDAR=1", "-DMEV_PRIO_POST=1"],
+               "post3": ["-DMEV_POST_AFTER_LIDAR=1", "-DMEV_PRIO_POST=3"],
                # exact variant: k_step stages every output in LDS and writes whole rows at the end
                "staged": ["-DMEV_FUSED_STAGED=1"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it

@@ -38,7 +38,7 @@ constexpr int WAVE = 64;
         __builtin_amdgcn_wave_barrier();                                 \
         if (threadIdx.x == 0) p.debug[e * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
-#define STAMP(k) do { if ((k) == 0) STAMP_RAW(1); if ((k) == 6) STAMP_RAW(2); } while (0)
+#define STAMP(k) do { if ((k) == 0) STAMP_RAW(1); if ((k) == 5) STAMP_RAW(2); } while (0)  // 5: end of cars_pre
 #define STAMPX(k) do {} while (0)
 #define STAMPY(k) do {} while (0)
 #elif defined(MEV_STAMPS_X)
@@ -90,6 +90,15 @@ constexpr int MAXOB = MAXN + MAXK;
 #endif
 #ifndef MEV_PRIO_P3
 #define MEV_PRIO_P3 0
+#endif
+// k_step runs cars_post right after cars_pre (0) or after the LiDAR (1: its
+// latency-bound chain then overlaps other waves' LiDAR, but the waves end later:
+// measured 41.6 -> 44.1 us per step at config 3)
+#ifndef MEV_POST_AFTER_LIDAR
+#define MEV_POST_AFTER_LIDAR 0
+#endif
+#ifndef MEV_PRIO_POST  // k_step's car part after the LiDAR (cars_post); -1 keeps the LiDAR's last level
+#define MEV_PRIO_POST -1
 #endif
 #ifndef MEV_PRIO_P4  // the LiDAR block writes
 #define MEV_PRIO_P4 -1
@@ -689,12 +698,12 @@ struct CarsLDS {
     int32_t* envw;
 };
 
-__host__ __device__ inline size_t lds_al(size_t b) { return (b + 15) & ~size_t(15); }
+__host__ __device__ constexpr size_t lds_al(size_t b) { return (b + 15) & ~size_t(15); }
 
 // NPC slots that need obstacle entries in k_cars' LDS (none without traffic)
 __host__ __device__ inline int cars_k(const SimParams& p) { return p.traffic ? p.K : 0; }
 
-__host__ __device__ inline size_t cars_lds_bytes(int N, int K) {
+__host__ __device__ constexpr size_t cars_lds_bytes(int N, int K) {
     const size_t n = (size_t)N, ob = (size_t)(N + K);
     return 22 * lds_al(n * 4) + 2 * lds_al(n * 16) + 3 * lds_al(n * 4) + 4 * lds_al(n) + lds_al(n * 8) +
            lds_al(ob * 16) + 3 * lds_al(ob * 4) + lds_al(n * 16);
@@ -737,13 +746,25 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
 #define MEV_FUSED_STAGED 0
 #endif
 
-// The per-env body of the step (k_cars, or the first half of k_step): el and
-// nl are this wave's LDS.  FUSED: the LiDAR runs in the same wave right after
+// What the two halves of the car part share (cars_pre -> cars_post).
+struct CarsCtx {
+    int step_no;    // step counter after this step
+    bool do_reset;  // the env was auto-reset at the start of this step
+    int ncnt;       // NPCs alive after the traffic phase
+};
+
+// The per-env body of the step before the LiDAR (k_cars, or the first part of
+// k_step): el and nl are this wave's LDS.  Only what the LiDAR needs runs
+// here -- kinematics, status, car-car resolution, respawn, the obstacle table
+// and candidate masks; the rest (bonuses, team mix, flags, the state
+// write-back and the observation head) is cars_post, which k_step runs after
+// the LiDAR so that its latency-bound chain overlaps other waves' LiDAR
+// instead of delaying this wave's.  FUSED: the LiDAR runs in the same wave
 // (k_step) and reads the obstacle table and candidate masks from LDS, so they
 // are not published to HBM.
 template <bool TRAFFIC, bool FUSED>
-__device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
-                                          const CarsLDS& el, NpcLDS* nl) {
+__device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
+                                            const CarsLDS& el, NpcLDS* nl) {
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
     // status, collisions, respawn, observation head); the LiDAR block of the
     // observation is filled by the LiDAR body right after.  Per-agent phases run on
@@ -950,6 +971,7 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
 
     STAMP(2);
     // ---- car-car SAT (:292-318): ego pairs (i<j) and ego x NPC, one pair per lane
+#ifndef MEV_EXP_NOSAT  // timing-only: no car-car SAT
     for (int pbase = 0; pbase < N * N; pbase += WAVE) {
         const int pi = pbase + tid;
         if (pi < N * N) {
@@ -961,6 +983,7 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
                 atomicOr(&el.col[a], 1ull << b);
         }
     }
+#endif
     if constexpr (TRAFFIC) {
         for (int pbase = 0; pbase < N * ncnt; pbase += WAVE) {
             const int pi = pbase + tid;
@@ -976,14 +999,13 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
     wave_lds_sync();
 
     STAMP(3);
-    // ---- greedy resolution in (i, j) order, bonuses, team mix, flags (:292-370).
-    // lane = agent (N <= 64); the order-dependent scan runs on wave-uniform masks.
+    // ---- greedy resolution in (i, j) order (:292-318): lane = agent (N <= 64);
+    // the order-dependent scan runs on wave-uniform masks
     {
         const int i = tid;
         const bool in_env = i < N;
         const uint8_t alive_i = in_env ? el.alive[i] : 0;
-        uint8_t done_i = in_env ? el.done[i] : 0, st_i = in_env ? el.status[i] : 0;
-        float rew_i = in_env ? el.rew[i] : 0.0f;
+        const uint8_t done_i = in_env ? el.done[i] : 0;
         const unsigned long long col_i = in_env ? el.col[i] : 0ull;
         const bool colnpc_i = TRAFFIC && in_env && el.colnpc[i];
         unsigned long long donem = ballot(in_env && (done_i || !alive_i));
@@ -1001,54 +1023,13 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
             }
         }
         STAMPY(1);
-        if ((crash >> i) & 1ull) { done_i = 1; st_i = ST_CRASH_CAR; }
-        if (done_i) {
-            if (st_i == ST_CRASH_CAR) rew_i += p.k_cv;
-            else if (st_i == ST_CRASH_WALL || st_i == ST_CRASH_LINE) rew_i += p.k_co;
-            else if (st_i == ST_SUCCESS) rew_i += p.k_succ;
-        }
-        if (p.use_team && N > 0) {  // sequential sum in agent order, as the reference
-            float avg = 0.0f;
-            for (int a = 0; a < N; ++a) avg += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), a));
-            avg /= float(N);
-            rew_i = (1.0f - p.alpha) * rew_i + p.alpha * avg;
-        }
-        const unsigned long long alive_m = ballot(in_env && alive_i);
-        const unsigned long long succ_m = ballot(in_env && alive_i && done_i && st_i == ST_SUCCESS);
-        const unsigned long long done_m = ballot(in_env && done_i);
-        const int alive_cnt = __builtin_popcountll(alive_m), succ_cnt = __builtin_popcountll(succ_m);
-        const bool terminated = p.respawn ? (succ_cnt > 0 && succ_cnt == alive_cnt) : (done_m != 0ull);
-        const bool truncated = p.max_steps > 0 && step_no >= p.max_steps;
-        if (in_env) { el.done[i] = done_i; el.status[i] = st_i; el.rew[i] = rew_i; }
-        if (tid == 0) {
-            if constexpr (STAGE) {
-                el.envw[0] = terminated;
-                el.envw[1] = truncated;
-                el.envw[2] = alive_cnt;
-                el.envw[3] = step_no;
-                el.envw[4] = (terminated || truncated) ? 1 : 0;
-                el.envw[5] = do_reset;
-            } else {
-                p.step_count[e] = step_no;
-                out.term[e] = terminated;
-                out.trunc[e] = truncated;
-                out.alive_cnt[e] = alive_cnt;
-                out.step[e] = step_no;
-                p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
-            }
-        }
+        if (in_env && ((crash >> i) & 1ull)) { el.done[i] = 1; el.status[i] = ST_CRASH_CAR; }
     }
     wave_lds_sync();
     STAMPY(2);
-    // respawn crashed egos (Car::respawn, Car.cpp:76-84; :339-351) and write the
-    // final ego state back (lane = agent)
+    // respawn crashed egos (Car::respawn, Car.cpp:76-84; :339-351), lane = agent;
+    // the final state is written back by cars_post
     for (int i = tid; i < N; i += WAVE) {
-        const int g = e * N + i;
-        if (!STAGE) {
-            out.rew[g] = el.rew[i];
-            out.done[g] = el.done[i];
-            out.status[g] = el.status[i];
-        }
         const uint8_t st = el.status[i];
         if (p.respawn && el.alive[i] && el.done[i] && (st == ST_CRASH_CAR || st == ST_CRASH_WALL || st == ST_CRASH_LINE)) {
             const float sh = el.sh[i];
@@ -1058,14 +1039,6 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
             el.pidx[i] = 0; el.prev_dist[i] = 0.0f; el.pa0[i] = 0.0f; el.pa1[i] = 0.0f;
             el.acc[i] = 0.0f; el.steer[i] = 0.0f;
             el.tgx[i] = el.t10x[i]; el.tgy[i] = el.t10y[i];  // path[min(0 + 10, 159)]
-        }
-        if (STAGE) continue;  // k_step writes the state back at its end (fused_store)
-        egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
-        egof(p, EF_ACC)[g] = el.acc[i]; egof(p, EF_STEER)[g] = el.steer[i]; egoi(p, EF_PIDX)[g] = el.pidx[i];
-        egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
-        if (do_reset) {
-            egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
-            egoi(p, EF_INTENT)[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
         }
     }
     wave_lds_sync();
@@ -1116,8 +1089,93 @@ __device__ __forceinline__ void cars_body(const SimParams& p, const StepInputs& 
     }
 
     STAMP(5);
+    return CarsCtx{step_no, do_reset, ncnt};
+}
+
+// The rest of the car part (after the LiDAR in k_step, right after cars_pre in
+// k_cars): bonuses, team mix and env flags (:320-370), the reward / done /
+// status outputs and the state write-back, the observation head (:418-520).
+// Reads only the car LDS (the LiDAR never writes it).
+template <bool TRAFFIC, bool FUSED>
+__device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out, const int e, const CarsLDS& el,
+                                          const NpcLDS* nl, const CarsCtx& cx) {
+    const int tid = threadIdx.x & (WAVE - 1);
+    const int N = p.N;
+    constexpr bool STAGE = FUSED && MEV_FUSED_STAGED;
+    const int step_no = cx.step_no, ncnt = cx.ncnt;
+    const bool do_reset = cx.do_reset;
+    const int grp = tid >> 3, sub = tid & 7;
+    const unsigned long long gmask = 0xFFull << (grp * 8);
+    // ---- bonuses, team mix, flags (:320-370), lane = agent
+    {
+        const int i = tid;
+        const bool in_env = i < N;
+        const uint8_t alive_i = in_env ? el.alive[i] : 0;
+        const uint8_t done_i = in_env ? el.done[i] : 0, st_i = in_env ? el.status[i] : 0;
+        float rew_i = in_env ? el.rew[i] : 0.0f;
+        if (done_i) {
+            if (st_i == ST_CRASH_CAR) rew_i += p.k_cv;
+            else if (st_i == ST_CRASH_WALL || st_i == ST_CRASH_LINE) rew_i += p.k_co;
+            else if (st_i == ST_SUCCESS) rew_i += p.k_succ;
+        }
+        if (p.use_team && N > 0) {  // sequential sum in agent order, as the reference
+            float avg = 0.0f;
+            for (int a = 0; a < N; ++a) avg += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), a));
+            avg /= float(N);
+            rew_i = (1.0f - p.alpha) * rew_i + p.alpha * avg;
+        }
+        const unsigned long long alive_m = ballot(in_env && alive_i);
+        const unsigned long long succ_m = ballot(in_env && alive_i && done_i && st_i == ST_SUCCESS);
+        const unsigned long long done_m = ballot(in_env && done_i);
+        const int alive_cnt = __builtin_popcountll(alive_m), succ_cnt = __builtin_popcountll(succ_m);
+        const bool terminated = p.respawn ? (succ_cnt > 0 && succ_cnt == alive_cnt) : (done_m != 0ull);
+        const bool truncated = p.max_steps > 0 && step_no >= p.max_steps;
+        if (in_env) {
+            if (STAGE) el.rew[i] = rew_i;
+            else {
+                const int g = e * N + i;
+                out.rew[g] = rew_i;
+                out.done[g] = done_i;
+                out.status[g] = st_i;
+            }
+        }
+        if (tid == 0) {
+            if constexpr (STAGE) {
+                el.envw[0] = terminated;
+                el.envw[1] = truncated;
+                el.envw[2] = alive_cnt;
+                el.envw[3] = step_no;
+                el.envw[4] = (terminated || truncated) ? 1 : 0;
+                el.envw[5] = do_reset;
+            } else {
+                p.step_count[e] = step_no;
+                out.term[e] = terminated;
+                out.trunc[e] = truncated;
+                out.alive_cnt[e] = alive_cnt;
+                out.step[e] = step_no;
+                p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
+            }
+        }
+    }
+    // ---- the final ego state back to HBM (lane = agent); k_step's staged variant
+    // writes it at its end (fused_store)
+    if (!STAGE) {
+        for (int i = tid; i < N; i += WAVE) {
+            const int g = e * N + i;
+            egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
+            egof(p, EF_ACC)[g] = el.acc[i]; egof(p, EF_STEER)[g] = el.steer[i]; egoi(p, EF_PIDX)[g] = el.pidx[i];
+            egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
+            if (do_reset) {
+                egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
+                egoi(p, EF_INTENT)[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
+            }
+        }
+    }
     STAMPY(4);
     if (FUSED && MEV_PRIO_HEAD >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_HEAD < 0 ? 0 : MEV_PRIO_HEAD);
+#ifdef MEV_EXP_NOHEAD  // timing-only: no observation head
+    return;
+#endif
     // ---- observation head (:418-520)
     const int C = N + (TRAFFIC ? ncnt : 0);
     if (C <= 8) {
@@ -1215,7 +1273,9 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
     __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
     NpcLDS* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
-    cars_body<TRAFFIC, false>(p, in, out, e, el, nl);
+    const CarsCtx cx = cars_pre<TRAFFIC, false>(p, in, out, e, el, nl);
+    wave_lds_sync();
+    cars_post<TRAFFIC, false>(p, out, e, el, nl, cx);
 }
 
 // ------------------------------------------------------------- LiDAR ---
@@ -1336,23 +1396,27 @@ __host__ __device__ inline int lidar_cand_max(const SimParams& p) { return p.N -
 
 // with_bx: a per-segment copy of the obstacle box (k_lidar, whose boxes are in
 // HBM); k_step reads them from its own LDS obstacle table instead.
-__host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax, bool with_bx = true) {
-    LidarLayout L;
+// beams: capacity of the beam arrays (>= G * R).
+__host__ __device__ constexpr LidarLayout lidar_layout_beams(int G, int beams, int cmax, bool with_bx) {
+    LidarLayout L{};
     const int C = G * cmax;
     int off = 0;
     L.ag = off; off += G * 16;
-    L.dir = off; off += G * R * 8;
-    L.res = off; off += G * R * 4;
+    L.dir = off; off += beams * 8;
+    L.res = off; off += beams * 4;
     off = (off + 15) & ~15;
     L.seg_rg = off; off += C * 16;
     L.seg_bx = off; off += with_bx ? C * 16 : 0;
     L.seg_jo = off; off += C * 4;
     L.queue = L.seg_rg;
-    if (off < L.queue + G * R * 2) off = L.queue + G * R * 2;
+    if (off < L.queue + beams * 2) off = L.queue + beams * 2;
     off = (off + 15) & ~15;
     L.scr = off; off += WAVE * 4;  // the car phase's segment lookup (3c)
     L.bytes = (off + 15) & ~15;
     return L;
+}
+__host__ __device__ inline LidarLayout lidar_layout(int G, int R, int cmax, bool with_bx = true) {
+    return lidar_layout_beams(G, G * R, cmax, with_bx);
 }
 
 int lidar_group(int R) {
@@ -1942,6 +2006,37 @@ __host__ __device__ inline StepLayout step_layout(const SimParams& p) {
     return L;
 }
 
+// Compile-time LDS geometry (NM > 0): every array sized for its capacity --
+// N <= NM agents, R <= kFixedRays beams per agent, one LiDAR pool of <= 512
+// beams, no NPCs -- so each LDS address is a constant offset from the wave's
+// base instead of a runtime pointer held in an SGPR.  The ~40 runtime LDS
+// pointers of the NM = 0 layout made k_step spill 131 SGPRs into VGPR lanes
+// (a v_readlane per reload).
+constexpr int kFixedRays = 128;
+constexpr int kPoolBeams = 512;
+template <int NM>
+struct FixedLayout {
+    static_assert(NM >= 1 && NM <= 64, "agents per env");
+    static constexpr int cars = (int)lds_al(cars_lds_bytes(NM, 0));
+    static constexpr int rel = cars;
+    static constexpr int envw = rel + kFixedRays * 4;
+    static constexpr int lidar = envw + 32;
+    static constexpr LidarLayout lay = lidar_layout_beams(NM, kPoolBeams, NM - 1, false);
+    static constexpr int bytes = lidar + lay.bytes;
+};
+template <int NM>
+__host__ __device__ inline StepLayout step_layout_t(const SimParams& p) {
+    if constexpr (NM == 0) return step_layout(p);
+    else return StepLayout{FixedLayout<NM>::rel, FixedLayout<NM>::rel, FixedLayout<NM>::envw, FixedLayout<NM>::lidar,
+                           FixedLayout<NM>::bytes};
+}
+// the handle's shape fits the compile-time layout of NM agents
+template <int NM>
+__host__ __device__ inline bool fixed_fits(const SimParams& p) {
+    // R <= 128 puts every pool (step_pool agents) within kPoolBeams beams
+    return p.N <= NM && p.R <= kFixedRays && !p.traffic && !MEV_FUSED_STAGED && FixedLayout<NM>::bytes <= 10 * 1024;
+}
+
 // agents per phase-1 pass in k_step (independent dependency chains interleaved)
 #ifndef MEV_PHASE1_ILP
 #define MEV_PHASE1_ILP 2
@@ -1955,15 +2050,15 @@ __host__ __device__ inline StepLayout step_layout(const SimParams& p) {
 // whose env finishes its car logic early starts its LiDAR while other waves
 // on the SIMD are still in theirs.  The car part runs at a higher issue
 // priority: it is the latency-bound critical path of each wave.
-template <bool TRAFFIC, bool TAB>
+template <bool TRAFFIC, bool TAB, int NM>
 __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Outputs out) {
     extern __shared__ __align__(16) unsigned char step_lds[];
     const int e = blockIdx.x;
 #if defined(MEV_STAMPS_R)
     STAMP_RAW(0);
 #endif
-    const StepLayout sl = step_layout(p);
-    CarsLDS el = carve_cars_lds(step_lds, p.N, cars_k(p));
+    const StepLayout sl = step_layout_t<NM>(p);
+    CarsLDS el = NM ? carve_cars_lds(step_lds, NM, 0) : carve_cars_lds(step_lds, p.N, cars_k(p));
     el.head = reinterpret_cast<float*>(step_lds + sl.head);
     el.rel = reinterpret_cast<float*>(step_lds + sl.rel);
     el.envw = reinterpret_cast<int32_t*>(step_lds + sl.envw);
@@ -1971,13 +2066,21 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Ou
     NpcLDS* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
     if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
-    cars_body<TRAFFIC, true>(p, in, out, e, el, nl);
+    const CarsCtx cx = cars_pre<TRAFFIC, true>(p, in, out, e, el, nl);
     wave_lds_sync();
+#if !defined(MEV_EXP_STOP) || MEV_EXP_STOP != 0  // timing-only stop0: the car part without cars_post
+    if (!MEV_POST_AFTER_LIDAR) {
+        cars_post<TRAFFIC, true>(p, out, e, el, nl, cx);
+        wave_lds_sync();
+    }
+#else
+    return;
+#endif
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 1  // timing-only: the car part alone
     return;
 #endif
     const int G = step_pool(p);
-    const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p), false);
+    const LidarLayout lay = NM ? FixedLayout<(NM ? NM : 1)>::lay : lidar_layout(G, p.R, lidar_cand_max(p), false);
     unsigned char* lbase = step_lds + sl.lidar;
     const int lane = threadIdx.x & (WAVE - 1);
     const int g0 = e * p.N;
@@ -1986,6 +2089,10 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Ou
         if (j0 > 0 || MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);  // each pool
         const int na = p.N - j0 < G ? p.N - j0 : G;
         lidar_body<TAB, MEV_PHASE1_ILP>(p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
+    }
+    if (MEV_POST_AFTER_LIDAR) {  // experiment (variant postlate): measured slower, 41.6 -> 44.1 us
+        if (MEV_PRIO_POST >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_POST);
+        cars_post<TRAFFIC, true>(p, out, e, el, nl, cx);
     }
     if (MEV_FUSED_STAGED) {
         wave_lds_sync();
@@ -2118,9 +2225,15 @@ hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& 
     if (kind == 0) return hipErrorInvalidValue;
     if (kind == 2) {
         if (ev) (void)hipEventRecord(ev[0], s);
-        const unsigned lds = (unsigned)step_layout(p).bytes;
-        if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
-        else hipLaunchKernelGGL((k_step<false, false>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
+        if (fixed_fits<8>(p)) {  // compile-time LDS layout
+            const unsigned lds = (unsigned)FixedLayout<8>::bytes;
+            if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true, 8>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
+            else hipLaunchKernelGGL((k_step<false, false, 8>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
+        } else {
+            const unsigned lds = (unsigned)step_layout(p).bytes;
+            if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true, 0>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
+            else hipLaunchKernelGGL((k_step<false, false, 0>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
+        }
         hipError_t e = hipGetLastError();
         if (ev && e == hipSuccess) { (void)hipEventRecord(ev[1], s); (void)hipEventRecord(ev[2], s); }
         return e;

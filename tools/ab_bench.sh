@@ -6,6 +6,6 @@ set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for v in "$@"; do
   printf "variant %-10s " "${v:-product}"
-  MEV_LIB_VARIANT=$v timeout -k 10 120 python bench.py --no-cpu-baseline --steps 2000 --no-kernel-events |
+  MEV_LIB_VARIANT=$v timeout -k 10 120 python bench.py --no-cpu-baseline --no-gather --steps 2000 --no-kernel-events |
     python -c "import json,sys; d=json.load(sys.stdin); print(round(d['value']/1e6,1), 'M agent-steps/s', d['ms_per_step'], 'ms/step')"
 done
