@@ -57,6 +57,9 @@ struct mev_handle {
     hipStream_t stream = nullptr;
     std::vector<void*> allocs;
     mev::SimParams sp{};
+    mev::SimParams* d_sp = nullptr;  // device copy of sp read by k_step (refreshed when sp changes)
+    mev::SimParams sp_dev{};         // what d_sp holds
+    bool sp_valid = false;
     mev::Outputs internal{};
     mev::Outputs last{};  // where the most recent outputs were written
     float* d_actions = nullptr;
@@ -284,6 +287,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&h->d_paths, h->h_paths.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
     A(&h->d_rel, rel.size()); A(&h->d_traffic, size_t(h->P) * size_t(h->P));
     A(&h->d_reset_routes, size_t(h->P) * size_t(h->P));
+    A(reinterpret_cast<uint8_t**>(&h->d_sp), sizeof(mev::SimParams));
     float* d_dist = nullptr;
     if (!dist_mul_exact) A(&d_dist, dists.size());
     if (err != hipSuccess) {
@@ -340,7 +344,6 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     p.lidar_steps = int(dists.size());
     p.ob_stride = N + c.max_npcs;
     p.dist_tab = d_dist;
-    p.spawn_prob = 0.0f;
     p.seed = c.seed;
     p.rt.path = h->d_paths;
     p.rt.intent = h->d_intent;
@@ -624,7 +627,7 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         }
     }
     // spawn probability, TrafficFlow.cpp:321-322 (host glibc expf, bit-identical to the reference)
-    h->sp.spawn_prob = 1.0f - expf(-h->cfg.traffic_density * a->dt);
+    in.spawn_prob = 1.0f - expf(-h->cfg.traffic_density * a->dt);
     mev::Outputs o = resolve_outputs(h, a->obs, a->reward, a->done, a->status, a->terminated, a->truncated,
                                      a->agents_alive, a->step, dev);
     const int slot = int(h->gathers & 1);
@@ -646,7 +649,15 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         ev = &h->tev[size_t(3 * h->tn)];
         ++h->tn;
     }
-    HIP_TRY(mev::launch_step(h->sp, in, o, h->stream, ev));
+    if (!h->sp_valid || memcmp(&h->sp, &h->sp_dev, sizeof(mev::SimParams)) != 0) {
+        // parameters changed (configuration calls only): stream-ordered after the
+        // launches that read the previous copy; waited for, so the host copy is free
+        HIP_TRY(hipMemcpyAsync(h->d_sp, &h->sp, sizeof(mev::SimParams), hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        memcpy(&h->sp_dev, &h->sp, sizeof(mev::SimParams));
+        h->sp_valid = true;
+    }
+    HIP_TRY(mev::launch_step(h->sp, h->d_sp, in, o, h->stream, ev));
     h->last = o;
     if (gather && h->world == 1) {
         ++h->gathers;  // a world of one: the root's row is written in place, nothing to move

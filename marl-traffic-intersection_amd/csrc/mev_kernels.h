@@ -71,7 +71,6 @@ struct SimParams {
     float lidar_max, lidar_step, lidar_inv;
     int32_t lidar_steps;      // S = number of march probes (dist < max_dist)
     const float* dist_tab;    // [S] accumulated probe distances, or null when dist_k == k*step exactly
-    float spawn_prob;        // 1 - expf(-density * dt) computed on host with glibc
     uint64_t seed;
     EgoSoA ego;
     NpcSoA npc;
@@ -98,6 +97,7 @@ struct StepInputs {
     const float* actions;      // [E*N*2]
     const int32_t* spawn_route;  // [E] or null
     float dt;
+    float spawn_prob;          // 1 - expf(-density * dt) computed on host with glibc
     int32_t auto_reset;
     uint64_t rng_counter;      // handle-wide step counter (Philox counter for NPC spawns)
 };
@@ -108,8 +108,9 @@ struct StepInputs {
 int step_kernel_for(const SimParams& p);
 // ev (nullable): three events recorded before k_cars, between k_cars and k_lidar, after k_lidar
 // (with k_step: before it, and twice after it)
-hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
-                       const hipEvent_t* ev = nullptr);
+// dp: a device copy of p (k_step reads its parameters through it)
+hipError_t launch_step(const SimParams& p, const SimParams* dp, const StepInputs& in, const Outputs& out,
+                       hipStream_t s, const hipEvent_t* ev = nullptr);
 hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s,
                         uint64_t rng_counter);
 // recompute the observation rows from the current state with LiDAR = max (after set_state)

@@ -297,7 +297,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     } else if (p.n_traffic_routes > 0) {
         uint32_t a0, a1;
         philox((uint32_t)in.rng_counter, (uint32_t)(in.rng_counter >> 32), (uint32_t)e, p.seed, &a0, &a1);
-        if (u01(a0) < p.spawn_prob) {
+        if (u01(a0) < in.spawn_prob) {
             r = (int)(((uint64_t)a1 * (uint32_t)p.n_traffic_routes) >> 32);
         }
     }
@@ -2050,8 +2050,15 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // whose env finishes its car logic early starts its LiDAR while other waves
 // on the SIMD are still in theirs.  The car part runs at a higher issue
 // priority: it is the latency-bound critical path of each wave.
+// The parameters come through a device-resident copy (pp, refreshed by the
+// host only when they change) rather than by value: LLVM loads every kernel
+// argument in the entry block, so by value the ~130 dwords of SimParams stay
+// live through the whole kernel and the SGPR allocator spills them into VGPR
+// lanes (a v_readlane per reload); through the pointer each field is an s_load
+// next to its use.
 template <bool TRAFFIC, bool TAB, int NM>
-__global__ __launch_bounds__(WAVE, 4) void k_step(SimParams p, StepInputs in, Outputs out) {
+__global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
+    const SimParams& p = *pp;
     extern __shared__ __align__(16) unsigned char step_lds[];
     const int e = blockIdx.x;
 #if defined(MEV_STAMPS_R)
@@ -2219,20 +2226,20 @@ int step_kernel_for(const SimParams& p) {
     return (fusable && p.E >= 1024) ? 2 : 1;
 }
 
-hipError_t launch_step(const SimParams& p, const StepInputs& in, const Outputs& out, hipStream_t s,
-                       const hipEvent_t* ev) {
+hipError_t launch_step(const SimParams& p, const SimParams* dp, const StepInputs& in, const Outputs& out,
+                       hipStream_t s, const hipEvent_t* ev) {
     const int kind = step_kernel_for(p);
     if (kind == 0) return hipErrorInvalidValue;
     if (kind == 2) {
         if (ev) (void)hipEventRecord(ev[0], s);
         if (fixed_fits<8>(p)) {  // compile-time LDS layout
             const unsigned lds = (unsigned)FixedLayout<8>::bytes;
-            if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true, 8>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
-            else hipLaunchKernelGGL((k_step<false, false, 8>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
+            if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+            else hipLaunchKernelGGL((k_step<false, false, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
         } else {
             const unsigned lds = (unsigned)step_layout(p).bytes;
-            if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true, 0>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
-            else hipLaunchKernelGGL((k_step<false, false, 0>), dim3(p.E), dim3(WAVE), lds, s, p, in, out);
+            if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true, 0>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+            else hipLaunchKernelGGL((k_step<false, false, 0>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
         }
         hipError_t e = hipGetLastError();
         if (ev && e == hipSuccess) { (void)hipEventRecord(ev[1], s); (void)hipEventRecord(ev[2], s); }
