@@ -65,6 +65,8 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # exact variants: k_step's cars_post after the LiDAR (product: before it), at the LiDAR's last
                # issue priority or a fixed one
                "postlate": ["-DMEV_POST_AFTER_LIDAR=1"],
+               # exact variant: k_step's plain block -> env order (product: XCD-aware)
+               "noxcd": ["-DMEV_XCD_REMAP=0"],
                "post1": ["-DMEV_POST_AFTER_LIDAR=1", "-DMEV_PRIO_POST=1"],
                "post3": ["-DMEV_POST_AFTER_LIDAR=1", "-DMEV_PRIO_POST=3"],
                # exact variant: k_step stages every output in LDS and writes whole rows at the end

@@ -2056,11 +2056,27 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // live through the whole kernel and the SGPR allocator spills them into VGPR
 // lanes (a v_readlane per reload); through the pointer each field is an s_load
 // next to its use.
+// XCD-aware env order: the dispatcher deals workgroups round-robin over the 8
+// XCDs (block b -> XCD b % 8), and each XCD has its own L2.  An env's SoA
+// slices are 4 B x N per field (32 B at N = 8), so four consecutive envs share
+// every 128-B line; mapping block b to env (b % 8) * (E / 8) + b / 8 keeps
+// consecutive envs -- and their shared lines, and the partial lines between
+// their observation rows -- on one XCD instead of fetching/merging them in
+// four L2s.  (Placement is a performance hint only: any bijection is correct.)
+#ifndef MEV_XCD_REMAP
+#define MEV_XCD_REMAP 1
+#endif
+__device__ inline int xcd_env(int b, int E) {
+    if (!MEV_XCD_REMAP) return b;
+    const int q = E >> 3;
+    return b < 8 * q ? (b & 7) * q + (b >> 3) : b;
+}
+
 template <bool TRAFFIC, bool TAB, int NM>
 __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
     const SimParams& p = *pp;
     extern __shared__ __align__(16) unsigned char step_lds[];
-    const int e = blockIdx.x;
+    const int e = xcd_env((int)blockIdx.x, p.E);
 #if defined(MEV_STAMPS_R)
     STAMP_RAW(0);
 #endif

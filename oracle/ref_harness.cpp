@@ -181,6 +181,15 @@ int rh_add_car(void* p, const char* start, const char* end, int route_tag) {
     return 0;
 }
 
+// IntersectionEnv::set_state(get_state()) (cpp/IntersectionEnv.cpp:394-416): the
+// same cars, NPCs, ids and step count, and -- the point of the round trip --
+// every LiDAR object rebuilt as a default Lidar() (72 rays, cpp/Lidar.h:11).
+void rh_state_roundtrip(void* p) {
+    auto* h = static_cast<Harness*>(p);
+    const EnvState s = h->env.get_state();
+    h->env.set_state(s);
+}
+
 int rh_num_cars(void* p) { return int(static_cast<Harness*>(p)->env.cars.size()); }
 int rh_num_npcs(void* p) { return int(static_cast<Harness*>(p)->env.traffic_cars.size()); }
 int rh_step_count(void* p) { return static_cast<Harness*>(p)->env.step_count; }

@@ -45,6 +45,7 @@ def lib():
         L.rh_set_reward.argtypes = [vp, fp]
         L.rh_set_lidar.argtypes = [vp, i, f, f, f]
         L.rh_reset.argtypes = [vp]
+        L.rh_state_roundtrip.argtypes = [vp]
         L.rh_add_car.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, i]
         L.rh_num_cars.argtypes = [vp]
         L.rh_num_npcs.argtypes = [vp]
@@ -104,6 +105,15 @@ class RefEnv:
 
     def reset(self):
         lib().rh_reset(self.h)
+
+    def state_roundtrip(self):
+        """IntersectionEnv::set_state(get_state()): the LiDAR objects become default Lidar() (72 rays)."""
+        lib().rh_state_roundtrip(self.h)
+        self.rays = 72
+
+    @property
+    def step_count(self) -> int:
+        return lib().rh_step_count(self.h)
 
     def add_car(self, start: str, end: str, tag: int = -1) -> int:
         return lib().rh_add_car(self.h, start.encode(), end.encode(), int(tag))

@@ -7,8 +7,8 @@
  * compares with the golden outputs bit for bit; any sanitizer report aborts
  * the process (the CPU restatement under ASan/UBSan).
  *
- * Input (little-endian): int32 hdr[12] = {lanes, n, rays, obs_dim, use_team,
- * respawn, max_steps, traffic, max_npcs, steps, n_traffic_routes, n_npcs};
+ * Input (little-endian): int32 hdr[13] = {lanes, n, rays, obs_dim, use_team,
+ * respawn, max_steps, traffic, max_npcs, steps, n_traffic_routes, n_npcs, step_count};
  * float fhdr[10] = {density, dt, reward[8]}; int32 traffic_routes[n_tr];
  * orc_car egos[n]; orc_car npcs[n_npcs]; float actions[steps][n][2];
  * int32 spawned[steps].
@@ -26,7 +26,7 @@ int main(int argc, char** argv) {
     FILE* in = fopen(argv[1], "rb");
     FILE* out = fopen(argv[2], "wb");
     if (!in || !out) return 2;
-    int32_t h[12];
+    int32_t h[13];
     float fh[10];
     if (rd(in, h, sizeof h) || rd(in, fh, sizeof fh)) return 3;
     const int lanes = h[0], n = h[1], rays = h[2], obs_dim = h[3], steps = h[9], ntr = h[10], nnpc = h[11];
@@ -43,7 +43,7 @@ int main(int argc, char** argv) {
         rd(in, sp, sizeof(int32_t) * (size_t)steps))
         return 3;
     orc_set_traffic_routes(e, tr, ntr);
-    orc_set_state(e, egos, npcs, nnpc, 0);
+    orc_set_state(e, egos, npcs, nnpc, h[12]);
     const int D = e->obs_dim;
     float* obs = (float*)malloc(sizeof(float) * (size_t)n * (size_t)D);
     float* rew = (float*)malloc(sizeof(float) * (size_t)n);

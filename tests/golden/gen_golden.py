@@ -55,7 +55,7 @@ def policy(obs: np.ndarray, rng: np.random.Generator, target_v=3.5, noise=0.05) 
 def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_steps=2000,
         traffic=False, density=0.5, lanes=3, ego_routes=None, reward=None, steps=200,
         act="random", seed=0, dt=1.0 / 60.0, act_scale=1.0, zero_throttle_p=0.0,
-        inject=None, notes=""):
+        inject=None, notes="", warmup=0, roundtrip=False):
     routes = ROUTES3 if lanes == 3 else ROUTES2
     if ego_routes is None:
         ego_routes = [routes[i % len(routes)] for i in range(n_agents)]
@@ -68,6 +68,18 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
     rng = np.random.default_rng(seed)
     if inject is not None:
         inject(env, rng)
+    # unrecorded warm-up steps, then optionally IntersectionEnv::set_state(get_state())
+    # (cpp/IntersectionEnv.cpp:394-416): the recorded part starts from that state, with
+    # every LiDAR rebuilt as a default Lidar() of 72 rays (cpp/Lidar.h:11)
+    wobs = env.obs()
+    for t in range(warmup):
+        wa = (rng.uniform(-1.0, 1.0, (env.n, 2)) * act_scale).astype(np.float32) if act == "random" \
+            else policy(wobs, rng)
+        wobs = env.step(wa, dt)["obs"]
+    if roundtrip:
+        env.state_roundtrip()
+        rays = 72
+    init_step = env.step_count
     n = env.n
     ef, ei = env.cars(0)
     nf, ni = env.cars(1)
@@ -108,7 +120,7 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
     meta = dict(name=name, num_lanes=lanes, n_agents=n, rays=rays, use_team=bool(use_team and not traffic),
                 respawn=respawn, max_steps=max_steps, traffic=traffic, density=density,
                 reward=reward, ego_routes=ego_routes, traffic_routes=routes, dt=dt, steps=steps,
-                act=act, seed=seed, notes=notes)
+                act=act, seed=seed, notes=notes, init_step=init_step, warmup=warmup, set_state=bool(roundtrip))
     arrays = dict(
         meta=np.array(json.dumps(meta)),
         init_ego_f=ef, init_ego_i=ei, init_npc_f=nf.reshape(-1, R.NF), init_npc_i=ni.reshape(-1, R.NI),
@@ -212,7 +224,18 @@ def gen_static(lanes: int):
     print(f"static_lanes{lanes}: {len(pairs)} routes, grid on-road px={int((grid & 1).sum())}")
 
 
+def gen_set_state():
+    """set_state round trips (reference IntersectionEnv.cpp:404-416): 40 steps, then
+    get_state/set_state, then 60 recorded steps with the 72-ray default LiDAR."""
+    run("set_state_72_team", n_agents=8, rays=64, use_team=True, steps=60, act="policy", seed=20, warmup=40,
+        roundtrip=True)
+    run("set_state_72_n3", n_agents=3, rays=96, steps=60, act="random", seed=21, warmup=40, roundtrip=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--set-state":  # only the set_state scenarios
+        gen_set_state()
+        return
     gen_static(3)
     gen_static(2)
     # Config 1 shape: 1 env x 1 agent, 16 beams.
@@ -252,6 +275,7 @@ def main():
     for k in (2, 5, 9):
         run(f"inject_npc_k{k}", n_agents=1, rays=64, traffic=True, density=0.0, steps=150, act="policy",
             seed=300 + k, inject=inject_npcs(k))
+    gen_set_state()
 
 
 if __name__ == "__main__":

@@ -125,7 +125,7 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
             st["npc_intention"][b, :k] = ni[:, 1]
             st["npc_path_index"][b, :k] = ni[:, 2]
             st["npc_route"][b, :k] = [troutes[r] for r in ni[:, 3]]
-        st["step_count"][b] = 0
+        st["step_count"][b] = int(d["meta"].get("init_step", 0))  # set_state scenarios start mid-episode
     h.set_state(st)
     reports = [Report(nm) for nm in names]
     obs0 = h.observations()

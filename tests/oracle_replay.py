@@ -41,7 +41,7 @@ def replay(name):
     egos = state_from_records(d["init_ego_f"], d["init_ego_i"], ego_routes)
     k = len(d["init_npc_f"])
     npcs = state_from_records(d["init_npc_f"], d["init_npc_i"], [tr[r] for r in d["init_npc_i"][:, 3]]) if k else []
-    env.set_state(egos, npcs, 0)
+    env.set_state(egos, npcs, int(meta.get("init_step", 0)))
     errs = []
     if not G.bits_equal(env.observe()[:, :127], d["init_obs"]):
         errs.append("initial obs")

@@ -209,3 +209,40 @@ def test_rgb_array_render():
     assert (frame == np.array(render.EGO, np.uint8)).all(-1).sum() > 4 * 400  # four 54x24 cars
     assert (frame == np.array(render.HIT, np.uint8)).all(-1).any()
     e.close()
+
+
+@pytest.mark.parametrize("name", ["set_state_72_team", "set_state_72_n3"])
+def test_cpp_backend_set_state_replays_reference(name):
+    """The reference's set_state path (IntersectionEnv.cpp:404-416): a state taken
+    from a running env, set into a fresh one, then stepped -- every LiDAR is then a
+    default Lidar() of 72 rays (Lidar.h:11, Lidar.cpp:4-14).  Golden recorded from
+    the reference itself (tests/golden/gen_golden.py gen_set_state): the full
+    obs[127] (72 beams + 24 zeros), rewards, status and flags, bit for bit."""
+    g = G.load(name)
+    meta = g["meta"]
+    assert meta["set_state"] and meta["rays"] == 72
+    src = cpp_backend.IntersectionEnv(meta["num_lanes"])
+    src.reset()
+    for s, t in meta["ego_routes"]:
+        src.add_car_with_route(s, t)
+    snap = src.get_state()  # cars that carry their routes; the golden state goes into them
+    f, i = g["init_ego_f"], g["init_ego_i"]
+    for k, c in enumerate(snap.cars):
+        v = [float(x) for x in f[k]]
+        c.state.x, c.state.y, c.state.v, c.state.heading, c.acc, c.steering_angle = v[0:6]
+        c.spawn_state.x, c.spawn_state.y, c.spawn_state.v, c.spawn_state.heading = v[6:10]
+        c.prev_dist_to_goal, c.prev_action = v[10], (v[11], v[12])
+        c.alive, c.intention, c.path_index = bool(i[k, 0]), int(i[k, 1]), int(i[k, 2])
+    snap.step_count = int(meta["init_step"])
+    src.close()
+    env = cpp_backend.IntersectionEnv(meta["num_lanes"])
+    env.configure(meta["use_team"], meta["respawn"], meta["max_steps"])
+    env.set_state(snap)
+    assert env.lidars[0].rays == 72
+    assert G.bits_equal(env.get_observations(), g["init_obs"])  # 72 x 1.0, then zeros
+    for t in range(len(g["actions"])):
+        a = g["actions"][t]
+        res = env.step(a[:, 0].tolist(), a[:, 1].tolist(), meta["dt"])
+        info = dict(agents_alive=res.agents_alive, step=res.step, status=res.status, done=res.done)
+        _check_step(name, g, t, res.obs, res.rewards, res.terminated, res.truncated, info)
+    env.close()

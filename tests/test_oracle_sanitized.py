@@ -19,7 +19,8 @@ EXE = os.path.join(ORACLE, "_build", "sanitize_replay")
 # a spread of the golden set: single agent, team/8 agents, ties, traffic with spawns, NPC fleets, 128 beams,
 # custom reward + dt, 2 lanes, truncation, unclipped actions
 SCENARIOS = ["cfg1_r16_random", "cfg3_team_random_s0", "n16_r96_ties", "traffic_d20", "inject_npc_k9",
-             "cfg5_r128_team", "dt_1_30_custom_reward", "lanes2_policy", "truncate_50", "unclipped_x3"]
+             "cfg5_r128_team", "dt_1_30_custom_reward", "lanes2_policy", "truncate_50", "unclipped_x3",
+             "set_state_72_team"]
 
 
 @pytest.fixture(scope="module")
@@ -52,7 +53,8 @@ def _write_input(path, name):
         else np.zeros(0, R.O.CAR_DTYPE)
     steps = int(meta["steps"])
     hdr = np.array([L, n, rays, obs_dim, int(bool(meta["use_team"])), int(bool(meta["respawn"])),
-                    int(meta["max_steps"]), int(bool(meta["traffic"])), 64, steps, len(tr), k], np.int32)
+                    int(meta["max_steps"]), int(bool(meta["traffic"])), 64, steps, len(tr), k,
+                    int(meta.get("init_step", 0))], np.int32)
     fh = np.concatenate([[np.float32(meta["density"]), np.float32(meta["dt"])],
                          np.asarray(meta["reward"], np.float32)]).astype(np.float32)
     spawned = np.asarray(d["spawned"], np.int32) if meta["traffic"] else np.full(steps, -1, np.int32)
