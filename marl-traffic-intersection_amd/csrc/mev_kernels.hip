@@ -247,6 +247,22 @@ __device__ inline int path_index_update(const float* path, int idx, float x, flo
     return best == 0x7fffffff ? start_i : best;
 }
 
+// XCD-aware env order: the dispatcher deals workgroups round-robin over the 8
+// XCDs (block b -> XCD b % 8), and each XCD has its own L2.  An env's SoA
+// slices are 4 B x N per field (32 B at N = 8), so four consecutive envs share
+// every 128-B line; mapping block b to env (b % 8) * (E / 8) + b / 8 keeps
+// consecutive envs -- and their shared lines, and the partial lines between
+// their observation rows -- on one XCD instead of fetching/merging them in
+// four L2s.  (Placement is a performance hint only: any bijection is correct.)
+#ifndef MEV_XCD_REMAP
+#define MEV_XCD_REMAP 1
+#endif
+__device__ inline int xcd_env(int b, int E) {
+    if (!MEV_XCD_REMAP) return b;
+    const int q = E >> 3;
+    return b < 8 * q ? (b & 7) * q + (b >> 3) : b;
+}
+
 // -------------------------------------------------------- shared state ---
 struct EgoLDS {
     float x[MAXN], y[MAXN], v[MAXN], h[MAXN], c[MAXN], s[MAXN];
@@ -264,30 +280,85 @@ struct NpcLDS {
     uint8_t alive[MAXK];
     float cx[MAXK][4], cy[MAXK][4];
     unsigned long long col[MAXK];
-    uint8_t pair_ok[MAXK], yield_far[MAXK];
-    float2 path[2][PATH_LEN];  // the route of the NPC being controlled (double buffered)
+    // the controller's per-NPC terms that depend on its own start-of-step state only
+    int32_t pidx0[MAXK];          // after the first update_path_index of its turn
+    float nsteer[MAXK], ntan[MAXK];  // Car::update's new steering angle and its tangent
+    float accb[MAXK], mdc[MAXK];  // cruise throttle, distance to the centre
+    float endx[MAXK], endy[MAXK];  // the route's last point (arrival test)
+};
+
+// One NPC slot's state in the registers of lane = slot, loaded together with the
+// ego state (one round of loads) and handed to npc_phase.
+struct NpcRegs {
+    float x, y, v, h, acc, steer;
+    int32_t pidx, route, intent;
+    uint8_t alive;
 };
 
 
 // --------------------------------------------------- NPC traffic phase ---
 // update_traffic_flow, cpp/TrafficFlow.cpp:317-367, for env e.  Egos (positions
 // in LDS) are read for spawn blocking but not moved.  On return NpcLDS holds the compacted NPCs.
+__device__ inline NpcRegs npc_load(const SimParams& p, int e, int lane) {
+    NpcRegs r{};
+    if (lane < p.K) {
+        const int g = e * p.K + lane;
+        r.x = npcf(p, NF_X)[g]; r.y = npcf(p, NF_Y)[g]; r.v = npcf(p, NF_V)[g]; r.h = npcf(p, NF_H)[g];
+        r.acc = npcf(p, NF_ACC)[g]; r.steer = npcf(p, NF_STEER)[g];
+        r.pidx = npci(p, NF_PIDX)[g]; r.route = npci(p, NF_ROUTE)[g]; r.intent = npci(p, NF_INTENT)[g];
+        r.alive = p.npc.alive[g];
+    }
+    return r;
+}
+
+// (d, i) pairs: the minimum d over the wave, ties to the smaller i (DPP within
+// each 16-lane row, then the four row results compared as scalars); wave-uniform
+__device__ inline int wave_argmin_dpp(float d, int i) {
+    auto take = [&](float od, int oi) {
+        if (od < d || (od == d && oi < i)) { d = od; i = oi; }
+    };
+    take(dpp_f(d, 0xB1), __builtin_amdgcn_mov_dpp(i, 0xB1, 0xf, 0xf, false));    // quad_perm [1,0,3,2]
+    take(dpp_f(d, 0x4E), __builtin_amdgcn_mov_dpp(i, 0x4E, 0xf, 0xf, false));    // quad_perm [2,3,0,1]
+    take(dpp_f(d, 0x141), __builtin_amdgcn_mov_dpp(i, 0x141, 0xf, 0xf, false));  // row_half_mirror
+    take(dpp_f(d, 0x140), __builtin_amdgcn_mov_dpp(i, 0x140, 0xf, 0xf, false));  // row_mirror
+    float bd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), 0));
+    int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+    for (int r = 16; r < WAVE; r += 16) {
+        const float od = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), r));
+        const int oi = __builtin_amdgcn_readlane(i, r);
+        if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+    }
+    return bi;
+}
+
+// Diagnostic build only (-DMEV_STAMPS_N): cycles spent in each part of the NPC
+// phase, accumulated over the turns and written to SimParams::debug[e*8 + part]
+// (tools/npc_profile.py --parts); never compiled into the product library.
+#ifdef MEV_STAMPS_N
+#define NT(k)                                                                  \
+    do {                                                                       \
+        __builtin_amdgcn_wave_barrier();                                       \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();            \
+        nt_acc[k] += t_ - nt_prev;                                             \
+        nt_prev = t_;                                                          \
+    } while (0)
+#else
+#define NT(k) do {} while (0)
+#endif
+
 __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NpcLDS& nl, int lane,
-                          const float* ego_x, const float* ego_y) {
+                          const float* ego_x, const float* ego_y, const NpcRegs& nr) {
     const int K = p.K;
-    // load
+#ifdef MEV_STAMPS_N
+    unsigned long long nt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long nt_prev = __builtin_amdgcn_s_memtime();
+#endif
+    // state -> LDS (loaded with the ego state)
     if (lane < cnt) {
-        const int g = e * K + lane;
-        nl.x[lane] = npcf(p, NF_X)[g];
-        nl.y[lane] = npcf(p, NF_Y)[g];
-        nl.v[lane] = npcf(p, NF_V)[g];
-        nl.h[lane] = npcf(p, NF_H)[g];
-        nl.acc[lane] = npcf(p, NF_ACC)[g];
-        nl.steer[lane] = npcf(p, NF_STEER)[g];
-        nl.pidx[lane] = npci(p, NF_PIDX)[g];
-        nl.route[lane] = npci(p, NF_ROUTE)[g];
-        nl.intent[lane] = npci(p, NF_INTENT)[g];
-        nl.alive[lane] = p.npc.alive[g];
+        nl.x[lane] = nr.x; nl.y[lane] = nr.y; nl.v[lane] = nr.v; nl.h[lane] = nr.h;
+        nl.acc[lane] = nr.acc; nl.steer[lane] = nr.steer;
+        nl.pidx[lane] = nr.pidx; nl.route[lane] = nr.route; nl.intent[lane] = nr.intent; nl.alive[lane] = nr.alive;
     }
     // -- spawn (TrafficFlow.cpp:320-329, try_spawn_traffic_car :275-315)
     int r = -1;
@@ -356,30 +427,103 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     }
     wave_lds_sync();
 
-    // -- sequential controller over NPCs in vector order (Gauss-Seidel, :337-344).
-    // Each NPC's route is staged in LDS (one round trip, prefetched during the
-    // previous NPC), so the path-index windows, the look-ahead target and the
-    // 120-point ghost scan read no global memory.
+    NT(0);  // state -> LDS, spawn
+    // -- controller (:331-344): update_path_index, plan_npc_action_tf, Car::update,
+    // update_path_index per NPC in vector order, each NPC planning against the
+    // others' CURRENT states (Gauss-Seidel: the ones before it already moved).
+    // Everything a turn needs from the NPC's own start-of-step state -- which no
+    // earlier turn changes -- is computed first for all NPCs at once (part 1), and
+    // the second update_path_index, which no later turn reads, after the loop
+    // (part 3); the sequential loop keeps only what depends on the others.
     const float CXf = WIDTH * 0.5f, CYf = HEIGHT * 0.5f;
-    constexpr int PPL = (PATH_LEN + WAVE - 1) / WAVE;  // route points per lane
-    float2 pre[PPL];
-    auto fetch_route = [&](int kk) {  // issue the loads of NPC kk's route (or nothing)
-        if (kk >= cnt) return;
-        const float2* g = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+    const int grp = lane >> 3, sub = lane & 7;
+    // path_index_update (Car.cpp:47-74) for NPCs k0 .. k0 + 7 at once (8 lanes
+    // each, 8 window points per lane, first minimum wins); returns the new index
+    // and leaves the 64-point window in pt
+    auto npc_window = [&](int kk, int idx, float x, float y, float2* pt, int& start_i) -> int {
+        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        start_i = idx < 0 ? 0 : idx;
+        const int wcnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
 #pragma unroll
-        for (int u = 0; u < PPL; ++u) {
-            const int i = lane + u * WAVE;
-            if (i < PATH_LEN) pre[u] = g[i];
+        for (int j = 0; j < 8; ++j) {
+            const int q = start_i + sub * 8 + j;
+            pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
         }
-    };
-    auto stage_route = [&](int buf) {
+        float bd = __builtin_inff();
+        int bi = 0x7fffffff;
 #pragma unroll
-        for (int u = 0; u < PPL; ++u) {
-            const int i = lane + u * WAVE;
-            if (i < PATH_LEN) nl.path[buf][i] = pre[u];
+        for (int j = 0; j < 8; ++j) {
+            const int off = sub * 8 + j;
+            if (off < wcnt) {
+                const float dx = pt[j].x - x, dy = pt[j].y - y;
+                const float d = dx * dx + dy * dy;
+                if (d < bd) { bd = d; bi = start_i + off; }
+            }
         }
+        auto take = [&](float od, int oi) {
+            if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+        };
+        take(dpp_f(bd, 0xB1), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xf, 0xf, false));    // quad_perm [1,0,3,2]
+        take(dpp_f(bd, 0x4E), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xf, 0xf, false));    // quad_perm [2,3,0,1]
+        take(dpp_f(bd, 0x141), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xf, 0xf, false));  // row_half_mirror
+        return bi == 0x7fffffff ? start_i : bi;
     };
-    fetch_route(0);
+    // part 1: the first path index, the steering command towards path[idx + 12]
+    // (:50-63) and Car::update's steering part with its tangent (Car.cpp:11-23;
+    // the steering input is known before the throttle), the cruise throttle
+    // (:66-70) and the distance to the centre (:83)
+    for (int k0 = 0; k0 < cnt; k0 += 8) {
+        const int k = k0 + grp;
+        const bool act = k < cnt;
+        const int kk = act ? k : 0;  // idle groups mirror NPC 0 so every lane reaches the DPP moves
+        const float x = nl.x[kk], y = nl.y[kk];
+        float2 pt[8];
+        int start_i;
+        const int pidx0 = npc_window(kk, nl.pidx[kk], x, y, pt, start_i);
+        // the look-ahead point min(pidx0 + 12, 159) lies in the 64-point window
+        const int tidx = pidx0 + 12 < PATH_LEN - 1 ? pidx0 + 12 : PATH_LEN - 1;
+        const int toff = tidx - start_i;
+        if (act && sub == (toff >> 3)) {
+            float2 t = pt[0];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) t = ((toff & 7) == j) ? pt[j] : t;
+            const float h = nl.h[k], v = nl.v[k];
+            const float tdx = t.x - x;
+            const float tdy = t.y - y;
+            const float heading_err = wrap_angle(atan2f(-tdy, tdx) - h);
+            float steer_cmd = heading_err * 3.0f;
+            steer_cmd = (1.0f < steer_cmd) ? 1.0f : steer_cmd;    // std::min(1, .)
+            steer_cmd = (steer_cmd < -1.0f) ? -1.0f : steer_cmd;  // std::max(-1, .)
+            const float ns = car_steer(nl.steer[k], steer_cmd);
+            nl.nsteer[k] = ns;
+            nl.ntan[k] = tanf(ns);
+            const float target_speed = PHYSICS_MAX_SPEED * 0.4f;
+            nl.accb[k] = (v < target_speed) ? 0.5f : ((v > target_speed + 1.0f) ? -0.1f : 0.0f);
+            nl.mdc[k] = hypotf(x - CXf, y - CYf);
+            nl.pidx0[k] = pidx0;
+        }
+        if (act && sub == 7) {  // the route's end point, for the arrival test after the turns
+            const float2 pe = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[k] * (2 * PATH_LEN))[PATH_LEN - 1];
+            nl.endx[k] = pe.x;
+            nl.endy[k] = pe.y;
+        }
+    }
+    wave_lds_sync();
+    NT(1);  // part 1
+    // part 2: the turns in vector order.  Lane j holds the other NPC j; the front-car
+    // and ghost-scan tests need only thresholds, so they are ballots, not reductions.
+    const float SAFE = CAR_WIDTH * 2.0f;
+    const float SAFE_SQ = SAFE * SAFE;
+    // NPC kk's ghost points path[idx0 + lane] and path[idx0 + 64 + lane] (clamped;
+    // only indices below min(idx0 + 120, 160) are used), loaded one turn ahead
+    auto fetch_ghost = [&](int kk, float2& a, float2& b) {
+        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const int i0 = nl.pidx0[kk] + lane, i1 = i0 + WAVE;
+        a = P[i0 < PATH_LEN ? i0 : PATH_LEN - 1];
+        b = P[i1 < PATH_LEN ? i1 : PATH_LEN - 1];
+    };
+    float2 ga = make_float2(0.0f, 0.0f), gb = ga;
+    if (cnt > 0) fetch_ghost(0, ga, gb);
     for (int k = 0; k < cnt; ++k) {
         if (MEV_NPC_PRIO) {  // the env with the most NPCs left to control sets the kernel's end: serve it first
             const int rem = cnt - k;
@@ -388,162 +532,156 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             else if (rem >= MEV_NPC_PRIO) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
-        stage_route(k & 1);
-        wave_lds_sync();
-        fetch_route(k + 1);  // in flight while NPC k is controlled
-        if (!nl.alive[k]) continue;
-        const float* path = reinterpret_cast<const float*>(nl.path[k & 1]);
-        float x = nl.x[k], y = nl.y[k];
-        int pidx = path_index_update(path, nl.pidx[k], x, y, lane);
-        const float h = nl.h[k], v = nl.v[k];
-        const float ck = nl.c[k], sk = nl.s[k];
-
-        // plan_npc_action_tf (:49-196) — 1) lateral
-        int tidx = pidx + 12;
-        if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
-        const float tdx = path[2 * tidx] - x;
-        const float tdy = path[2 * tidx + 1] - y;
-        const float heading_err = wrap_angle(atan2f(-tdy, tdx) - h);
-        float steer_cmd = heading_err * 3.0f;
-        steer_cmd = (1.0f < steer_cmd) ? 1.0f : steer_cmd;  // std::min(1, .)
-        steer_cmd = (steer_cmd < -1.0f) ? -1.0f : steer_cmd;  // std::max(-1, .)
-        // 2) longitudinal cruise + front car (get_front_car_dist_tf :22-47)
-        const float target_speed = PHYSICS_MAX_SPEED * 0.4f;
-        float acc_thr = 0.0f;
-        if (v < target_speed) acc_thr = 0.5f;
-        else if (v > target_speed + 1.0f) acc_thr = -0.1f;
-        const float vx = ck, vy = -sk;
-        float fd = 1e9f;
-        const int j = lane;
-        bool jvalid = j < cnt && j != k && nl.alive[j];
-        float oxj = 0, oyj = 0, ohj = 0, ovj = 0, ocj = 0, osj = 0;
-        if (j < cnt) {
-            oxj = nl.x[j]; oyj = nl.y[j]; ohj = nl.h[j]; ovj = nl.v[j]; ocj = nl.c[j]; osj = nl.s[j];
-        }
-        if (jvalid) {
-            const float dx = oxj - x;
-            const float dy = oyj - y;
-            const float dist = hypotf(dx, dy);
-            if (!(dist > 80.0f)) {
-                const float dot = (dx * vx + dy * vy) / (dist + 1e-5f);
-                if (dot > 0.8f) {
-                    const float angle_diff = fabs_f(wrap_angle(h - ohj));
-                    if (angle_diff < (45.0f * PI_F / 180.0f)) fd = dist;
+        float2 na = ga, nb = gb;
+        if (k + 1 < cnt) fetch_ghost(k + 1, na, nb);  // in flight while NPC k is controlled
+        if (nl.alive[k]) {
+            const float x = nl.x[k], y = nl.y[k], h = nl.h[k], v = nl.v[k];
+            const float ck = nl.c[k], sk = nl.s[k];
+            const int j = lane;
+            const bool jvalid = j < cnt && j != k && nl.alive[j];
+            float oxj = 0, oyj = 0, ohj = 0, ovj = 0, ocj = 0, osj = 0;
+            if (j < cnt) {
+                oxj = nl.x[j]; oyj = nl.y[j]; ohj = nl.h[j]; ovj = nl.v[j]; ocj = nl.c[j]; osj = nl.s[j];
+            }
+            // 2) front car (get_front_car_dist_tf :22-47, used as front < 30 / < 50 at :72-73)
+            const float vx = ck, vy = -sk;
+            bool f30 = false, f50 = false;
+            // |wrap(h - h_j)| and the distance to j: shared by the front-car test and the
+            // ghost-scan filters (the same expressions in the reference, :37/:101/:107)
+            const float dxj = oxj - x;
+            const float dyj = oyj - y;
+            const float dist_j = hypotf(dxj, dyj);
+            const float adiff_j = fabs_f(wrap_angle(h - ohj));
+            if (jvalid) {
+                const float dist = dist_j;
+                if (!(dist > 80.0f)) {
+                    const float dot = (dxj * vx + dyj * vy) / (dist + 1e-5f);
+                    if (dot > 0.8f) {
+                        if (adiff_j < (45.0f * PI_F / 180.0f)) { f30 = dist < 30.0f; f50 = dist < 50.0f; }
+                    }
                 }
             }
-        }
-        fd = wave_min(fd);
-        if (fd < 30.0f) acc_thr = -1.0f;
-        else if (fd < 50.0f) acc_thr = (-0.2f < acc_thr) ? -0.2f : acc_thr;
-
-        // 3) ghost path scan: per-other terms first (independent of the ghost point)
-        const float my_dist_to_center = hypotf(x - CXf, y - CYf);
-        uint8_t pok = 0, yfar = 0;
-        if (jvalid) {
-            const float angle_diff = fabs_f(wrap_angle(h - ohj));
-            pok = 1;
-            if (angle_diff < (60.0f * PI_F / 180.0f)) pok = 0;
-            if (pok) {
-                const float dxo = oxj - x;
-                const float dyo = oyj - y;
-                const float dist_o = hypotf(dxo, dyo);
-                if (dist_o > 1e-5f) {
-                    const float mdx = ck, mdy = -sk;
-                    const float two_pi_m = 2.0f * PI_F - angle_diff;
-                    const float adn = (two_pi_m < angle_diff) ? two_pi_m : angle_diff;
-                    const bool parallel = (adn < (30.0f * PI_F / 180.0f)) || (adn > (150.0f * PI_F / 180.0f));
-                    if (parallel) {
-                        const float lon = dxo * mdx + dyo * mdy;
-                        float lsq = dist_o * dist_o - lon * lon;
-                        lsq = (0.0f < lsq) ? lsq : 0.0f;  // std::max(0, .)
-                        const float lat = __builtin_sqrtf(lsq);
-                        const bool sideways = fabs_f(lat) < (LANE_WIDTH_PX * 1.5f);
-                        const bool near_lon = fabs_f(lon) < (CAR_LENGTH * 2.0f);
-                        if (sideways && near_lon) {
-                            const float fdist = 20.0f;
-                            const float mfx = x + mdx * fdist;
-                            const float mfy = y + mdy * fdist;
-                            const float odx = ocj, ody = -osj;
-                            const float ofx = oxj + odx * fdist;
-                            const float ofy = oyj + ody * fdist;
-                            const float fdx = ofx - mfx;
-                            const float fdy = ofy - mfy;
-                            const float fmag = hypotf(fdx, fdy);
-                            if (fmag > 1e-5f) {
-                                const float flon = fdx * mdx + fdy * mdy;
-                                float flsq = fmag * fmag - flon * flon;
-                                flsq = (0.0f < flsq) ? flsq : 0.0f;
-                                const float flat = __builtin_sqrtf(flsq);
-                                const float change = fabs_f(flat - lat);
-                                if (change < (LANE_WIDTH_PX * 0.5f)) pok = 0;  // side by side: skip
+            NT(2);  // turn: LDS reads, front car
+            float acc_thr = nl.accb[k];
+            if (ballot(f30)) acc_thr = -1.0f;
+            else if (ballot(f50)) acc_thr = (-0.2f < acc_thr) ? -0.2f : acc_thr;
+            // 3) ghost path scan: the per-other filters first (independent of the ghost point)
+            const float my_dist_to_center = nl.mdc[k];
+            bool pok = false, yfar = false;
+            if (jvalid) {
+                const float angle_diff = adiff_j;
+                pok = true;
+                if (angle_diff < (60.0f * PI_F / 180.0f)) pok = false;
+                if (pok) {
+                    const float dxo = dxj;
+                    const float dyo = dyj;
+                    const float dist_o = dist_j;
+                    if (dist_o > 1e-5f) {
+                        const float mdx = ck, mdy = -sk;
+                        const float two_pi_m = 2.0f * PI_F - angle_diff;
+                        const float adn = (two_pi_m < angle_diff) ? two_pi_m : angle_diff;
+                        const bool parallel = (adn < (30.0f * PI_F / 180.0f)) || (adn > (150.0f * PI_F / 180.0f));
+                        if (parallel) {
+                            const float lon = dxo * mdx + dyo * mdy;
+                            float lsq = dist_o * dist_o - lon * lon;
+                            lsq = (0.0f < lsq) ? lsq : 0.0f;  // std::max(0, .)
+                            const float lat = __builtin_sqrtf(lsq);
+                            const bool sideways = fabs_f(lat) < (LANE_WIDTH_PX * 1.5f);
+                            const bool near_lon = fabs_f(lon) < (CAR_LENGTH * 2.0f);
+                            if (sideways && near_lon) {
+                                const float fdist = 20.0f;
+                                const float mfx = x + mdx * fdist;
+                                const float mfy = y + mdy * fdist;
+                                const float odx = ocj, ody = -osj;
+                                const float ofx = oxj + odx * fdist;
+                                const float ofy = oyj + ody * fdist;
+                                const float fdx = ofx - mfx;
+                                const float fdy = ofy - mfy;
+                                const float fmag = hypotf(fdx, fdy);
+                                if (fmag > 1e-5f) {
+                                    const float flon = fdx * mdx + fdy * mdy;
+                                    float flsq = fmag * fmag - flon * flon;
+                                    flsq = (0.0f < flsq) ? flsq : 0.0f;
+                                    const float flat = __builtin_sqrtf(flsq);
+                                    const float change = fabs_f(flat - lat);
+                                    if (change < (LANE_WIDTH_PX * 0.5f)) pok = false;  // side by side: skip
+                                }
                             }
                         }
                     }
                 }
-            }
-            if (pok) {
-                const float odc = hypotf(oxj - CXf, oyj - CYf);
-                if (v < 1.0f && ovj > 3.0f && odc < my_dist_to_center + 25.0f) yfar = 1;
-                else if (odc < my_dist_to_center - 5.0f) yfar = 1;
-                else if (fabs_f(odc - my_dist_to_center) <= 5.0f) yfar = (k < j) ? 1 : 0;  // address order
-            }
-        }
-        if (j < MAXK) {
-            nl.pair_ok[j] = pok;
-            nl.yield_far[j] = yfar;
-        }
-        wave_lds_sync();
-        // scan ghost points path[pidx, min(pidx+120, 160)); first conflicting point wins
-        const int g_start = pidx;
-        int g_end = pidx + 120;
-        if (g_end > PATH_LEN) g_end = PATH_LEN;
-        const float SAFE = CAR_WIDTH * 2.0f;
-        const float SAFE_SQ = SAFE * SAFE;
-        bool conflict = false;
-        float min_conflict = 1e9f;
-        for (int base = g_start; base < g_end; base += WAVE) {
-            const int gi = base + lane;
-            bool hit = false;
-            float dtc = 0.0f;
-            if (gi < g_end) {
-                const float gx = path[2 * gi], gy = path[2 * gi + 1];
-                dtc = hypotf(gx - x, gy - y);
-                for (int o = 0; o < cnt; ++o) {
-                    if (!nl.pair_ok[o]) continue;
-                    const float dxg = nl.x[o] - gx;
-                    const float dyg = nl.y[o] - gy;
-                    if (dxg * dxg + dyg * dyg < SAFE_SQ && (dtc < 15.0f || nl.yield_far[o])) { hit = true; break; }
+                if (pok) {
+                    const float odc = hypotf(oxj - CXf, oyj - CYf);
+                    if (v < 1.0f && ovj > 3.0f && odc < my_dist_to_center + 25.0f) yfar = true;
+                    else if (odc < my_dist_to_center - 5.0f) yfar = true;
+                    else if (fabs_f(odc - my_dist_to_center) <= 5.0f) yfar = k < j;  // address order
                 }
             }
-            const unsigned long long m = ballot(hit);
-            if (m) {
-                const int first = __builtin_ctzll(m);
-                min_conflict = __shfl(dtc, first);
-                conflict = true;
-                break;
+            const unsigned long long em = ballot(pok), ym = ballot(yfar);
+            NT(3);  // turn: ghost-scan filters
+            // scan path[idx0, min(idx0 + 120, 160)) in order; the first point with a
+            // yielding conflict wins (its distance is the min, :183-188); only the
+            // others that passed the filters take part (usually none)
+            bool conflict = false;
+            float min_conflict = 1e9f;
+            if (em) {
+                const int g_start = nl.pidx0[k];
+                const int g_end = g_start + 120 < PATH_LEN ? g_start + 120 : PATH_LEN;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    if (conflict || g_start + c * WAVE >= g_end) break;
+                    const float2 gp = c ? gb : ga;
+                    const bool gv = g_start + c * WAVE + lane < g_end;
+                    const float dtc = hypotf(gp.x - x, gp.y - y);
+                    bool hit = false;
+                    for (unsigned long long mm = em; mm; mm &= mm - 1ull) {
+                        const int o = __builtin_ctzll(mm);
+                        const float ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(oxj), o));
+                        const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(oyj), o));
+                        const float dxg = ox - gp.x;
+                        const float dyg = oy - gp.y;
+                        if (dxg * dxg + dyg * dyg < SAFE_SQ && (dtc < 15.0f || ((ym >> o) & 1ull))) hit = true;
+                    }
+                    const unsigned long long m = ballot(gv && hit);
+                    if (m) {
+                        min_conflict = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dtc), __builtin_ctzll(m)));
+                        conflict = true;
+                    }
+                }
             }
+            NT(4);  // turn: ghost scan
+            // 4) compose (:190-195), then Car::update with the steering part from part 1
+            float thr = acc_thr;
+            if (conflict) {
+                if (min_conflict < 35.0f) thr = -1.0f;
+                else if (min_conflict < 60.0f) thr = -0.8f;
+                else thr = (0.0f < thr) ? 0.0f : thr;
+            }
+            Kin kin{x, y, v, h, nl.acc[k], nl.steer[k]};
+            float cn, sn;
+            car_update_steered(kin, thr, nl.nsteer[k], nl.ntan[k], in.dt, &cn, &sn);
+            // the second update_path_index (:343) over path[idx0, idx0 + 50): lane i holds
+            // path[idx0 + i] among the ghost points; no later turn reads it
+            const int pidx0 = nl.pidx0[k];
+            const bool wv = lane < 50 && pidx0 + lane < PATH_LEN;
+            const float wdx = ga.x - kin.x, wdy = ga.y - kin.y;
+            const int best = wave_argmin_dpp(wv ? wdx * wdx + wdy * wdy : __builtin_inff(),
+                                             wv ? pidx0 + lane : 0x7fffffff);
+            const int pidx_new = best == 0x7fffffff ? (pidx0 < 0 ? 0 : pidx0) : best;
+            NT(5);  // turn: Car::update + second path index
+            wave_lds_sync();  // every lane has read this turn's states
+            if (lane == 0) {
+                nl.x[k] = kin.x; nl.y[k] = kin.y; nl.v[k] = kin.v; nl.h[k] = kin.h;
+                nl.acc[k] = kin.acc; nl.steer[k] = kin.steer;
+                nl.c[k] = cn; nl.s[k] = sn;
+                nl.pidx[k] = pidx_new;
+            }
+            wave_lds_sync();
+            NT(6);  // turn: write back
         }
-        // 4) compose
-        float thr = acc_thr;
-        if (conflict) {
-            if (min_conflict < 35.0f) thr = -1.0f;
-            else if (min_conflict < 60.0f) thr = -0.8f;
-            else thr = (0.0f < thr) ? 0.0f : thr;
-        }
-        // Car::update + second path-index update (:342-343); every lane computes it redundantly
-        Kin kin{x, y, v, h, nl.acc[k], nl.steer[k]};
-        float cn, sn;
-        car_update(kin, thr, steer_cmd, in.dt, &cn, &sn);
-        pidx = path_index_update(path, pidx, kin.x, kin.y, lane);
-        wave_lds_sync();
-        if (lane == 0) {
-            nl.x[k] = kin.x; nl.y[k] = kin.y; nl.v[k] = kin.v; nl.h[k] = kin.h;
-            nl.acc[k] = kin.acc; nl.steer[k] = kin.steer; nl.pidx[k] = pidx;
-            nl.c[k] = cn; nl.s[k] = sn;
-        }
-        wave_lds_sync();
+        ga = na;
+        gb = nb;
     }
-
     // -- NPC-NPC collision: greedy i<j, both removed (:347-356)
     if (lane < cnt) {
         car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
@@ -568,8 +706,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // -- erase dead / arrived / out-of-screen, order preserving (:359-366)
     bool keep = false;
     if (lane < cnt && ((alive_m >> lane) & 1ull)) {
-        const float* path = p.rt.path + (size_t)nl.route[lane] * (2 * PATH_LEN);
-        const float gx = path[2 * (PATH_LEN - 1)], gy = path[2 * (PATH_LEN - 1) + 1];
+        const float gx = nl.endx[lane], gy = nl.endy[lane];
         const bool arrived = hypotf(nl.x[lane] - gx, nl.y[lane] - gy) < 20.0f;
         const float x = nl.x[lane], y = nl.y[lane];
         const float m = 100.0f;
@@ -601,6 +738,11 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     }
     if (lane == 0) p.npc.count[e] = newcnt;
     wave_lds_sync();
+#ifdef MEV_STAMPS_N
+    NT(7);  // collisions, erase, store
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) p.debug[e * 8 + q] = nt_acc[q];
+#endif
     return newcnt;
 }
 
@@ -791,6 +933,8 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     if constexpr (FUSED) {
         for (int b = tid; b < p.R; b += WAVE) el.rel[b] = p.rel_angles[b];
     }
+    NpcRegs nreg{};
+    if constexpr (TRAFFIC) nreg = npc_load(p, e, tid);  // in flight with the ego loads
     for (int i = tid; i < N; i += WAVE) {
         const int g = e * N + i;
         const int route_l = egoi(p, EF_ROUTE)[g];
@@ -827,7 +971,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
 
     STAMP(0);
     int ncnt = 0;
-    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y);
+    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg);
     if (TRAFFIC && !FUSED && MEV_NPC_PRIO) __builtin_amdgcn_s_setprio(0);
     STAMP(1);
 
@@ -1202,40 +1346,47 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
                 }
             }
             const float ddx = ox - x, ddy = oy - y;
-            const float d = valid ? __builtin_sqrtf(ddx * ddx + ddy * ddy) : __builtin_inff();
+            // an invalid candidate's distance is NaN: it compares false both ways, so it
+            // is neither before nor tied with anyone
+            const float d = valid ? __builtin_sqrtf(ddx * ddx + ddy * ddy) : __builtin_nanf("");
+            // rank among the group's 7 other candidates, each brought in by DPP moves
+            // (quad permutations, then the same after the half-row mirror: lanes sub ^ k
+            // and 7 - (sub ^ k), k = 0..3), no LDS permutes
             int rank = 0;
-#pragma unroll
-            for (int sft = 1; sft < 8; ++sft) {
-                const int kk = (sub + sft) & 7;
-                const float dk = __shfl(d, (grp << 3) + kk);
-                const int vk = __shfl((int)valid, (grp << 3) + kk);
-                rank += (vk != 0) && (dk < d || (dk == d && kk < j));
-            }
+            auto before = [&](float dk, int kk) { rank += (dk < d || (dk == d && kk < j)) ? 1 : 0; };
+            const float dm = dpp_f(d, 0x141);  // row_half_mirror: candidate 7 - sub
+            before(dpp_f(d, 0xB1), sub ^ 1);   // quad_perm [1,0,3,2]
+            before(dpp_f(d, 0x4E), sub ^ 2);   // quad_perm [2,3,0,1]
+            before(dpp_f(d, 0x1B), sub ^ 3);   // quad_perm [3,2,1,0]
+            before(dm, 7 - sub);
+            before(dpp_f(dm, 0xB1), 7 - (sub ^ 1));
+            before(dpp_f(dm, 0x4E), 7 - (sub ^ 2));
+            before(dpp_f(dm, 0x1B), 7 - (sub ^ 3));
             const int nb = __builtin_popcountll(ballot(valid) & gmask);
             STAMPY(5);
+            // one straight-line block for every lane: the agent's own features (the
+            // lane of its own index: never a candidate), its look-ahead terms, or a
+            // neighbour's features -- the atan2f chain runs beside the divisions
+            const bool self = j == ii;
+            const float dxd = el.tgx[ii] - x, dyd = el.tgy[ii] - y;  // path[min(idx + 10, 159)] (:444-452)
+            const float f4 = __builtin_sqrtf(dxd * dxd + dyd * dyd) / float(WIDTH);
+            const float f5 = wrap_angle(atan2f(-dyd, dxd) - h) / PI_F;
+            const float f0 = (self ? x : ox - x) / float(WIDTH);
+            const float f1 = (self ? y : oy - y) / float(HEIGHT);
+            const float f2 = (self ? v : ov - v) / PHYSICS_MAX_SPEED;
+            const float f3 = (self ? h : wrap_angle(oh - h)) / PI_F;
             if (act) {
                 // k_step stages the head in LDS (written with the LiDAR block by fused_store)
                 float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)(e * N + i) * p.D;
                 if (!alv) {
                     for (int cc = sub; cc < OBS_HEAD; cc += 8) row[cc] = 0.0f;
                 } else {
-                    if (sub == 0) {
-                        row[0] = x / float(WIDTH);
-                        row[1] = y / float(HEIGHT);
-                        row[2] = v / PHYSICS_MAX_SPEED;
-                        row[3] = h / PI_F;
-                    } else if (sub == 1) {
-                        const float dxd = el.tgx[i] - x, dyd = el.tgy[i] - y;
-                        row[4] = __builtin_sqrtf(dxd * dxd + dyd * dyd) / float(WIDTH);
-                        row[5] = wrap_angle(atan2f(-dyd, dxd) - h) / PI_F;
+                    if (self) {
+                        row[0] = f0; row[1] = f1; row[2] = f2; row[3] = f3; row[4] = f4; row[5] = f5;
                     }
                     if (valid && rank < NEIGHBOR_COUNT) {
                         float* o = row + 6 + 5 * rank;
-                        o[0] = (ox - x) / float(WIDTH);
-                        o[1] = (oy - y) / float(HEIGHT);
-                        o[2] = (ov - v) / PHYSICS_MAX_SPEED;
-                        o[3] = wrap_angle(oh - h) / PI_F;
-                        o[4] = float(oi);
+                        o[0] = f0; o[1] = f1; o[2] = f2; o[3] = f3; o[4] = float(oi);
                     }
                     if (sub < NEIGHBOR_COUNT && sub >= nb) {
                         float* o = row + 6 + 5 * sub;
@@ -1265,7 +1416,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
 template <bool TRAFFIC>
 __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outputs out, int e_begin) {
     extern __shared__ __align__(16) unsigned char cars_lds[];
-    const int e = e_begin + (int)blockIdx.x;
+    const int e = e_begin + xcd_env((int)blockIdx.x, (int)gridDim.x);
 #if defined(MEV_STAMPS_R)
     STAMP_RAW(0);
 #endif
@@ -1917,7 +2068,8 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     extern __shared__ __align__(16) unsigned char lds_raw[];
     const int lane = threadIdx.x & (WAVE - 1);
     const int wv = threadIdx.x / WAVE;
-    const int a0 = __builtin_amdgcn_readfirstlane(a_begin + (int)(blockIdx.x * (blockDim.x / WAVE) + wv) * G);
+    const int blk = xcd_env((int)blockIdx.x, (int)gridDim.x);  // neighbouring groups on one XCD
+    const int a0 = __builtin_amdgcn_readfirstlane(a_begin + (blk * (int)(blockDim.x / WAVE) + wv) * G);
     if (a0 >= a_end) return;  // wave-uniform exit: the kernel has no block-level barrier
     const int na = a_end - a0 < G ? a_end - a0 : G;
     if (MEV_PRIO_HBM) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
@@ -2056,22 +2208,6 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // live through the whole kernel and the SGPR allocator spills them into VGPR
 // lanes (a v_readlane per reload); through the pointer each field is an s_load
 // next to its use.
-// XCD-aware env order: the dispatcher deals workgroups round-robin over the 8
-// XCDs (block b -> XCD b % 8), and each XCD has its own L2.  An env's SoA
-// slices are 4 B x N per field (32 B at N = 8), so four consecutive envs share
-// every 128-B line; mapping block b to env (b % 8) * (E / 8) + b / 8 keeps
-// consecutive envs -- and their shared lines, and the partial lines between
-// their observation rows -- on one XCD instead of fetching/merging them in
-// four L2s.  (Placement is a performance hint only: any bijection is correct.)
-#ifndef MEV_XCD_REMAP
-#define MEV_XCD_REMAP 1
-#endif
-__device__ inline int xcd_env(int b, int E) {
-    if (!MEV_XCD_REMAP) return b;
-    const int q = E >> 3;
-    return b < 8 * q ? (b & 7) * q + (b >> 3) : b;
-}
-
 template <bool TRAFFIC, bool TAB, int NM>
 __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
     const SimParams& p = *pp;

@@ -169,6 +169,37 @@ MEV_HD void car_update(Kin& k, float throttle, float steer_input, float dt, floa
     *sinH = s;
 }
 
+// Car::update split for the NPC controller, whose steering input is known
+// before its throttle: car_steer is the steering part (its new angle), and
+// car_update_steered the rest given that angle and its tangent -- the same
+// operations in the same order as car_update.
+MEV_HD float car_steer(float steer, float steer_input) {
+    const float target_steering = steer_input * MAX_STEERING_ANGLE;
+    return steer + (target_steering - steer) * 0.2f;
+}
+MEV_HD void car_update_steered(Kin& k, float throttle, float new_steer, float tan_steer, float dt, float* cosH,
+                               float* sinH) {
+    k.acc = throttle * MAX_ACC;
+    k.steer = new_steer;
+    if (throttle == 0.0f) k.v *= 0.95f;
+    k.v += k.acc * dt;
+    if (k.v < 0.0f) k.v = 0.0f;
+    if (k.v > PHYSICS_MAX_SPEED) k.v = PHYSICS_MAX_SPEED;
+    if (fabs_f(k.v) > 0.1f) {
+        const float ang_vel = (k.v / WHEELBASE) * tan_steer;
+        k.h += ang_vel;
+    }
+    k.h = fmodf(k.h + PI_F, 2.0f * PI_F);
+    if (k.h < 0) k.h += 2.0f * PI_F;
+    k.h -= PI_F;
+    float s, c;
+    sincosf(k.h, &s, &c);
+    k.x += k.v * c;
+    k.y -= k.v * s;
+    *cosH = c;
+    *sinH = s;
+}
+
 // LiDAR obstacle box: rotated rectangle's AABB (cpp/Lidar.cpp:65-75) turned
 // into an inclusive integer pixel range — `float(px) >= x - ex` <=> px >= ceil(x - ex).
 struct PxBox {
