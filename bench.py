@@ -145,6 +145,21 @@ def valu_roofline(kernel_ms: float, envs: int):
             "source": "profiles/valu_counters.json (rocprofv3 --pmc pass of this bench) / live kernel_ms"}
 
 
+class stdout_to_stderr:
+    """RCCL prints its version banner on fd 1 at communicator init: keep the bench's stdout
+    to the one JSON line by pointing fd 1 at stderr around the init."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -326,7 +341,8 @@ def main():
                 uid = bytes(store.get("mev_comm_id"))
             else:
                 uid = _capi.comm_unique_id()
-            env.comm_init(uid, world, rank, root=0, slots=E)
+            with stdout_to_stderr():
+                env.comm_init(uid, world, rank, root=0, slots=E)
             env.reset(device=True)
             for t in range(W):
                 env.step(actions[t].data_ptr(), 1.0 / 60.0, auto_reset=True, device=True, gather=True)
