@@ -432,8 +432,12 @@ int mev_configure(mev_handle* h, int32_t use_team, int32_t respawn, int32_t max_
 int mev_configure_traffic(mev_handle* h, int32_t enabled, float density) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (enabled && h->cfg.max_npcs == 0) return fail(MEV_E_INVALID, "traffic needs max_npcs > 0 (set at creation)");
-    if (enabled && h->sp.step_kernel == 2)
-        return fail(MEV_E_INVALID, "the fused step kernel (mev_set_step_kernel 2) does not support traffic");
+    if (enabled && h->sp.step_kernel == 2) {
+        mev::SimParams q = h->sp;
+        q.traffic = 1;
+        if (mev::step_kernel_for(q) == 0)
+            return fail(MEV_E_INVALID, "the fused step kernel (mev_set_step_kernel 2) cannot hold this handle's NPC slots");
+    }
     h->cfg.traffic_flow = enabled;
     h->cfg.traffic_density = density < 0.0f ? 0.0f : density;  // configure_traffic clamps (:56-60)
     h->sp.traffic = enabled;

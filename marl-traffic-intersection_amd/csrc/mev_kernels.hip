@@ -274,18 +274,24 @@ struct EgoLDS {
     uint8_t colnpc[MAXN];
 };
 
-struct NpcLDS {
-    float x[MAXK], y[MAXK], v[MAXK], h[MAXK], c[MAXK], s[MAXK], acc[MAXK], steer[MAXK];
-    int32_t pidx[MAXK], route[MAXK], intent[MAXK];
-    uint8_t alive[MAXK];
-    float cx[MAXK][4], cy[MAXK][4];
-    unsigned long long col[MAXK];
+// capacity KM NPC slots (k_cars / k_reset: MAXK; the fused k_step: the smallest
+// of 32 / 64 that holds the handle's max_npcs, so that the NPC arrays leave room
+// in the wave's LDS for a LiDAR pool)
+template <int KM>
+struct NpcLDST {
+    static constexpr int kCap = KM;
+    float x[KM], y[KM], v[KM], h[KM], c[KM], s[KM], acc[KM], steer[KM];
+    int32_t pidx[KM], route[KM], intent[KM];
+    uint8_t alive[KM];
+    float cx[KM][4], cy[KM][4];
+    unsigned long long col[KM];
     // the controller's per-NPC terms that depend on its own start-of-step state only
-    int32_t pidx0[MAXK];          // after the first update_path_index of its turn
-    float nsteer[MAXK], ntan[MAXK];  // Car::update's new steering angle and its tangent
-    float accb[MAXK], mdc[MAXK];  // cruise throttle, distance to the centre
-    float endx[MAXK], endy[MAXK];  // the route's last point (arrival test)
+    int32_t pidx0[KM];          // after the first update_path_index of its turn
+    float nsteer[KM], ntan[KM];  // Car::update's new steering angle and its tangent
+    float accb[KM], mdc[KM];  // cruise throttle, distance to the centre
+    float endx[KM], endy[KM];  // the route's last point (arrival test)
 };
+using NpcLDS = NpcLDST<MAXK>;
 
 // One NPC slot's state in the registers of lane = slot, loaded together with the
 // ego state (one round of loads) and handed to npc_phase.
@@ -347,7 +353,8 @@ __device__ inline int wave_argmin_dpp(float d, int i) {
 #define NT(k) do {} while (0)
 #endif
 
-__device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NpcLDS& nl, int lane,
+template <class NL>
+__device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NL& nl, int lane,
                           const float* ego_x, const float* ego_y, const NpcRegs& nr) {
     const int K = p.K;
 #ifdef MEV_STAMPS_N
@@ -750,8 +757,8 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
 // get_observations (cpp/IntersectionEnv.cpp:418-520) minus the LiDAR block:
 // ego features, path look-ahead, 5 nearest alive neighbours (egos first, then
 // NPCs; stable by distance == libstdc++ insertion sort for <= 16 candidates).
-template <bool TRAFFIC, class EL>
-__device__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const NpcLDS* nl, int ncnt, float tx,
+template <bool TRAFFIC, class EL, class NL>
+__device__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt, float tx,
                                   float ty, float* row, bool pad = true) {
     const float x = el.x[i], y = el.y[i], v = el.v[i], h = el.h[i];
     row[0] = x / float(WIDTH);
@@ -811,8 +818,8 @@ __device__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const
         for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
 }
 
-template <bool TRAFFIC, class EL>
-__device__ void write_obs_head(const SimParams& p, int i, const EL& el, const NpcLDS* nl, int ncnt,
+template <bool TRAFFIC, class EL, class NL>
+__device__ void write_obs_head(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt,
                                const float* path, int pidx, float* row) {
     int tidx = pidx + 10;
     if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
@@ -904,9 +911,9 @@ struct CarsCtx {
 // instead of delaying this wave's.  FUSED: the LiDAR runs in the same wave
 // (k_step) and reads the obstacle table and candidate masks from LDS, so they
 // are not published to HBM.
-template <bool TRAFFIC, bool FUSED>
+template <bool TRAFFIC, bool FUSED, class NL>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
-                                            const CarsLDS& el, NpcLDS* nl) {
+                                            const CarsLDS& el, NL* nl) {
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
     // status, collisions, respawn, observation head); the LiDAR block of the
     // observation is filled by the LiDAR body right after.  Per-agent phases run on
@@ -972,7 +979,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     STAMP(0);
     int ncnt = 0;
     if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg);
-    if (TRAFFIC && !FUSED && MEV_NPC_PRIO) __builtin_amdgcn_s_setprio(0);
+    if (TRAFFIC && MEV_NPC_PRIO) __builtin_amdgcn_s_setprio(FUSED ? MEV_PRIO_CARS : 0);
     STAMP(1);
 
     // ---- phase 1: kinematics (:151-163), path index, base reward (:15-46),
@@ -1240,9 +1247,9 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
 // k_cars): bonuses, team mix and env flags (:320-370), the reward / done /
 // status outputs and the state write-back, the observation head (:418-520).
 // Reads only the car LDS (the LiDAR never writes it).
-template <bool TRAFFIC, bool FUSED>
+template <bool TRAFFIC, bool FUSED, class NL>
 __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out, const int e, const CarsLDS& el,
-                                          const NpcLDS* nl, const CarsCtx& cx) {
+                                          const NL* nl, const CarsCtx& cx) {
     const int tid = threadIdx.x & (WAVE - 1);
     const int N = p.N;
     constexpr bool STAGE = FUSED && MEV_FUSED_STAGED;
@@ -2208,7 +2215,7 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // live through the whole kernel and the SGPR allocator spills them into VGPR
 // lanes (a v_readlane per reload); through the pointer each field is an s_load
 // next to its use.
-template <bool TRAFFIC, bool TAB, int NM>
+template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK>
 __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
     const SimParams& p = *pp;
     extern __shared__ __align__(16) unsigned char step_lds[];
@@ -2221,8 +2228,8 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
     el.head = reinterpret_cast<float*>(step_lds + sl.head);
     el.rel = reinterpret_cast<float*>(step_lds + sl.rel);
     el.envw = reinterpret_cast<int32_t*>(step_lds + sl.envw);
-    __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
-    NpcLDS* nl = nullptr;
+    __shared__ typename std::conditional<TRAFFIC, NpcLDST<KM>, char>::type nl_storage;
+    NpcLDST<KM>* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
     if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
     const CarsCtx cx = cars_pre<TRAFFIC, true>(p, in, out, e, el, nl);
@@ -2360,22 +2367,50 @@ static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Ou
     return e;
 }
 
-// k_step applies without traffic when its LDS (cars + one LiDAR pool of
-// step_pool(p) agents) fits a wave's share: at 4 waves per SIMD (128 VGPRs) a
-// CU holds 16 waves, so a wave may take 160 KB / 16 = 10 KB.
+// NPC slots of the fused kernel's LDS arrays (NpcLDST<KM>): the smallest
+// compiled capacity that holds the handle's max_npcs
+static int fused_npc_cap(const SimParams& p) { return p.K <= 32 ? 32 : 64; }
+
+// LDS of one k_step wave: the dynamic part (cars + one LiDAR pool of
+// step_pool(p) agents) plus, with traffic, the static NPC arrays
+static size_t fused_lds_bytes(const SimParams& p) {
+    size_t b = (size_t)step_layout(p).bytes;
+    if (p.traffic) b += fused_npc_cap(p) == 32 ? sizeof(NpcLDST<32>) : sizeof(NpcLDST<64>);
+    return b;
+}
+
+// k_step applies when its LDS fits one workgroup (64 KB); it is the automatic
+// choice when it also fits a wave's share at 4 waves per SIMD (128 VGPRs): a CU
+// holds 16 waves, so a wave may take 160 KB / 16 = 10 KB.
 static bool fused_fits(const SimParams& p) {
-    if (p.traffic) return false;  // the NPC phase's LDS leaves no room for a LiDAR pool
-    if (MEV_FUSED_STAGED && p.N * p.R > 512) return false;
-    return step_layout(p).bytes <= 10 * 1024;
+    if (MEV_FUSED_STAGED && (p.traffic || p.N * p.R > 512)) return false;
+    return fused_lds_bytes(p) <= 64 * 1024;
 }
 
 int step_kernel_for(const SimParams& p) {
     const bool fusable = fused_fits(p);
     if (p.step_kernel == 1) return 1;
     if (p.step_kernel == 2) return fusable ? 2 : 0;
-    // auto: fused once the batch fills the chip with one wave per env (>= 4 per CU);
-    // smaller batches keep the LiDAR's finer per-group waves
-    return (fusable && p.E >= 1024) ? 2 : 1;
+    // auto: fused once the batch fills the chip with one wave per env (>= 4 per CU)
+    // and a wave's LDS leaves 4 waves per SIMD; smaller batches keep the LiDAR's
+    // finer per-group waves
+    return (fusable && fused_lds_bytes(p) <= 10 * 1024 && p.E >= 1024) ? 2 : 1;
+}
+
+template <bool TAB>
+static void launch_fused(const SimParams& p, const SimParams* dp, const StepInputs& in, const Outputs& out,
+                         hipStream_t s) {
+    if (p.traffic) {
+        const unsigned lds = (unsigned)step_layout(p).bytes;  // + the static NpcLDST
+        if (fused_npc_cap(p) == 32) hipLaunchKernelGGL((k_step<true, TAB, 0, 32>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+        else hipLaunchKernelGGL((k_step<true, TAB, 0, 64>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+    } else if (fixed_fits<8>(p)) {  // compile-time LDS layout
+        const unsigned lds = (unsigned)FixedLayout<8>::bytes;
+        hipLaunchKernelGGL((k_step<false, TAB, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+    } else {
+        const unsigned lds = (unsigned)step_layout(p).bytes;
+        hipLaunchKernelGGL((k_step<false, TAB, 0>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+    }
 }
 
 hipError_t launch_step(const SimParams& p, const SimParams* dp, const StepInputs& in, const Outputs& out,
@@ -2384,15 +2419,8 @@ hipError_t launch_step(const SimParams& p, const SimParams* dp, const StepInputs
     if (kind == 0) return hipErrorInvalidValue;
     if (kind == 2) {
         if (ev) (void)hipEventRecord(ev[0], s);
-        if (fixed_fits<8>(p)) {  // compile-time LDS layout
-            const unsigned lds = (unsigned)FixedLayout<8>::bytes;
-            if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
-            else hipLaunchKernelGGL((k_step<false, false, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
-        } else {
-            const unsigned lds = (unsigned)step_layout(p).bytes;
-            if (p.dist_tab) hipLaunchKernelGGL((k_step<false, true, 0>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
-            else hipLaunchKernelGGL((k_step<false, false, 0>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
-        }
+        if (p.dist_tab) launch_fused<true>(p, dp, in, out, s);
+        else launch_fused<false>(p, dp, in, out, s);
         hipError_t e = hipGetLastError();
         if (ev && e == hipSuccess) { (void)hipEventRecord(ev[1], s); (void)hipEventRecord(ev[2], s); }
         return e;

@@ -72,6 +72,35 @@ def test_fused_and_two_kernel_paths_agree_full_size(mev, rays):
         h.close()
 
 
+def test_fused_and_two_kernel_paths_agree_traffic_full_size(mev):
+    """Config 4 shape (4096 envs x 1 ego x 64 beams, traffic at density 0.5 with
+    the Philox spawn stream, 32 NPC slots): the fused k_step (NPC phase, car
+    part and LiDAR in one wave) and k_cars + k_lidar agree bit for bit, step
+    after step, with auto-reset on; the NPC fleets (counts and every NPC
+    field) too."""
+    cfg = dict(num_envs=E, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32,
+               max_steps=300, seed=11)
+    hs = [mev.Handle(**cfg) for _ in range(2)]
+    for h, kernel in zip(hs, (1, 2)):
+        h.set_step_kernel(kernel)
+    rng = np.random.default_rng(12)
+    most = 0
+    for t in range(400):
+        a = rng.uniform(-1, 1, (E, 1, 2)).astype(np.float32)
+        o1 = hs[0].step(a, auto_reset=True)
+        o2 = hs[1].step(a, auto_reset=True)
+        for k in o1:
+            assert np.array_equal(o1[k], o2[k]), (t, k)
+        if t % 50 == 49 or t == 399:
+            s1, s2 = hs[0].get_state(), hs[1].get_state()
+            for k in s1:
+                assert np.array_equal(s1[k], s2[k]), (t, k)
+            most = max(most, int(s1["npc_count"].max()))
+    assert most >= 4  # busy intersections were exercised
+    for h in hs:
+        h.close()
+
+
 def test_step_kernel_selection(mev):
     h = _handle(mev)
     assert h.step_kernel() == 2  # automatic: fused at 4096 envs
@@ -80,19 +109,23 @@ def test_step_kernel_selection(mev):
     with pytest.raises(mev.MevError):
         h.set_step_kernel(3)
     h.set_step_kernel(2)
-    with pytest.raises(mev.MevError):  # the fused kernel has no NPC phase
-        h.configure_traffic(1, 0.5)
+    h.configure_traffic(1, 0.5)  # the fused kernel runs the NPC phase too
+    assert h.step_kernel() == 2
     h.set_step_kernel(0)
-    h.configure_traffic(1, 0.5)
+    # automatic: 8 egos + 64 NPC slots need more than a wave's 10 KB LDS share
     assert h.step_kernel() == 1
-    with pytest.raises(mev.MevError):
-        h.set_step_kernel(2)
+    h.set_step_kernel(2)
+    assert h.step_kernel() == 2
     h.close()
     small = _handle(mev, num_envs=64)
     assert small.step_kernel() == 1  # automatic: finer LiDAR waves for small batches
     small.set_step_kernel(2)
     assert small.step_kernel() == 2
     small.close()
+    # config 4 shape (1 ego, traffic, 32 NPC slots): fused automatically
+    t = mev.Handle(num_envs=4096, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32)
+    assert t.step_kernel() == 2
+    t.close()
 
 
 def test_env_permutation_equivariance(mev):

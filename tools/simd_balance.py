@@ -29,14 +29,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--rays", type=int, default=64)
     a = ap.parse_args()
     mev = pkgload.load()
-    h = mev.Handle(num_envs=a.envs, num_agents=8, lidar_rays=64, use_team_reward=1)
+    h = mev.Handle(num_envs=a.envs, num_agents=a.agents, lidar_rays=a.rays, use_team_reward=1)
     h.set_step_kernel(2)
     rng = np.random.default_rng(0)
     slots, entries, ph, spans, fin, life, simd_sum, simd_max, simd_mean, nw, first_end = [], [], [], [], [], [], [], [], [], Counter(), []
     for t in range(a.steps):
-        h.step(rng.uniform(-1, 1, (a.envs, 8, 2)).astype(np.float32), auto_reset=True)
+        h.step(rng.uniform(-1, 1, (a.envs, a.agents, 2)).astype(np.float32), auto_reset=True)
         if t < a.steps // 2:
             continue
         r = h.debug_stamps().astype(np.uint64).reshape(a.envs, 8)
@@ -62,7 +64,7 @@ def main():
             simd_sum.append(lt[m].sum())
             simd_max.append(lt[m].max())
             simd_mean.append(lt[m].mean())
-    print(f"envs={a.envs}: SIMDs per step {len(fin) // len(spans)}, waves per SIMD {dict(sorted(nw.items()))}")
+    print(f"envs={a.envs} agents={a.agents} rays={a.rays}: SIMDs per step {len(fin) // len(spans)}, waves per SIMD {dict(sorted(nw.items()))}")
     print("  us (p0 / p10 / p50 / p90 / p100)")
     print(f"  step span (entry -> end)   {pct(spans)}")
     print(f"  first wave end             {pct(first_end)}")
