@@ -200,6 +200,11 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
 
 /* Diagnostics: spawns dropped because max_npcs was full (cumulative). */
 int mev_npc_overflow(mev_handle* h, int64_t* count);
+/* Diagnostics (cumulative): the spawn overflow above, and the NPC turns the
+ * controller ran one after another because its parallel rounds disagreed
+ * (mev_kernels.hip npc_phase: round B changed a throttle; results are the
+ * sequential ones either way). */
+int mev_npc_stats(mev_handle* h, int64_t* overflow, int64_t* sequential_turns);
 /* Diagnostics: per-env phase timestamps [E][8] of the last step; all zero
  * unless the library was built with -DMEV_STAMPS (tools/phase_profile.py). */
 int mev_debug_stamps(mev_handle* h, uint64_t* out);

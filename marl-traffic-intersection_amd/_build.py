@@ -57,7 +57,10 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # the compiler's default machine scheduler instead of SCHED (k_step 41.6 -> 41.9 us)
                "sch_default": [],
                # k_cars' NPC-count priorities (product: level = NPCs left / 2): off / per NPC / per 3 NPCs
-               "npcprio0": ["-DMEV_NPC_PRIO=0"], "npcprio1": ["-DMEV_NPC_PRIO=1"], "npcprio3": ["-DMEV_NPC_PRIO=3"],
+               # exact variant: the NPC controller's first move pass loads its path windows before the plans
+               "npcprewin": ["-DMEV_NPC_PREWIN=1"],
+               "npcprio1": ["-DMEV_NPC_PRIO=1"], "npcprio3": ["-DMEV_NPC_PRIO=3"],
+               "npcprio0": ["-DMEV_NPC_PRIO=0"],
                # timing-only: k_step stopped after the car part / LiDAR phase 1 / 2 / 3 (instruction budgets)
                "stop1": ["-DMEV_EXP_STOP=1"], "stop2": ["-DMEV_EXP_STOP=2"], "stop3": ["-DMEV_EXP_STOP=3"],
                "stop4": ["-DMEV_EXP_STOP=4"], "stop0": ["-DMEV_EXP_STOP=0"],

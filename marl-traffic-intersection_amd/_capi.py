@@ -35,7 +35,7 @@ EXPORTED = (
     "mev_get_config", "mev_obs_dim", "mev_set_stream", "mev_sync", "mev_num_points", "mev_point_xy",
     "mev_route_id", "mev_route_info", "mev_path_len", "mev_set_ego_routes", "mev_set_traffic_routes",
     "mev_default_traffic_routes", "mev_reset", "mev_step", "mev_get_outputs", "mev_get_state", "mev_set_state",
-    "mev_device_outputs", "mev_npc_overflow", "mev_use_own_stream", "mev_debug_stamps",
+    "mev_device_outputs", "mev_npc_overflow", "mev_npc_stats", "mev_use_own_stream", "mev_debug_stamps",
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
     "mev_kernel_timing", "mev_kernel_times", "mev_set_reset_routes", "mev_snapshot_size", "mev_snapshot",
     "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel",
@@ -130,6 +130,7 @@ def load_library(variant: str = None):
     L.mev_set_state.argtypes = [_vp, ctypes.POINTER(MevState)]
     L.mev_device_outputs.argtypes = [_vp] + [ctypes.POINTER(_vp)] * 6
     L.mev_npc_overflow.argtypes = [_vp, ctypes.POINTER(ctypes.c_int64)]
+    L.mev_npc_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     L.mev_device_count.argtypes = [i32p]
     L.mev_use_own_stream.argtypes = [_vp]
     L.mev_debug_stamps.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64)]
@@ -496,6 +497,12 @@ class Handle:
     def restore(self, src, env_mask=None, device: bool = False):
         mask = None if env_mask is None else (env_mask if device else np.ascontiguousarray(env_mask, np.uint8))
         _check(self._lib.mev_restore(self._h, _ptr(src), _ptr(mask), MEV_DEVICE_PTRS if device else 0))
+
+    def npc_stats(self):
+        """(dropped spawns, NPC turns run sequentially after a parallel-round disagreement), cumulative."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        _check(self._lib.mev_npc_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def npc_overflow(self) -> int:
         v = ctypes.c_int64()

@@ -276,7 +276,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     }
     A(&p.ego.alive, EN);
     A(&p.npc.alive, EK); A(&p.npc.count, size_t(E));
-    A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 1); A(&p.debug, size_t(E) * 8);
+    A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 2); A(&p.debug, size_t(E) * 8);
     A(&p.ob_box, size_t(E) * size_t(N + c.max_npcs)); A(&p.ob_cand, EN * 2);
     // outputs
     A(&h->internal.obs, EN * size_t(D)); A(&h->internal.rew, EN); A(&h->internal.done, EN); A(&h->internal.status, EN);
@@ -1173,6 +1173,17 @@ int mev_npc_overflow(mev_handle* h, int64_t* count) {
     HIP_TRY(hipMemcpyAsync(&v, h->sp.overflow, sizeof(v), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     *count = int64_t(v);
+    return MEV_OK;
+}
+
+int mev_npc_stats(mev_handle* h, int64_t* overflow, int64_t* sequential_turns) {
+    if (!h || !overflow || !sequential_turns) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    unsigned long long v[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(v, h->sp.overflow, sizeof(v), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    *overflow = int64_t(v[0]);
+    *sequential_turns = int64_t(v[1]);
     return MEV_OK;
 }
 

@@ -80,7 +80,7 @@ struct SimParams {
     int32_t n_traffic_routes;
     int32_t* step_count;      // [E]
     uint8_t* pending_reset;   // [E]
-    unsigned long long* overflow;  // [1]
+    unsigned long long* overflow;  // [2]: dropped spawns, sequential NPC turns (npc_phase)
     unsigned long long* debug;     // diagnostic builds only (MEV_STAMPS): [E*8]
     // LiDAR hand-off k_cars -> k_lidar (L2-resident, rewritten every step)
     int4* ob_box;                  // [E][ob_stride] integer pixel AABB (x0, x1, y0, y1)

@@ -107,8 +107,8 @@ constexpr int MAXOB = MAXN + MAXK;
 #define MEV_PRIO_HBM 1
 #endif
 
-// k_cars with traffic: issue priority by the NPCs an env has left to control
-// (level = remaining / MEV_NPC_PRIO, capped at 3; 0: off).  The env with the
+// With traffic: issue priority of the NPC controller by the NPCs an env has to
+// control (level = NPCs / MEV_NPC_PRIO, capped at 3; 0: off).  The env with the
 // most NPCs is the kernel's critical path (config 4: k_cars 53.9 -> 48.3 us).
 #ifndef MEV_NPC_PRIO
 #define MEV_NPC_PRIO 2
@@ -283,8 +283,22 @@ struct NpcLDST {
     float x[KM], y[KM], v[KM], h[KM], c[KM], s[KM], acc[KM], steer[KM];
     int32_t pidx[KM], route[KM], intent[KM];
     uint8_t alive[KM];
-    float cx[KM][4], cy[KM][4];
+    union {
+        struct {  // the car corners (collision phase, after the controller)
+            float cx[KM][4], cy[KM][4];
+        };
+        struct {  // the controller's round-A states (npc_phase part 2), dead once committed
+            float xn[KM], yn[KM], vn[KM], hn[KM], accn[KM], steern[KM], cn[KM], sn[KM];
+        };
+    };
     unsigned long long col[KM];
+    // the controller's parallel rounds: throttles of round A / B, ghost-scan candidates
+    // (others that passed the filters) and which of them k must yield to, new path index
+    float thr_a[KM], thr_b[KM];
+    unsigned long long em[KM], ym[KM];      // this round's filtered others / yields (scans)
+    unsigned long long em_a[KM], ym_a[KM];  // round A's
+    float mc_a[KM];                         // round A's conflict distance (< 0: none)
+    int32_t pidxn[KM];
     // the controller's per-NPC terms that depend on its own start-of-step state only
     int32_t pidx0[KM];          // after the first update_path_index of its turn
     float nsteer[KM], ntan[KM];  // Car::update's new steering angle and its tangent
@@ -352,6 +366,137 @@ __device__ inline int wave_argmin_dpp(float d, int i) {
 #else
 #define NT(k) do {} while (0)
 #endif
+
+// One (NPC k, other NPC j) pair of plan_npc_action_tf's longitudinal tests:
+// f30 / f50 -- j is a front car closer than 30 / 50 (get_front_car_dist_tf,
+// TrafficFlow.cpp:22-47, used as front < 30 / < 50 at :72-73); pok -- j passes
+// the ghost-scan filters (:97-154); yfar -- k yields to j (:156-181).  k's own
+// terms: pose, speed, cos/sin of its heading, distance to the centre.  The
+// front-car and ghost-scan tests need only these thresholds, so a turn's plan
+// is ballots over j, not reductions.
+struct NpcPair {
+    bool f30, f50, pok, yfar;
+};
+__device__ __forceinline__ NpcPair npc_pair(int k, float x, float y, float h, float v, float ck, float sk,
+                                            float my_dist_to_center, bool jvalid, int j, float oxj, float oyj,
+                                            float ohj, float ovj, float ocj, float osj) {
+    const float CXf = WIDTH * 0.5f, CYf = HEIGHT * 0.5f;
+    NpcPair r{false, false, false, false};
+    const float vx = ck, vy = -sk;
+    // |wrap(h - h_j)| and the distance to j: shared by the front-car test and the
+    // ghost-scan filters (the same expressions in the reference, :37/:101/:107)
+    const float dxj = oxj - x;
+    const float dyj = oyj - y;
+    const float dist_j = hypotf(dxj, dyj);
+    const float adiff_j = fabs_f(wrap_angle(h - ohj));
+    if (jvalid) {
+        const float dist = dist_j;
+        if (!(dist > 80.0f)) {
+            const float dot = (dxj * vx + dyj * vy) / (dist + 1e-5f);
+            if (dot > 0.8f) {
+                if (adiff_j < (45.0f * PI_F / 180.0f)) { r.f30 = dist < 30.0f; r.f50 = dist < 50.0f; }
+            }
+        }
+    }
+    bool pok = false, yfar = false;
+    if (jvalid) {
+        const float angle_diff = adiff_j;
+        pok = true;
+        if (angle_diff < (60.0f * PI_F / 180.0f)) pok = false;
+        if (pok) {
+            const float dxo = dxj;
+            const float dyo = dyj;
+            const float dist_o = dist_j;
+            if (dist_o > 1e-5f) {
+                const float mdx = ck, mdy = -sk;
+                const float two_pi_m = 2.0f * PI_F - angle_diff;
+                const float adn = (two_pi_m < angle_diff) ? two_pi_m : angle_diff;
+                const bool parallel = (adn < (30.0f * PI_F / 180.0f)) || (adn > (150.0f * PI_F / 180.0f));
+                if (parallel) {
+                    const float lon = dxo * mdx + dyo * mdy;
+                    float lsq = dist_o * dist_o - lon * lon;
+                    lsq = (0.0f < lsq) ? lsq : 0.0f;  // std::max(0, .)
+                    const float lat = __builtin_sqrtf(lsq);
+                    const bool sideways = fabs_f(lat) < (LANE_WIDTH_PX * 1.5f);
+                    const bool near_lon = fabs_f(lon) < (CAR_LENGTH * 2.0f);
+                    if (sideways && near_lon) {
+                        const float fdist = 20.0f;
+                        const float mfx = x + mdx * fdist;
+                        const float mfy = y + mdy * fdist;
+                        const float odx = ocj, ody = -osj;
+                        const float ofx = oxj + odx * fdist;
+                        const float ofy = oyj + ody * fdist;
+                        const float fdx = ofx - mfx;
+                        const float fdy = ofy - mfy;
+                        const float fmag = hypotf(fdx, fdy);
+                        if (fmag > 1e-5f) {
+                            const float flon = fdx * mdx + fdy * mdy;
+                            float flsq = fmag * fmag - flon * flon;
+                            flsq = (0.0f < flsq) ? flsq : 0.0f;
+                            const float flat = __builtin_sqrtf(flsq);
+                            const float change = fabs_f(flat - lat);
+                            if (change < (LANE_WIDTH_PX * 0.5f)) pok = false;  // side by side: skip
+                        }
+                    }
+                }
+            }
+        }
+        if (pok) {
+            const float odc = hypotf(oxj - CXf, oyj - CYf);
+            if (v < 1.0f && ovj > 3.0f && odc < my_dist_to_center + 25.0f) yfar = true;
+            else if (odc < my_dist_to_center - 5.0f) yfar = true;
+            else if (fabs_f(odc - my_dist_to_center) <= 5.0f) yfar = k < j;  // address order
+        }
+    }
+    r.pok = pok;
+    r.yfar = yfar;
+    return r;
+}
+
+// The ghost path scan of NPC k (:157-188) with its path points path[idx0 + lane]
+// (ga) and path[idx0 + 64 + lane] (gb): the first point, in path order, within
+// SAFE of an other in em (k's filtered others; lane o holds other o's position)
+// that k yields to there (ym, or the point is within 15 of k) is the conflict;
+// its distance to k is the minimum (:183-188).  Returns the conflict distance,
+// or -1 without a conflict.
+__device__ __forceinline__ float npc_ghost_scan(int g_start, float x, float y, float2 ga, float2 gb,
+                                                unsigned long long em, unsigned long long ym, float oxj, float oyj,
+                                                int lane) {
+    const float SAFE = CAR_WIDTH * 2.0f;
+    const float SAFE_SQ = SAFE * SAFE;
+    const int g_end = g_start + 120 < PATH_LEN ? g_start + 120 : PATH_LEN;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        if (g_start + c * WAVE >= g_end) break;
+        const float2 gp = c ? gb : ga;
+        const bool gv = g_start + c * WAVE + lane < g_end;
+        const float dtc = hypotf(gp.x - x, gp.y - y);
+        bool hit = false;
+        for (unsigned long long mm = em; mm; mm &= mm - 1ull) {
+            const int o = __builtin_ctzll(mm);
+            const float ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(oxj), o));
+            const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(oyj), o));
+            const float dxg = ox - gp.x;
+            const float dyg = oy - gp.y;
+            if (dxg * dxg + dyg * dyg < SAFE_SQ && (dtc < 15.0f || ((ym >> o) & 1ull))) hit = true;
+        }
+        const unsigned long long m = ballot(gv && hit);
+        if (m) return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dtc), __builtin_ctzll(m)));
+    }
+    return -1.0f;
+}
+
+// compose (:190-195): the longitudinal throttle after the front-car rules (acc_thr)
+// and the ghost scan's conflict distance (< 0: none)
+__device__ __forceinline__ float npc_throttle(float acc_thr, float min_conflict) {
+    float thr = acc_thr;
+    if (min_conflict >= 0.0f) {
+        if (min_conflict < 35.0f) thr = -1.0f;
+        else if (min_conflict < 60.0f) thr = -0.8f;
+        else thr = (0.0f < thr) ? 0.0f : thr;
+    }
+    return thr;
+}
 
 template <class NL>
 __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NL& nl, int lane,
@@ -517,153 +662,302 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     }
     wave_lds_sync();
     NT(1);  // part 1
-    // part 2: the turns in vector order.  Lane j holds the other NPC j; the front-car
-    // and ghost-scan tests need only thresholds, so they are ballots, not reductions.
-    const float SAFE = CAR_WIDTH * 2.0f;
-    const float SAFE_SQ = SAFE * SAFE;
+    // part 2: the turns in vector order (Gauss-Seidel: NPC k plans against the
+    // others' CURRENT states -- the NPCs before it have already moved).  A turn's
+    // plan is one throttle value; the steering, Car::update and the path indices
+    // are k's own.  So the turns run as parallel rounds, not one after another:
+    //   round A: every NPC plans against the start-of-step states (Jacobi) and moves;
+    //   round B: every NPC re-plans against the round-A states of the NPCs before
+    //            it and the start states of the NPCs after it.
+    // If round B reproduces every round-A throttle, the round-A moves ARE the
+    // sequential result (induction over k: NPC 0 has no predecessor; when NPCs < k
+    // planned as in sequence, round B gave NPC k exactly its sequential inputs).
+    // Otherwise the first NPC k* that differs takes its round-B throttle (its
+    // inputs were right) and the NPCs after it run the sequential turns.
+    const unsigned long long alive_k = ballot(lane < cnt && nl.alive[lane < cnt ? lane : 0] != 0);
+    if (MEV_NPC_PRIO) {  // the env with the most NPCs to control sets the kernel's end: serve it first
+        const int lvl = __popcll(alive_k) / MEV_NPC_PRIO;
+        if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+        else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
     // NPC kk's ghost points path[idx0 + lane] and path[idx0 + 64 + lane] (clamped;
-    // only indices below min(idx0 + 120, 160) are used), loaded one turn ahead
+    // only indices below min(idx0 + 120, 160) are used)
     auto fetch_ghost = [&](int kk, float2& a, float2& b) {
         const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
         const int i0 = nl.pidx0[kk] + lane, i1 = i0 + WAVE;
         a = P[i0 < PATH_LEN ? i0 : PATH_LEN - 1];
         b = P[i1 < PATH_LEN ? i1 : PATH_LEN - 1];
     };
-    float2 ga = make_float2(0.0f, 0.0f), gb = ga;
-    if (cnt > 0) fetch_ghost(0, ga, gb);
-    for (int k = 0; k < cnt; ++k) {
-        if (MEV_NPC_PRIO) {  // the env with the most NPCs left to control sets the kernel's end: serve it first
-            const int rem = cnt - k;
-            if (rem >= 3 * MEV_NPC_PRIO) __builtin_amdgcn_s_setprio(3);
-            else if (rem >= 2 * MEV_NPC_PRIO) __builtin_amdgcn_s_setprio(2);
-            else if (rem >= MEV_NPC_PRIO) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
+    // the ghost points of NPC kk in the scan layout: lane t of its 16 holds
+    // path[idx0 + 8t .. idx0 + 8t + 7] (clamped; only indices below min(idx0 + 120,
+    // 160) are used)
+    auto load_ghost8 = [&](int kk, float2* gp) {
+        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const int q0 = nl.pidx0[kk] + 8 * (lane & 15);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gp[i] = P[q0 + i < PATH_LEN ? q0 + i : PATH_LEN - 1];
+    };
+    // plan every alive NPC (mixed: round B) into thr.  Lane = (NPC k of the chunk,
+    // other j) over Kp = 8 / 16 / 32 / 64 others.  Then the ghost scans, four NPCs
+    // per pass (16 lanes x 8 path points each); round B reuses round A's scan of
+    // an NPC whose filtered others are the same and all come after it (unmoved).
+    auto plan_all = [&](bool mixed, float* thr) {
+        const int lk = cnt <= 8 ? 3 : (cnt <= 16 ? 4 : (cnt <= 32 ? 5 : 6));
+        const int Kp = 1 << lk;
+        const int kpc = WAVE >> lk;  // NPCs per chunk
+        const int jl = lane & (Kp - 1), kl = lane >> lk;
+        const unsigned long long seg = Kp == WAVE ? ~0ull : ((1ull << Kp) - 1ull);
+        unsigned long long scan_m = 0ull;
+#pragma nounroll
+        for (int k0 = 0; k0 < cnt; k0 += kpc) {
+            const int k = k0 + kl;
+            const int kk = k < cnt ? k : 0;
+            const bool kact = k < cnt && ((alive_k >> kk) & 1ull);
+            const int j = jl;
+            const int jj = j < cnt ? j : 0;
+            const bool jvalid = kact && j < cnt && j != k && ((alive_k >> jj) & 1ull);
+            const bool newj = mixed && j < k;  // j has moved before k's turn
+            const float oxj = newj ? nl.xn[jj] : nl.x[jj], oyj = newj ? nl.yn[jj] : nl.y[jj];
+            const float ohj = newj ? nl.hn[jj] : nl.h[jj], ovj = newj ? nl.vn[jj] : nl.v[jj];
+            const float ocj = newj ? nl.cn[jj] : nl.c[jj], osj = newj ? nl.sn[jj] : nl.s[jj];
+            const NpcPair pr = npc_pair(k, nl.x[kk], nl.y[kk], nl.h[kk], nl.v[kk], nl.c[kk], nl.s[kk], nl.mdc[kk],
+                                        jvalid, j, oxj, oyj, ohj, ovj, ocj, osj);
+            const unsigned long long b30 = ballot(pr.f30), b50 = ballot(pr.f50);
+            const unsigned long long bok = ballot(pr.pok), byf = ballot(pr.yfar);
+            const int sh = kl << lk;
+            float acc_thr = nl.accb[kk];
+            if ((b30 >> sh) & seg) acc_thr = -1.0f;
+            else if ((b50 >> sh) & seg) acc_thr = (-0.2f < acc_thr) ? -0.2f : acc_thr;
+            const unsigned long long em = (bok >> sh) & seg, ym = (byf >> sh) & seg;
+            bool scan = em != 0ull;
+            float t = acc_thr;
+            if (mixed && scan) {
+                const unsigned long long before = k == 0 ? 0ull : (k >= 64 ? ~0ull : (~0ull >> (64 - k)));
+                if (em == nl.em_a[kk] && ym == nl.ym_a[kk] && !(em & before)) {
+                    t = npc_throttle(acc_thr, nl.mc_a[kk]);  // the same scan as in round A
+                    scan = false;
+                }
+            }
+            if (kact && jl == 0) {
+                thr[k] = t;
+                nl.em[k] = em;
+                nl.ym[k] = ym;
+                if (!mixed) { nl.em_a[k] = em; nl.ym_a[k] = ym; nl.mc_a[k] = -1.0f; }
+            }
+            for (unsigned long long sb = ballot(kact && jl == 0 && scan); sb; sb &= sb - 1ull)
+                scan_m |= 1ull << (k0 + (__builtin_ctzll(sb) >> lk));
         }
+        wave_lds_sync();
+        // ghost scans (:88-188), four NPCs per pass: NPC ks[u] on lanes u*16 ..
+        // u*16 + 15, lane t of them testing path points idx0 + 8t .. idx0 + 8t + 7;
+        // the first point in path order with a yielding conflict ends the scan, its
+        // distance is the minimum
+        const float SAFE = CAR_WIDTH * 2.0f;
+        const float SAFE_SQ = SAFE * SAFE;
+#ifdef MEV_X_NOSCAN
+        scan_m = 0;
+#endif
+        while (scan_m) {
+            int ks[4];
+            int nb = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                ks[u] = scan_m ? __builtin_ctzll(scan_m) : 0;
+                if (scan_m) { scan_m &= scan_m - 1ull; ++nb; }
+            }
+            const int u = lane >> 4;
+            const int k = u == 0 ? ks[0] : (u == 1 ? ks[1] : (u == 2 ? ks[2] : ks[3]));
+            const bool act = u < nb;
+            const int g_start = nl.pidx0[k];
+            const int g_end = g_start + 120 < PATH_LEN ? g_start + 120 : PATH_LEN;
+            const int q0 = g_start + 8 * (lane & 15);
+            float2 gp[8];
+            load_ghost8(k, gp);
+            const float x = nl.x[k], y = nl.y[k];
+            const unsigned long long em = act ? nl.em[k] : 0ull, ym = nl.ym[k];
+            // per point: some filtered other within SAFE (near), one of them yielded to (near_y)
+            unsigned near = 0u, near_y = 0u;
+            for (unsigned long long mm = em; mm; mm &= mm - 1ull) {
+                const int o = __builtin_ctzll(mm);
+                const bool newo = mixed && o < k;
+                const float ox = newo ? nl.xn[o] : nl.x[o], oy = newo ? nl.yn[o] : nl.y[o];
+                const unsigned yo = (unsigned)((ym >> o) & 1ull);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float dxg = ox - gp[i].x;
+                    const float dyg = oy - gp[i].y;
+                    const unsigned c = (q0 + i < g_end && dxg * dxg + dyg * dyg < SAFE_SQ) ? 1u : 0u;
+                    near |= c << i;
+                    near_y |= (c & yo) << i;
+                }
+            }
+            // a near point is a conflict if k yields there: to a yielded-to other, or
+            // to anyone when the point is within 15 of k (dist_to_crash, :158-161)
+            unsigned hits = near_y;
+            for (unsigned m = near & ~near_y; m; m &= m - 1u) {
+                const int i = __builtin_ctz(m);
+                float2 g = gp[0];
+#pragma unroll
+                for (int v = 1; v < 8; ++v) g = i == v ? gp[v] : g;
+                if (hypotf(g.x - x, g.y - y) < 15.0f) hits |= 1u << i;
+            }
+            float fd = 0.0f;  // the first conflict's distance to k
+            if (hits) {
+                const int i = __builtin_ctz(hits);
+                float2 g = gp[0];
+#pragma unroll
+                for (int v = 1; v < 8; ++v) g = i == v ? gp[v] : g;
+                fd = hypotf(g.x - x, g.y - y);
+            }
+            const unsigned long long hb = ballot(act && hits != 0u);
+            float mc = -1.0f;  // lane u < nb: the conflict distance of NPC ks[u]
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const unsigned sg = (unsigned)(hb >> (16 * v)) & 0xffffu;
+                const float mv = sg ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fd), 16 * v + __builtin_ctz(sg)))
+                                    : -1.0f;
+                mc = lane == v ? mv : mc;
+            }
+            wave_lds_sync();  // every lane has read this batch's LDS inputs
+            if (lane < nb) {
+                const int kq = lane == 0 ? ks[0] : (lane == 1 ? ks[1] : (lane == 2 ? ks[2] : ks[3]));
+                thr[kq] = npc_throttle(thr[kq], mc);
+                if (!mixed) nl.mc_a[kq] = mc;
+            }
+            wave_lds_sync();
+        }
+    };
+    // move the NPCs in `which` with the throttles thr into the round-A arrays
+    // (xn .. sn, pidxn): Car::update with the steering from part 1 (Car.cpp:9-40)
+    // and the second update_path_index (:343) over path[idx0, idx0 + 50), 8 lanes
+    // per NPC (7 window points each, first minimum wins).  pre: the window points
+    // of the first 8 NPCs, loaded before the plans
+    auto load_window = [&](int kk, float2* w) {
+        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const int pidx0 = nl.pidx0[kk];
+#pragma unroll
+        for (int t = 0; t < 7; ++t) {
+            const int q = pidx0 + sub * 7 + t;
+            w[t] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+        }
+    };
+#ifndef MEV_NPC_PREWIN  // the first move pass's window points loaded before the plans
+#define MEV_NPC_PREWIN 0
+#endif
+    float2 w0[7];
+    if (MEV_NPC_PREWIN && cnt > 0) load_window(grp < cnt ? grp : 0, w0);  // cnt = 0: no valid route to read
+    auto move_all = [&](const float* thr, unsigned long long which, bool use_pre) {
+#ifdef MEV_X_NOMOVE
+        return;
+#endif
+        for (int k0 = 0; k0 < cnt; k0 += 8) {
+            const int k = k0 + grp;
+            const int kk = k < cnt ? k : 0;
+            const bool act = k < cnt && ((which >> kk) & 1ull);
+            float2 w[7];
+            if (MEV_NPC_PREWIN && k0 == 0 && use_pre) {
+#pragma unroll
+                for (int t = 0; t < 7; ++t) w[t] = w0[t];
+            } else {
+                load_window(kk, w);
+            }
+            const int pidx0 = nl.pidx0[kk];
+            Kin kin{nl.x[kk], nl.y[kk], nl.v[kk], nl.h[kk], nl.acc[kk], nl.steer[kk]};
+            float cn, sn;
+            car_update_steered(kin, thr[kk], nl.nsteer[kk], nl.ntan[kk], in.dt, &cn, &sn);
+            float bd = __builtin_inff();
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {
+                const int off = sub * 7 + t;
+                if (off < 50 && pidx0 + off < PATH_LEN) {
+                    const float wdx = w[t].x - kin.x, wdy = w[t].y - kin.y;
+                    const float d = wdx * wdx + wdy * wdy;
+                    if (d < bd) { bd = d; bi = pidx0 + off; }
+                }
+            }
+            auto take = [&](float od, int oi) {
+                if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+            };
+            take(dpp_f(bd, 0xB1), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xf, 0xf, false));    // quad_perm [1,0,3,2]
+            take(dpp_f(bd, 0x4E), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xf, 0xf, false));    // quad_perm [2,3,0,1]
+            take(dpp_f(bd, 0x141), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xf, 0xf, false));  // row_half_mirror
+            if (act && sub == 0) {
+                nl.xn[k] = kin.x; nl.yn[k] = kin.y; nl.vn[k] = kin.v; nl.hn[k] = kin.h;
+                nl.accn[k] = kin.acc; nl.steern[k] = kin.steer; nl.cn[k] = cn; nl.sn[k] = sn;
+                nl.pidxn[k] = bi == 0x7fffffff ? (pidx0 < 0 ? 0 : pidx0) : bi;
+            }
+        }
+        wave_lds_sync();
+    };
+#ifdef MEV_X_NOPLAN
+    if (false) {
+#else
+    if (__popcll(alive_k) >= 2) {
+#endif
+        plan_all(false, nl.thr_a);
+    } else if (lane < cnt) {
+        nl.thr_a[lane] = nl.accb[lane];  // no other NPC to plan against: the cruise throttle
+        wave_lds_sync();
+    }
+    NT(2);  // round A: plans
+    move_all(nl.thr_a, alive_k, true);
+    NT(3);  // round A: moves
+    unsigned long long done_m = alive_k;  // NPCs whose round-A move is final
+    int kseq = cnt;                       // the first NPC left to the sequential turns
+#ifdef MEV_X_NOPLAN
+    if (false) {
+#else
+    if (__popcll(alive_k) >= 2) {
+#endif
+        plan_all(true, nl.thr_b);
+        const bool differs = lane < cnt && ((alive_k >> lane) & 1ull) &&
+                             __float_as_uint(nl.thr_a[lane < cnt ? lane : 0]) !=
+                                 __float_as_uint(nl.thr_b[lane < cnt ? lane : 0]);
+        const unsigned long long diff = ballot(differs);
+        if (diff) {
+            const int ks = __builtin_ctzll(diff);
+            move_all(nl.thr_b, 1ull << ks, false);  // its inputs were the sequential ones
+            if (lane == 0) atomicAdd(p.overflow + 1, (unsigned long long)(cnt - ks - 1));  // diagnostics
+            done_m = alive_k & ((ks == 63 ? ~0ull : ((2ull << ks) - 1ull)));
+            kseq = ks + 1;
+        }
+    }
+    NT(4);  // round B
+    // commit the final moves
+    if (lane < cnt && ((done_m >> lane) & 1ull)) {
+        nl.x[lane] = nl.xn[lane]; nl.y[lane] = nl.yn[lane]; nl.v[lane] = nl.vn[lane]; nl.h[lane] = nl.hn[lane];
+        nl.acc[lane] = nl.accn[lane]; nl.steer[lane] = nl.steern[lane]; nl.c[lane] = nl.cn[lane];
+        nl.s[lane] = nl.sn[lane]; nl.pidx[lane] = nl.pidxn[lane];
+    }
+    wave_lds_sync();
+    // the sequential turns after a round-B disagreement (lane j = other NPC j)
+#ifdef MEV_X_NOSEQ
+    kseq = cnt;
+#endif
+    float2 ga = make_float2(0.0f, 0.0f), gb = ga;
+    if (kseq < cnt) fetch_ghost(kseq, ga, gb);
+    for (int k = kseq; k < cnt; ++k) {
         float2 na = ga, nb = gb;
         if (k + 1 < cnt) fetch_ghost(k + 1, na, nb);  // in flight while NPC k is controlled
         if (nl.alive[k]) {
             const float x = nl.x[k], y = nl.y[k], h = nl.h[k], v = nl.v[k];
-            const float ck = nl.c[k], sk = nl.s[k];
             const int j = lane;
-            const bool jvalid = j < cnt && j != k && nl.alive[j];
+            const bool jvalid = j < cnt && j != k && nl.alive[j < cnt ? j : 0];
             float oxj = 0, oyj = 0, ohj = 0, ovj = 0, ocj = 0, osj = 0;
             if (j < cnt) {
                 oxj = nl.x[j]; oyj = nl.y[j]; ohj = nl.h[j]; ovj = nl.v[j]; ocj = nl.c[j]; osj = nl.s[j];
             }
-            // 2) front car (get_front_car_dist_tf :22-47, used as front < 30 / < 50 at :72-73)
-            const float vx = ck, vy = -sk;
-            bool f30 = false, f50 = false;
-            // |wrap(h - h_j)| and the distance to j: shared by the front-car test and the
-            // ghost-scan filters (the same expressions in the reference, :37/:101/:107)
-            const float dxj = oxj - x;
-            const float dyj = oyj - y;
-            const float dist_j = hypotf(dxj, dyj);
-            const float adiff_j = fabs_f(wrap_angle(h - ohj));
-            if (jvalid) {
-                const float dist = dist_j;
-                if (!(dist > 80.0f)) {
-                    const float dot = (dxj * vx + dyj * vy) / (dist + 1e-5f);
-                    if (dot > 0.8f) {
-                        if (adiff_j < (45.0f * PI_F / 180.0f)) { f30 = dist < 30.0f; f50 = dist < 50.0f; }
-                    }
-                }
-            }
-            NT(2);  // turn: LDS reads, front car
+            const NpcPair pr = npc_pair(k, x, y, h, v, nl.c[k], nl.s[k], nl.mdc[k], jvalid, j, oxj, oyj, ohj, ovj,
+                                        ocj, osj);
             float acc_thr = nl.accb[k];
-            if (ballot(f30)) acc_thr = -1.0f;
-            else if (ballot(f50)) acc_thr = (-0.2f < acc_thr) ? -0.2f : acc_thr;
-            // 3) ghost path scan: the per-other filters first (independent of the ghost point)
-            const float my_dist_to_center = nl.mdc[k];
-            bool pok = false, yfar = false;
-            if (jvalid) {
-                const float angle_diff = adiff_j;
-                pok = true;
-                if (angle_diff < (60.0f * PI_F / 180.0f)) pok = false;
-                if (pok) {
-                    const float dxo = dxj;
-                    const float dyo = dyj;
-                    const float dist_o = dist_j;
-                    if (dist_o > 1e-5f) {
-                        const float mdx = ck, mdy = -sk;
-                        const float two_pi_m = 2.0f * PI_F - angle_diff;
-                        const float adn = (two_pi_m < angle_diff) ? two_pi_m : angle_diff;
-                        const bool parallel = (adn < (30.0f * PI_F / 180.0f)) || (adn > (150.0f * PI_F / 180.0f));
-                        if (parallel) {
-                            const float lon = dxo * mdx + dyo * mdy;
-                            float lsq = dist_o * dist_o - lon * lon;
-                            lsq = (0.0f < lsq) ? lsq : 0.0f;  // std::max(0, .)
-                            const float lat = __builtin_sqrtf(lsq);
-                            const bool sideways = fabs_f(lat) < (LANE_WIDTH_PX * 1.5f);
-                            const bool near_lon = fabs_f(lon) < (CAR_LENGTH * 2.0f);
-                            if (sideways && near_lon) {
-                                const float fdist = 20.0f;
-                                const float mfx = x + mdx * fdist;
-                                const float mfy = y + mdy * fdist;
-                                const float odx = ocj, ody = -osj;
-                                const float ofx = oxj + odx * fdist;
-                                const float ofy = oyj + ody * fdist;
-                                const float fdx = ofx - mfx;
-                                const float fdy = ofy - mfy;
-                                const float fmag = hypotf(fdx, fdy);
-                                if (fmag > 1e-5f) {
-                                    const float flon = fdx * mdx + fdy * mdy;
-                                    float flsq = fmag * fmag - flon * flon;
-                                    flsq = (0.0f < flsq) ? flsq : 0.0f;
-                                    const float flat = __builtin_sqrtf(flsq);
-                                    const float change = fabs_f(flat - lat);
-                                    if (change < (LANE_WIDTH_PX * 0.5f)) pok = false;  // side by side: skip
-                                }
-                            }
-                        }
-                    }
-                }
-                if (pok) {
-                    const float odc = hypotf(oxj - CXf, oyj - CYf);
-                    if (v < 1.0f && ovj > 3.0f && odc < my_dist_to_center + 25.0f) yfar = true;
-                    else if (odc < my_dist_to_center - 5.0f) yfar = true;
-                    else if (fabs_f(odc - my_dist_to_center) <= 5.0f) yfar = k < j;  // address order
-                }
-            }
-            const unsigned long long em = ballot(pok), ym = ballot(yfar);
-            NT(3);  // turn: ghost-scan filters
-            // scan path[idx0, min(idx0 + 120, 160)) in order; the first point with a
-            // yielding conflict wins (its distance is the min, :183-188); only the
-            // others that passed the filters take part (usually none)
-            bool conflict = false;
-            float min_conflict = 1e9f;
-            if (em) {
-                const int g_start = nl.pidx0[k];
-                const int g_end = g_start + 120 < PATH_LEN ? g_start + 120 : PATH_LEN;
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    if (conflict || g_start + c * WAVE >= g_end) break;
-                    const float2 gp = c ? gb : ga;
-                    const bool gv = g_start + c * WAVE + lane < g_end;
-                    const float dtc = hypotf(gp.x - x, gp.y - y);
-                    bool hit = false;
-                    for (unsigned long long mm = em; mm; mm &= mm - 1ull) {
-                        const int o = __builtin_ctzll(mm);
-                        const float ox = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(oxj), o));
-                        const float oy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(oyj), o));
-                        const float dxg = ox - gp.x;
-                        const float dyg = oy - gp.y;
-                        if (dxg * dxg + dyg * dyg < SAFE_SQ && (dtc < 15.0f || ((ym >> o) & 1ull))) hit = true;
-                    }
-                    const unsigned long long m = ballot(gv && hit);
-                    if (m) {
-                        min_conflict = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dtc), __builtin_ctzll(m)));
-                        conflict = true;
-                    }
-                }
-            }
-            NT(4);  // turn: ghost scan
-            // 4) compose (:190-195), then Car::update with the steering part from part 1
-            float thr = acc_thr;
-            if (conflict) {
-                if (min_conflict < 35.0f) thr = -1.0f;
-                else if (min_conflict < 60.0f) thr = -0.8f;
-                else thr = (0.0f < thr) ? 0.0f : thr;
-            }
+            if (ballot(pr.f30)) acc_thr = -1.0f;
+            else if (ballot(pr.f50)) acc_thr = (-0.2f < acc_thr) ? -0.2f : acc_thr;
+            const unsigned long long em = ballot(pr.pok), ym = ballot(pr.yfar);
+            const float mc = em ? npc_ghost_scan(nl.pidx0[k], x, y, ga, gb, em, ym, oxj, oyj, lane) : -1.0f;
+            const float thr = npc_throttle(acc_thr, mc);
             Kin kin{x, y, v, h, nl.acc[k], nl.steer[k]};
             float cn, sn;
             car_update_steered(kin, thr, nl.nsteer[k], nl.ntan[k], in.dt, &cn, &sn);
@@ -675,7 +969,6 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const int best = wave_argmin_dpp(wv ? wdx * wdx + wdy * wdy : __builtin_inff(),
                                              wv ? pidx0 + lane : 0x7fffffff);
             const int pidx_new = best == 0x7fffffff ? (pidx0 < 0 ? 0 : pidx0) : best;
-            NT(5);  // turn: Car::update + second path index
             wave_lds_sync();  // every lane has read this turn's states
             if (lane == 0) {
                 nl.x[k] = kin.x; nl.y[k] = kin.y; nl.v[k] = kin.v; nl.h[k] = kin.h;
@@ -684,11 +977,11 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                 nl.pidx[k] = pidx_new;
             }
             wave_lds_sync();
-            NT(6);  // turn: write back
         }
         ga = na;
         gb = nb;
     }
+    NT(5);  // sequential turns
     // -- NPC-NPC collision: greedy i<j, both removed (:347-356)
     if (lane < cnt) {
         car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
@@ -2173,27 +2466,32 @@ __host__ __device__ inline StepLayout step_layout(const SimParams& p) {
 // (a v_readlane per reload).
 constexpr int kFixedRays = 128;
 constexpr int kPoolBeams = 512;
-template <int NM>
+template <int NM, int KM = 0>
 struct FixedLayout {
     static_assert(NM >= 1 && NM <= 64, "agents per env");
-    static constexpr int cars = (int)lds_al(cars_lds_bytes(NM, 0));
+    static constexpr int beams = NM * kFixedRays < kPoolBeams ? NM * kFixedRays : kPoolBeams;
+    static constexpr int cars = (int)lds_al(cars_lds_bytes(NM, KM));
     static constexpr int rel = cars;
     static constexpr int envw = rel + kFixedRays * 4;
     static constexpr int lidar = envw + 32;
-    static constexpr LidarLayout lay = lidar_layout_beams(NM, kPoolBeams, NM - 1, false);
+    static constexpr LidarLayout lay = lidar_layout_beams(NM, beams, NM - 1 + KM, false);
     static constexpr int bytes = lidar + lay.bytes;
 };
-template <int NM>
+template <int NM, int KM>
 __host__ __device__ inline StepLayout step_layout_t(const SimParams& p) {
     if constexpr (NM == 0) return step_layout(p);
-    else return StepLayout{FixedLayout<NM>::rel, FixedLayout<NM>::rel, FixedLayout<NM>::envw, FixedLayout<NM>::lidar,
-                           FixedLayout<NM>::bytes};
+    else return StepLayout{FixedLayout<NM, KM>::rel, FixedLayout<NM, KM>::rel, FixedLayout<NM, KM>::envw,
+                           FixedLayout<NM, KM>::lidar, FixedLayout<NM, KM>::bytes};
 }
-// the handle's shape fits the compile-time layout of NM agents
-template <int NM>
+// the handle's shape fits the compile-time layout of NM agents and (traffic) KM
+// NPC slots within a wave's 10 KB LDS share, the NPC arrays included
+template <int NM, int KM>
 __host__ __device__ inline bool fixed_fits(const SimParams& p) {
-    // R <= 128 puts every pool (step_pool agents) within kPoolBeams beams
-    return p.N <= NM && p.R <= kFixedRays && !p.traffic && !MEV_FUSED_STAGED && FixedLayout<NM>::bytes <= 10 * 1024;
+    // R <= 128 puts every pool (step_pool agents) within the layout's beams
+    const bool npcs = KM == 0 ? !p.traffic : (p.traffic && p.K <= KM);
+    const size_t npc_lds = KM == 0 ? 0 : sizeof(NpcLDST<(KM ? KM : 1)>);
+    return p.N <= NM && p.R <= kFixedRays && npcs && !MEV_FUSED_STAGED &&
+           (size_t)FixedLayout<NM, KM>::bytes + npc_lds <= 10 * 1024;
 }
 
 // agents per phase-1 pass in k_step (independent dependency chains interleaved)
@@ -2223,8 +2521,9 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
 #if defined(MEV_STAMPS_R)
     STAMP_RAW(0);
 #endif
-    const StepLayout sl = step_layout_t<NM>(p);
-    CarsLDS el = NM ? carve_cars_lds(step_lds, NM, 0) : carve_cars_lds(step_lds, p.N, cars_k(p));
+    constexpr int KF = TRAFFIC ? KM : 0;  // NPC obstacle slots of the compile-time layout
+    const StepLayout sl = step_layout_t<NM, KF>(p);
+    CarsLDS el = NM ? carve_cars_lds(step_lds, NM, KF) : carve_cars_lds(step_lds, p.N, cars_k(p));
     el.head = reinterpret_cast<float*>(step_lds + sl.head);
     el.rel = reinterpret_cast<float*>(step_lds + sl.rel);
     el.envw = reinterpret_cast<int32_t*>(step_lds + sl.envw);
@@ -2246,7 +2545,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
     return;
 #endif
     const int G = step_pool(p);
-    const LidarLayout lay = NM ? FixedLayout<(NM ? NM : 1)>::lay : lidar_layout(G, p.R, lidar_cand_max(p), false);
+    const LidarLayout lay = NM ? FixedLayout<(NM ? NM : 1), KF>::lay : lidar_layout(G, p.R, lidar_cand_max(p), false);
     unsigned char* lbase = step_lds + sl.lidar;
     const int lane = threadIdx.x & (WAVE - 1);
     const int g0 = e * p.N;
@@ -2401,10 +2700,15 @@ template <bool TAB>
 static void launch_fused(const SimParams& p, const SimParams* dp, const StepInputs& in, const Outputs& out,
                          hipStream_t s) {
     if (p.traffic) {
+        if (fixed_fits<1, 32>(p)) {  // compile-time LDS layout (config 4: one ego, <= 32 NPC slots)
+            const unsigned lds = (unsigned)FixedLayout<1, 32>::bytes;  // + the static NpcLDST
+            hipLaunchKernelGGL((k_step<true, TAB, 1, 32>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+            return;
+        }
         const unsigned lds = (unsigned)step_layout(p).bytes;  // + the static NpcLDST
         if (fused_npc_cap(p) == 32) hipLaunchKernelGGL((k_step<true, TAB, 0, 32>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
         else hipLaunchKernelGGL((k_step<true, TAB, 0, 64>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
-    } else if (fixed_fits<8>(p)) {  // compile-time LDS layout
+    } else if (fixed_fits<8, 0>(p)) {  // compile-time LDS layout
         const unsigned lds = (unsigned)FixedLayout<8>::bytes;
         hipLaunchKernelGGL((k_step<false, TAB, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
     } else {

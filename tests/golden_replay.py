@@ -58,6 +58,7 @@ class Report:
     steps: int = 0
     mismatches: List[str] = field(default_factory=list)
     max_obs_diff: float = 0.0
+    seq_turns: int = 0  # NPC turns the controller ran sequentially (handle-wide, npc_stats)
 
     @property
     def ok(self) -> bool:
@@ -188,5 +189,8 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
                     rep.add(f"step {t + 1}: npc route differ")
         if stop_at_first and all(not r.ok for r in reports):
             break
+    seq = h.npc_stats()[1]
+    for r in reports:
+        r.seq_turns = seq
     h.close()
     return reports

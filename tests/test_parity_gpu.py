@@ -42,3 +42,14 @@ def test_same_scenario_replicated_envs(mev, name, kernel):
     reps = _replay(mev, [name] * 37, kernel)
     bad = [i for i, r in enumerate(reps) if not r.ok]
     assert not bad, reps[bad[0]].mismatches[:5]
+
+
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
+def test_dense_traffic_goldens_cover_sequential_fallback(mev, kernel):
+    """The traffic goldens at density 20 bit-exact on both kernel paths, and
+    reporting how often the NPC controller left its parallel rounds for the
+    sequential turns (round B changed a throttle)."""
+    reps = _replay(mev, ["traffic_d20"] * 8, kernel)
+    bad = [r.mismatches[:3] for r in reps if not r.ok]
+    assert not bad, bad
+    print(f"kernel {kernel}: sequential NPC turns over 8 x traffic_d20: {reps[0].seq_turns}")

@@ -1,0 +1,3 @@
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+bash tools/ab_sweep.sh cfg4 2 "" npcprewin npcprio0 npcprio1
