@@ -229,6 +229,14 @@ int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* 
  * step is one sequential loop, cpp/IntersectionEnv.cpp:133-392). */
 int mev_set_step_kernel(mev_handle* h, int32_t kernel);
 int mev_get_step_kernel(const mev_handle* h, int32_t* kernel);
+/* Scheduling (results are identical either way): envs per fused k_step wave.
+ * With few agents per env (N <= 4, no traffic) 2 or 4 envs share a wave's 64
+ * lanes (8 agent slots), so one wave's latency chain steps them all.
+ * 0 = automatic; a request is reduced to fit N * envs <= 8.  mev_get_step_pack
+ * returns what the next step uses (1 on the two-kernel path).  Replaces
+ * nothing in the reference (one env per IntersectionEnv object). */
+int mev_set_step_pack(mev_handle* h, int32_t envs_per_wave);
+int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave);
 
 /* ---- Multi-GPU: the per-step RCCL gather of the stacked outputs ----------
  * envs are sharded over the GPUs of a node, one process and

@@ -38,7 +38,7 @@ EXPORTED = (
     "mev_device_outputs", "mev_npc_overflow", "mev_npc_stats", "mev_use_own_stream", "mev_debug_stamps",
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
     "mev_kernel_timing", "mev_kernel_times", "mev_set_reset_routes", "mev_snapshot_size", "mev_snapshot",
-    "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel",
+    "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel", "mev_set_step_pack", "mev_get_step_pack",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
     "mev_gather_wait", "mev_output_dlpack",
 )
@@ -143,6 +143,8 @@ def load_library(variant: str = None):
                                    ctypes.POINTER(ctypes.c_int64)]
     L.mev_set_step_kernel.argtypes = [_vp, ctypes.c_int32]
     L.mev_get_step_kernel.argtypes = [_vp, i32p]
+    L.mev_set_step_pack.argtypes = [_vp, ctypes.c_int32]
+    L.mev_get_step_pack.argtypes = [_vp, i32p]
     L.mev_configure.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.mev_configure_traffic.argtypes = [_vp, ctypes.c_int32, ctypes.c_float]
     L.mev_set_reward.argtypes = [_vp, f32p]
@@ -472,6 +474,16 @@ class Handle:
         """The kernel path the next step uses: 1 (k_cars + k_lidar) or 2 (fused k_step)."""
         v = ctypes.c_int32()
         _check(self._lib.mev_get_step_kernel(self._h, ctypes.byref(v)))
+        return v.value
+
+    def set_step_pack(self, envs_per_wave: int = 0):
+        """Envs per fused k_step wave: 0 automatic, 1, 2 or 4 (scheduling only; results identical)."""
+        _check(self._lib.mev_set_step_pack(self._h, int(envs_per_wave)))
+
+    def step_pack(self) -> int:
+        """Envs per wave the next step uses (1 on the two-kernel path)."""
+        v = ctypes.c_int32()
+        _check(self._lib.mev_get_step_pack(self._h, ctypes.byref(v)))
         return v.value
 
     def set_reset_routes(self, routes):

@@ -825,6 +825,22 @@ int mev_get_step_kernel(const mev_handle* h, int32_t* kernel) {
     return MEV_OK;
 }
 
+int mev_set_step_pack(mev_handle* h, int32_t envs_per_wave) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (envs_per_wave != 0 && envs_per_wave != 1 && envs_per_wave != 2 && envs_per_wave != 4)
+        return fail(MEV_E_INVALID, "envs per wave must be 0 (auto), 1, 2 or 4");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->sp.step_pack = envs_per_wave;
+    return MEV_OK;
+}
+
+int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave) {
+    if (!h || !envs_per_wave) return fail(MEV_E_INVALID, "null argument");
+    *envs_per_wave = mev::step_kernel_for(h->sp) == 2 ? mev::step_pack(h->sp) : 1;
+    return MEV_OK;
+}
+
 int mev_set_reset_routes(mev_handle* h, const int32_t* routes, int32_t count) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (count < 0 || count > h->nroutes) return fail(MEV_E_INVALID, "count must be in [0, number of routes]");

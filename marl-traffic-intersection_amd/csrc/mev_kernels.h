@@ -91,6 +91,8 @@ struct SimParams {
     int32_t n_reset_routes;
     // step kernel choice (host side): 0 auto, 1 k_cars + k_lidar, 2 fused k_step
     int32_t step_kernel;
+    // envs per fused k_step wave (host side): 0 auto, 1, 2 or 4 (reduced to fit 8 agent slots)
+    int32_t step_pack;
 };
 
 struct StepInputs {
@@ -106,6 +108,8 @@ struct StepInputs {
 // k_step (one wave per env); 0 when p.step_kernel == 2 but k_step cannot run p
 // (traffic mode, or a pool that does not fit a wave's LDS budget).
 int step_kernel_for(const SimParams& p);
+// envs per k_step wave the fused path uses for p (1, 2 or 4)
+int step_pack(const SimParams& p);
 // ev (nullable): three events recorded before k_cars, between k_cars and k_lidar, after k_lidar
 // (with k_step: before it, and twice after it)
 // dp: a device copy of p (k_step reads its parameters through it)

@@ -907,7 +907,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     NT(3);  // round A: moves
     unsigned long long done_m = alive_k;  // NPCs whose round-A move is final
     int kseq = cnt;                       // the first NPC left to the sequential turns
-#ifdef MEV_X_NOPLAN
+#if defined(MEV_X_NOPLAN) || defined(MEV_X_NOB)
     if (false) {
 #else
     if (__popcll(alive_k) >= 2) {
@@ -1204,9 +1204,10 @@ struct CarsCtx {
 // instead of delaying this wave's.  FUSED: the LiDAR runs in the same wave
 // (k_step) and reads the obstacle table and candidate masks from LDS, so they
 // are not published to HBM.
-template <bool TRAFFIC, bool FUSED, class NL>
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
                                             const CarsLDS& el, NL* nl) {
+    static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
     // status, collisions, respawn, observation head); the LiDAR block of the
     // observation is filled by the LiDAR body right after.  Per-agent phases run on
@@ -1215,7 +1216,12 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // memory is touched in two dependent rounds (state, then route table) and
     // written once at the end.
     const int tid = threadIdx.x & (WAVE - 1);
-    const int N = p.N;
+    const int NE = p.N;  // agents per env
+    // PK > 1 (k_step, few agents per env): the wave steps envs e .. e + npk - 1;
+    // agent slot i is agent i % NE of env e + i / NE, global agent e * NE + i
+    // (consecutive envs are consecutive in the SoA).  N: the wave's agent slots.
+    const int npk = PK == 1 ? 1 : (p.E - e < PK ? p.E - e : PK);
+    const int N = PK == 1 ? NE : npk * NE;
     // STAGE: every output and the state are written at the end of k_step (fused_store)
     constexpr bool STAGE = FUSED && MEV_FUSED_STAGED;
 
@@ -1224,8 +1230,9 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // add_car_with_route, :66-131).
     // Every load is issued up front (one round trip); only an env being reset
     // waits a second round for its spawn poses.
-    const bool pending = p.pending_reset[e] != 0;
-    const int step_prev = p.step_count[e];
+    const int ee = PK == 1 ? e : e + (tid < N ? tid : 0) / NE;  // the lane's env (lane = agent slot)
+    const bool pending = p.pending_reset[ee] != 0;
+    const int step_prev = p.step_count[ee];
     const int npcs_prev = TRAFFIC ? p.npc.count[e] : 0;
     const bool do_reset = in.auto_reset && pending;
     const int prev_step = do_reset ? 0 : step_prev;
@@ -1236,7 +1243,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     NpcRegs nreg{};
     if constexpr (TRAFFIC) nreg = npc_load(p, e, tid);  // in flight with the ego loads
     for (int i = tid; i < N; i += WAVE) {
-        const int g = e * N + i;
+        const int g = e * NE + i;
         const int route_l = egoi(p, EF_ROUTE)[g];
         const float a0 = in.actions[2 * g], a1 = in.actions[2 * g + 1];
         const float x = egof(p, EF_X)[g], y = egof(p, EF_Y)[g], v = egof(p, EF_V)[g], h = egof(p, EF_H)[g];
@@ -1248,7 +1255,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         el.a0[i] = a0;
         el.a1[i] = a1;
         if (do_reset) {
-            const int rid = reset_route(p, in.rng_counter, e, i, route_l);
+            const int rid = reset_route(p, in.rng_counter, ee, PK == 1 ? i : i - (ee - e) * NE, route_l);
             const float rx = p.rt.spawn[3 * rid], ry = p.rt.spawn[3 * rid + 1], rh = p.rt.spawn[3 * rid + 2];
             el.route[i] = rid;
             el.x[i] = rx; el.y[i] = ry; el.v[i] = 0.0f; el.h[i] = rh;
@@ -1420,7 +1427,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         const int pi = pbase + tid;
         if (pi < N * N) {
             const int a = pi / N, b = pi % N;
-            if (a < b && el.alive[a] && el.alive[b] &&
+            if (a < b && (PK == 1 || a / NE == b / NE) && el.alive[a] && el.alive[b] &&
                 sat_collide(reinterpret_cast<const float*>(&el.cx[a]), reinterpret_cast<const float*>(&el.cy[a]),
                             el.c[a], el.s[a], reinterpret_cast<const float*>(&el.cx[b]),
                             reinterpret_cast<const float*>(&el.cy[b]), el.c[b], el.s[b]))
@@ -1513,7 +1520,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         if (pi < N * nob) {
             const int a = pi / nob, o = pi - a * nob;
             const float cx = el.x[a], cy = el.y[a];
-            if (o != a && el.alive[a] &&
+            if (o != a && (PK == 1 || a / NE == o / NE) && el.alive[a] &&
                 !(fabs_f(el.px[o] - cx) < 1e-3f && fabs_f(el.py[o] - cy) < 1e-3f && fabs_f(el.ph[o] - el.h[a]) < 1e-3f)) {
                 const int4 bx = el.box[o];
                 const float ddx = fmaxf(fmaxf((float)bx.x - cx, cx - (float)bx.y), 0.0f);
@@ -1526,7 +1533,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     wave_lds_sync();
     if (!FUSED) {
         for (int i = tid; i < N; i += WAVE) {
-            const int g = e * N + i;
+            const int g = e * NE + i;
             p.ob_cand[2 * g] = el.cand[2 * i];
             p.ob_cand[2 * g + 1] = el.cand[2 * i + 1];
         }
@@ -1540,11 +1547,13 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
 // k_cars): bonuses, team mix and env flags (:320-370), the reward / done /
 // status outputs and the state write-back, the observation head (:418-520).
 // Reads only the car LDS (the LiDAR never writes it).
-template <bool TRAFFIC, bool FUSED, class NL>
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1>
 __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out, const int e, const CarsLDS& el,
                                           const NL* nl, const CarsCtx& cx) {
     const int tid = threadIdx.x & (WAVE - 1);
-    const int N = p.N;
+    const int NE = p.N;  // agents per env (PK > 1: see cars_pre)
+    const int npk = PK == 1 ? 1 : (p.E - e < PK ? p.E - e : PK);
+    const int N = PK == 1 ? NE : npk * NE;
     constexpr bool STAGE = FUSED && MEV_FUSED_STAGED;
     const int step_no = cx.step_no, ncnt = cx.ncnt;
     const bool do_reset = cx.do_reset;
@@ -1564,26 +1573,47 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
         }
         if (p.use_team && N > 0) {  // sequential sum in agent order, as the reference
             float avg = 0.0f;
-            for (int a = 0; a < N; ++a) avg += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), a));
-            avg /= float(N);
+            if (PK == 1) {
+                for (int a = 0; a < N; ++a) avg += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), a));
+                avg /= float(N);
+            } else {
+                for (int ps = 0; ps < npk; ++ps) {  // each env's own mean
+                    float sm = 0.0f;
+                    for (int a = 0; a < NE; ++a)
+                        sm += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), ps * NE + a));
+                    sm /= float(NE);
+                    avg = (i < N && i / NE == ps) ? sm : avg;
+                }
+            }
             rew_i = (1.0f - p.alpha) * rew_i + p.alpha * avg;
         }
         const unsigned long long alive_m = ballot(in_env && alive_i);
         const unsigned long long succ_m = ballot(in_env && alive_i && done_i && st_i == ST_SUCCESS);
         const unsigned long long done_m = ballot(in_env && done_i);
-        const int alive_cnt = __builtin_popcountll(alive_m), succ_cnt = __builtin_popcountll(succ_m);
-        const bool terminated = p.respawn ? (succ_cnt > 0 && succ_cnt == alive_cnt) : (done_m != 0ull);
-        const bool truncated = p.max_steps > 0 && step_no >= p.max_steps;
+        // the env flags: lane ps < npk holds env e + ps (PK == 1: every lane env e)
+        unsigned long long emask = ~0ull;
+        int step_e = step_no;
+        if (PK > 1) {
+            const unsigned long long one = NE >= 64 ? ~0ull : ((1ull << NE) - 1ull);
+            emask = tid < npk ? one << (tid * NE) : 0ull;
+            for (int ps = 0; ps < npk; ++ps) {
+                const int v = __builtin_amdgcn_readlane(step_no, ps * NE);
+                step_e = tid == ps ? v : step_e;
+            }
+        }
+        const int alive_cnt = __builtin_popcountll(alive_m & emask), succ_cnt = __builtin_popcountll(succ_m & emask);
+        const bool terminated = p.respawn ? (succ_cnt > 0 && succ_cnt == alive_cnt) : ((done_m & emask) != 0ull);
+        const bool truncated = p.max_steps > 0 && step_e >= p.max_steps;
         if (in_env) {
             if (STAGE) el.rew[i] = rew_i;
             else {
-                const int g = e * N + i;
+                const int g = e * NE + i;
                 out.rew[g] = rew_i;
                 out.done[g] = done_i;
                 out.status[g] = st_i;
             }
         }
-        if (tid == 0) {
+        if (PK > 1 ? tid < npk : tid == 0) {
             if constexpr (STAGE) {
                 el.envw[0] = terminated;
                 el.envw[1] = truncated;
@@ -1592,12 +1622,13 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
                 el.envw[4] = (terminated || truncated) ? 1 : 0;
                 el.envw[5] = do_reset;
             } else {
-                p.step_count[e] = step_no;
-                out.term[e] = terminated;
-                out.trunc[e] = truncated;
-                out.alive_cnt[e] = alive_cnt;
-                out.step[e] = step_no;
-                p.pending_reset[e] = (terminated || truncated) ? 1 : 0;
+                const int ev = e + (PK > 1 ? tid : 0);
+                p.step_count[ev] = step_e;
+                out.term[ev] = terminated;
+                out.trunc[ev] = truncated;
+                out.alive_cnt[ev] = alive_cnt;
+                out.step[ev] = step_e;
+                p.pending_reset[ev] = (terminated || truncated) ? 1 : 0;
             }
         }
     }
@@ -1605,7 +1636,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
     // writes it at its end (fused_store)
     if (!STAGE) {
         for (int i = tid; i < N; i += WAVE) {
-            const int g = e * N + i;
+            const int g = e * NE + i;
             egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
             egof(p, EF_ACC)[g] = el.acc[i]; egof(p, EF_STEER)[g] = el.steer[i]; egoi(p, EF_PIDX)[g] = el.pidx[i];
             egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
@@ -1621,7 +1652,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
     return;
 #endif
     // ---- observation head (:418-520)
-    const int C = N + (TRAFFIC ? ncnt : 0);
+    const int C = PK > 1 ? NE : N + (TRAFFIC ? ncnt : 0);  // neighbour candidates per agent (+ itself)
     if (C <= 8) {
         // lane (grp, sub): agent i0 + grp, neighbour candidate sub; rank = position
         // in the stable distance order (== libstdc++ insertion sort, <= 16 elements)
@@ -1632,13 +1663,14 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             const bool alv = act && el.alive[ii] != 0;
             const float x = el.x[ii], y = el.y[ii], v = el.v[ii], h = el.h[ii];
             const int j = sub;
+            const int js = PK == 1 ? j : (ii / NE) * NE + j;  // candidate j's agent slot
             bool valid = false;
             float ox = 0.0f, oy = 0.0f, ov = 0.0f, oh = 0.0f;
             int oi = 0;
-            if (alv && j < C && j != ii) {
-                if (j < N) {
-                    valid = el.alive[j] != 0;
-                    ox = el.x[j]; oy = el.y[j]; ov = el.v[j]; oh = el.h[j]; oi = el.intent[j];
+            if (alv && j < C && js != ii) {
+                if (js < N) {
+                    valid = el.alive[js] != 0;
+                    ox = el.x[js]; oy = el.y[js]; ov = el.v[js]; oh = el.h[js]; oi = el.intent[js];
                 } else {
                     const int kk = j - N;
                     valid = nl->alive[kk] != 0;
@@ -1667,7 +1699,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             // one straight-line block for every lane: the agent's own features (the
             // lane of its own index: never a candidate), its look-ahead terms, or a
             // neighbour's features -- the atan2f chain runs beside the divisions
-            const bool self = j == ii;
+            const bool self = js == ii;
             const float dxd = el.tgx[ii] - x, dyd = el.tgy[ii] - y;  // path[min(idx + 10, 159)] (:444-452)
             const float f4 = __builtin_sqrtf(dxd * dxd + dyd * dyd) / float(WIDTH);
             const float f5 = wrap_angle(atan2f(-dyd, dxd) - h) / PI_F;
@@ -1677,7 +1709,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             const float f3 = (self ? h : wrap_angle(oh - h)) / PI_F;
             if (act) {
                 // k_step stages the head in LDS (written with the LiDAR block by fused_store)
-                float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)(e * N + i) * p.D;
+                float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)(e * NE + i) * p.D;
                 if (!alv) {
                     for (int cc = sub; cc < OBS_HEAD; cc += 8) row[cc] = 0.0f;
                 } else {
@@ -1699,7 +1731,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
         }
     } else {
         for (int i = tid; i < N; i += WAVE) {
-            const int g = e * N + i;
+            const int g = e * NE + i;
             float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)g * p.D;
             if (!el.alive[i]) {
                 for (int c = 0; c < OBS_HEAD; ++c) row[c] = 0.0f;
@@ -2513,11 +2545,12 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // live through the whole kernel and the SGPR allocator spills them into VGPR
 // lanes (a v_readlane per reload); through the pointer each field is an s_load
 // next to its use.
-template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK>
+template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1>
 __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
     const SimParams& p = *pp;
     extern __shared__ __align__(16) unsigned char step_lds[];
-    const int e = xcd_env((int)blockIdx.x, p.E);
+    // PK envs per wave (few agents per env): envs e .. e + PK - 1, see cars_pre
+    const int e = xcd_env((int)blockIdx.x, (int)gridDim.x) * PK;
 #if defined(MEV_STAMPS_R)
     STAMP_RAW(0);
 #endif
@@ -2531,11 +2564,11 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
     NpcLDST<KM>* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
     if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
-    const CarsCtx cx = cars_pre<TRAFFIC, true>(p, in, out, e, el, nl);
+    const CarsCtx cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK>(p, in, out, e, el, nl);
     wave_lds_sync();
 #if !defined(MEV_EXP_STOP) || MEV_EXP_STOP != 0  // timing-only stop0: the car part without cars_post
     if (!MEV_POST_AFTER_LIDAR) {
-        cars_post<TRAFFIC, true>(p, out, e, el, nl, cx);
+        cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
         wave_lds_sync();
     }
 #else
@@ -2544,20 +2577,24 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 1  // timing-only: the car part alone
     return;
 #endif
-    const int G = step_pool(p);
+    // agent slots of this wave and its LiDAR pools of <= 512 beams (one at config 3)
+    const int NS = PK == 1 ? p.N : (p.E - e < PK ? p.E - e : PK) * p.N;
+    int G = 512 / (p.R > 0 ? p.R : 1);
+    G = G < 1 ? 1 : (G < NS ? G : NS);
+    if (PK == 1) G = step_pool(p);
     const LidarLayout lay = NM ? FixedLayout<(NM ? NM : 1), KF>::lay : lidar_layout(G, p.R, lidar_cand_max(p), false);
     unsigned char* lbase = step_lds + sl.lidar;
     const int lane = threadIdx.x & (WAVE - 1);
     const int g0 = e * p.N;
-    for (int j0 = 0; j0 < p.N; j0 += G) {  // pools of G agents (one at config 3)
+    for (int j0 = 0; j0 < NS; j0 += G) {  // pools of G agents (one at config 3)
         if (j0 > 0) wave_lds_sync();
         if (j0 > 0 || MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);  // each pool
-        const int na = p.N - j0 < G ? p.N - j0 : G;
+        const int na = NS - j0 < G ? NS - j0 : G;
         lidar_body<TAB, MEV_PHASE1_ILP>(p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
     }
     if (MEV_POST_AFTER_LIDAR) {  // experiment (variant postlate): measured slower, 41.6 -> 44.1 us
         if (MEV_PRIO_POST >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_POST);
-        cars_post<TRAFFIC, true>(p, out, e, el, nl, cx);
+        cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
     }
     if (MEV_FUSED_STAGED) {
         wave_lds_sync();
@@ -2696,6 +2733,23 @@ int step_kernel_for(const SimParams& p) {
     return (fusable && fused_lds_bytes(p) <= 10 * 1024 && p.E >= 1024) ? 2 : 1;
 }
 
+// envs per k_step wave (1, 2 or 4) for a handle without traffic whose N agents
+// fit the 8-slot layout: several small envs share a wave's lanes, so one latency
+// chain serves them all.  p.step_pack (mev_set_step_pack) chooses; 0 = automatic.
+// Automatic: the most envs per wave that keeps >= 2048 waves (2 per SIMD) --
+// config 2 (4096 x 1 agent): 2 envs per wave, 177 -> 202 M agent-steps/s; 4
+// envs per wave (1024 waves, one per SIMD) 194 M (profiles/r2_pack_sweep.txt).
+int step_pack(const SimParams& p) {
+    if (p.traffic || !fixed_fits<8, 0>(p)) return 1;
+    int pk = p.step_pack;
+    if (pk != 1 && pk != 2 && pk != 4) {
+        pk = 4;
+        while (pk > 1 && p.E / pk < 2048) pk /= 2;
+    }
+    while (pk > 1 && pk * p.N > 8) pk /= 2;
+    return pk;
+}
+
 template <bool TAB>
 static void launch_fused(const SimParams& p, const SimParams* dp, const StepInputs& in, const Outputs& out,
                          hipStream_t s) {
@@ -2710,7 +2764,10 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         else hipLaunchKernelGGL((k_step<true, TAB, 0, 64>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
     } else if (fixed_fits<8, 0>(p)) {  // compile-time LDS layout
         const unsigned lds = (unsigned)FixedLayout<8>::bytes;
-        hipLaunchKernelGGL((k_step<false, TAB, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+        const int pk = step_pack(p);
+        if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3((p.E + 3) / 4), dim3(WAVE), lds, s, dp, in, out);
+        else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2>), dim3((p.E + 1) / 2), dim3(WAVE), lds, s, dp, in, out);
+        else hipLaunchKernelGGL((k_step<false, TAB, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
     } else {
         const unsigned lds = (unsigned)step_layout(p).bytes;
         hipLaunchKernelGGL((k_step<false, TAB, 0>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);

@@ -132,6 +132,21 @@ def _oracle_from_state(cfg, st, e, troutes):
 @pytest.mark.parametrize("kernel", STEP_KERNELS)
 @pytest.mark.parametrize("cfg", CONFIGS, ids=[c["name"] for c in CONFIGS])
 def test_random_states_match_oracle(mev, cfg, kernel):
+    _random_states_vs_oracle(mev, cfg, kernel)
+
+
+PACKED = [c for c in CONFIGS if c["n"] <= 4 and not c.get("traffic")]
+
+
+@pytest.mark.parametrize("pack", [2, 4])
+@pytest.mark.parametrize("cfg", PACKED, ids=[c["name"] for c in PACKED])
+def test_random_states_match_oracle_packed_waves(mev, cfg, pack):
+    """Several envs per fused k_step wave (mev_set_step_pack), each env from its
+    own random state: every output and the state after every step bit-exact."""
+    _random_states_vs_oracle(mev, cfg, 2, pack)
+
+
+def _random_states_vs_oracle(mev, cfg, kernel, pack=0):
     rng = np.random.default_rng(zlib.crc32(cfg["name"].encode()))
     E, T = 24, 50
     n, lanes = cfg["n"], cfg.get("lanes", 3)
@@ -143,6 +158,9 @@ def test_random_states_match_oracle(mev, cfg, kernel):
                    max_steps=cfg.get("max_steps", 2000), max_npcs=64,
                    reward=cfg.get("reward", [10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2]))
     use_step_kernel(mev, h, kernel)
+    if pack:
+        h.set_step_pack(pack)
+        assert h.step_pack() == (pack if pack * n <= 8 else max(1, 8 // n)), h.step_pack()
     table = ROUTES2 if lanes == 2 else ROUTES3
     st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0))
     h.set_traffic_routes(troutes)

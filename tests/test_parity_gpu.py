@@ -53,3 +53,28 @@ def test_dense_traffic_goldens_cover_sequential_fallback(mev, kernel):
     bad = [r.mismatches[:3] for r in reps if not r.ok]
     assert not bad, bad
     print(f"kernel {kernel}: sequential NPC turns over 8 x traffic_d20: {reps[0].seq_turns}")
+
+
+PACKABLE = [n for n in SINGLE if G.load(n)["meta"]["n_agents"] <= 4 and not G.load(n)["meta"]["traffic"]]
+
+
+@pytest.mark.parametrize("pack", [2, 4])
+@pytest.mark.parametrize("name", PACKABLE)
+def test_golden_scenario_packed_waves(mev, name, pack):
+    """Several envs per fused k_step wave (mev_set_step_pack): each golden
+    scenario replicated into 7 envs (the last wave partly filled), every env
+    bit-exact against the reference."""
+    reps = G.replay(mev, [name] * 7, kernel=2, pack=pack)
+    assert reps is not None
+    bad = [(i, r.mismatches[:3]) for i, r in enumerate(reps) if not r.ok]
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("pack", [2, 4])
+def test_golden_routes_packed_in_one_handle(mev, pack):
+    """The 12 config-2 route scenarios as 12 envs of ONE handle, 2 or 4 envs per
+    fused wave: neighbours in a wave hold different states, each env bit-exact."""
+    names = [n for n in SINGLE if n.startswith("cfg2_r64_route")]
+    reps = G.replay(mev, names, kernel=2, pack=pack)
+    bad = [(r.name, r.mismatches[:3]) for r in reps if not r.ok]
+    assert not bad, bad

@@ -72,6 +72,34 @@ def test_fused_and_two_kernel_paths_agree_full_size(mev, rays):
         h.close()
 
 
+@pytest.mark.parametrize("pack", [2, 4])
+def test_packed_waves_agree_full_size(mev, pack):
+    """Config 2 shape (4096 envs x 1 agent x 64 beams) and 4096 x 2 agents:
+    2 or 4 envs per fused k_step wave == one env per wave == k_cars + k_lidar,
+    bit for bit, step after step with auto-reset on."""
+    for n in (1, 2):
+        cfg = dict(num_envs=E, num_agents=n, lidar_rays=64, use_team_reward=1, max_steps=90, seed=5)
+        hs = [mev.Handle(**cfg) for _ in range(3)]
+        hs[0].set_step_kernel(1)
+        hs[1].set_step_kernel(2)
+        hs[1].set_step_pack(1)
+        hs[2].set_step_kernel(2)
+        hs[2].set_step_pack(pack)
+        assert hs[2].step_pack() == pack and hs[1].step_pack() == 1
+        rng = np.random.default_rng(13)
+        for t in range(120):
+            a = rng.uniform(-1, 1, (E, n, 2)).astype(np.float32)
+            o = [h.step(a, auto_reset=True) for h in hs]
+            for k in o[0]:
+                assert np.array_equal(o[0][k], o[1][k]), (n, t, k)
+                assert np.array_equal(o[0][k], o[2][k]), (n, t, k)
+        s = [h.get_state() for h in hs]
+        for k in s[0]:
+            assert np.array_equal(s[0][k], s[2][k]), (n, k)
+        for h in hs:
+            h.close()
+
+
 def test_fused_and_two_kernel_paths_agree_traffic_full_size(mev):
     """Config 4 shape (4096 envs x 1 ego x 64 beams, traffic at density 0.5 with
     the Philox spawn stream, 32 NPC slots): the fused k_step (NPC phase, car

@@ -1,3 +1,4 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-bash tools/ab_sweep.sh cfg4 2 "" npcprewin npcprio0 npcprio1
+bash tools/ab_sweep.sh cfg4 1 "" x_noscan x_nob x_noplan
+bash tools/ab_sweep.sh cfg2 1 ""

@@ -24,7 +24,7 @@ CONFIGS = [
 ]
 
 
-def run(cfg, steps, warmup, step_kernel=0):
+def run(cfg, steps, warmup, step_kernel=0, pack=0):
     import torch
     import pkgload
     mev = pkgload.load()
@@ -35,6 +35,8 @@ def run(cfg, steps, warmup, step_kernel=0):
                    max_npcs=32)
     if step_kernel:
         h.set_step_kernel(step_kernel)
+    if pack:
+        h.set_step_pack(pack)
     st = torch.cuda.Stream(dev)
     torch.cuda.set_stream(st)
     h.set_stream(st.cuda_stream)
@@ -52,9 +54,11 @@ def run(cfg, steps, warmup, step_kernel=0):
     dt = (time.perf_counter() - t0) / steps
     c, l_, n = h.kernel_times()
     npc = float(h.get_state()["npc_count"].mean()) if cfg.get("traffic") else 0.0
+    pk = h.step_pack()
     h.close()
     r = dict(name=cfg["name"], workload=cfg["desc"], agent_steps_per_s=round(E * N / dt, 1),
              ms_per_step=round(dt * 1e3, 5), step_kernel="k_step (fused)" if fused else "k_cars + k_lidar",
+             envs_per_wave=pk,
              mean_npcs=round(npc, 3))
     if fused:
         r["k_step_ms_events"] = round(c / n, 5)
@@ -70,12 +74,13 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="comma-separated config names (e.g. cfg4)")
     ap.add_argument("--step-kernel", type=int, default=0, help="0 auto, 1 k_cars + k_lidar, 2 fused k_step")
+    ap.add_argument("--pack", type=int, default=0, help="envs per fused wave: 0 auto, 1, 2, 4")
     a = ap.parse_args()
     res = []
     for cfg in CONFIGS:
         if a.only and cfg["name"] not in a.only.split(","):
             continue
-        r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup, a.step_kernel)
+        r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup, a.step_kernel, a.pack)
         print(json.dumps(r), flush=True)
         res.append(r)
     if a.out:
