@@ -59,6 +59,7 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # k_cars' NPC-count priorities (product: level = NPCs left / 2): off / per NPC / per 3 NPCs
                # exact variant: the NPC controller's first move pass loads its path windows before the plans
                "npcprewin": ["-DMEV_NPC_PREWIN=1"],
+               "npcpf": ["-DMEV_NPC_PREFETCH=1"],
                "npcprio1": ["-DMEV_NPC_PRIO=1"], "npcprio3": ["-DMEV_NPC_PRIO=3"],
                "npcprio0": ["-DMEV_NPC_PRIO=0"],
                # timing-only (wrong results): NPC controller without ghost scans / without round B

@@ -629,6 +629,16 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         const bool act = k < cnt;
         const int kk = act ? k : 0;  // idle groups mirror NPC 0 so every lane reaches the DPP moves
         const float x = nl.x[kk], y = nl.y[kk];
+#ifndef MEV_NPC_PREFETCH  // touch the path lines the ghost scans and moves read, while part 1 runs
+#define MEV_NPC_PREFETCH 0
+#endif
+        float2 pf0 = make_float2(0.0f, 0.0f), pf1 = pf0;
+        if (MEV_NPC_PREFETCH) {
+            const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+            const int s0 = (nl.pidx[kk] < 0 ? 0 : nl.pidx[kk]) + 64 + sub * 16;
+            pf0 = P[s0 < PATH_LEN ? s0 : PATH_LEN - 1];
+            pf1 = P[s0 + 8 < PATH_LEN ? s0 + 8 : PATH_LEN - 1];
+        }
         float2 pt[8];
         int start_i;
         const int pidx0 = npc_window(kk, nl.pidx[kk], x, y, pt, start_i);
@@ -659,6 +669,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             nl.endx[k] = pe.x;
             nl.endy[k] = pe.y;
         }
+        if (MEV_NPC_PREFETCH) asm volatile("" ::"v"(pf0.x), "v"(pf1.x));  // keep the touches (values unused)
     }
     wave_lds_sync();
     NT(1);  // part 1
@@ -750,6 +761,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                 scan_m |= 1ull << (k0 + (__builtin_ctzll(sb) >> lk));
         }
         wave_lds_sync();
+        if (mixed) NT(4); else NT(2);  // the pair pass
         // ghost scans (:88-188), four NPCs per pass: NPC ks[u] on lanes u*16 ..
         // u*16 + 15, lane t of them testing path points idx0 + 8t .. idx0 + 8t + 7;
         // the first point in path order with a yielding conflict ends the scan, its
@@ -760,6 +772,9 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         scan_m = 0;
 #endif
         while (scan_m) {
+#ifdef MEV_STAMPS_N
+            nt_acc[5] += 1;  // scan passes
+#endif
             int ks[4];
             int nb = 0;
 #pragma unroll
@@ -796,7 +811,16 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             // a near point is a conflict if k yields there: to a yielded-to other, or
             // to anyone when the point is within 15 of k (dist_to_crash, :158-161)
             unsigned hits = near_y;
-            for (unsigned m = near & ~near_y; m; m &= m - 1u) {
+            unsigned close = 0u, unsure = 0u;  // dist_to_crash < 15 surely / too close to 15 to tell in f32
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float dx = gp[i].x - x, dy = gp[i].y - y;
+                const float d2 = dx * dx + dy * dy;  // within a few ulp of the double sum hypotf rounds
+                close |= (d2 < 224.0f ? 1u : 0u) << i;
+                unsure |= (d2 >= 224.0f && d2 <= 226.0f ? 1u : 0u) << i;
+            }
+            hits |= near & close;
+            for (unsigned m = near & ~hits & unsure; m; m &= m - 1u) {  // exact test only near 15
                 const int i = __builtin_ctz(m);
                 float2 g = gp[0];
 #pragma unroll
@@ -828,6 +852,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             }
             wave_lds_sync();
         }
+        NT(6);  // the ghost scans
     };
     // move the NPCs in `which` with the throttles thr into the round-A arrays
     // (xn .. sn, pidxn): Car::update with the steering from part 1 (Car.cpp:9-40)
@@ -902,7 +927,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         nl.thr_a[lane] = nl.accb[lane];  // no other NPC to plan against: the cruise throttle
         wave_lds_sync();
     }
-    NT(2);  // round A: plans
+    NT(2);  // round A: plans (pairs)
     move_all(nl.thr_a, alive_k, true);
     NT(3);  // round A: moves
     unsigned long long done_m = alive_k;  // NPCs whose round-A move is final
@@ -925,7 +950,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             kseq = ks + 1;
         }
     }
-    NT(4);  // round B
+    NT(3);  // round B's re-move
     // commit the final moves
     if (lane < cnt && ((done_m >> lane) & 1ull)) {
         nl.x[lane] = nl.xn[lane]; nl.y[lane] = nl.yn[lane]; nl.v[lane] = nl.vn[lane]; nl.h[lane] = nl.hn[lane];
@@ -981,7 +1006,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         ga = na;
         gb = nb;
     }
-    NT(5);  // sequential turns
+    NT(3);  // sequential turns (with the moves)
     // -- NPC-NPC collision: greedy i<j, both removed (:347-356)
     if (lane < cnt) {
         car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);

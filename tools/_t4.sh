@@ -1,4 +1,3 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-bash tools/ab_sweep.sh cfg4 1 "" x_noscan x_nob x_noplan
-bash tools/ab_sweep.sh cfg2 1 ""
+MEV_LIB_VARIANT=stampsn timeout -k 10 200 python tools/npc_profile.py --parts 2>&1 | grep -v amdgpu

@@ -43,7 +43,8 @@ def main():
     print(f"k_cars {c / n * 1e3:.1f} us, k_lidar {l_ / n * 1e3:.1f} us per step; NPCs per env mean {kk.mean():.2f} "
           f"max {kk.max()}; per-step max NPCs over envs (mean) {np.mean(np.max(kk.reshape(a.steps, -1), 1)):.1f}")
     if a.parts:
-        names = ["state+spawn", "part 1", "A: plans", "A: moves", "round B", "sequential", "-", "collide+erase"]
+        names = ["state+spawn", "part 1", "A: pairs", "moves (+seq)", "B: pairs", "scan passes #", "scans (A+B)",
+                 "collide+erase"]
         dd = np.concatenate(parts)
         print("NPCs  envs  " + "  ".join(f"{n:>16s}" for n in names))
         for k in range(int(kk.max()) + 1):
