@@ -146,10 +146,13 @@ def test_step_kernel_selection(mev):
     assert h.step_kernel() == 2
     h.close()
     small = _handle(mev, num_envs=64)
-    assert small.step_kernel() == 1  # automatic: finer LiDAR waves for small batches
+    assert small.step_kernel() == 1  # automatic: finer LiDAR waves for small batches (8 agents x 64 beams)
     small.set_step_kernel(2)
     assert small.step_kernel() == 2
     small.close()
+    tiny = mev.Handle(num_envs=1, num_agents=1, lidar_rays=16)
+    assert tiny.step_kernel() == 2  # automatic: one agent's beams fit one LiDAR wave, one launch
+    tiny.close()
     # config 4 shape (1 ego, traffic, 32 NPC slots): fused automatically
     t = mev.Handle(num_envs=4096, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32)
     assert t.step_kernel() == 2
