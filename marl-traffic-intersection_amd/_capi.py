@@ -99,6 +99,7 @@ def load_library(variant: str = None):
     if variant in _libs:
         return _libs[variant]
     path = _build.lib_path(variant)
+    _one_runtime()
     if not _build.up_to_date(variant):
         try:
             _build.build(variant=variant)
@@ -192,14 +193,28 @@ def _ptr(a) -> Optional[int]:
 _torch_first_done = False
 
 
+def _one_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own runtime
+    (torch/lib/libamdhip64.so, SONAME libamdhip64.so.7, loaded by path) next to
+    the /opt/rocm one this library links by that SONAME.  Imported first, torch's
+    copy is already loaded when ours is, and the dynamic linker binds our
+    NEEDED libamdhip64.so.7 / librccl.so.1 to it: a single runtime serves both
+    (tests/test_capi_symbols.py::test_one_hip_runtime_with_torch).  Loaded the
+    other way round, torch would bring its copy in beside ours -- two runtimes in
+    one process -- so torch, when installed, is imported before the library.
+    MEV_TORCH_FIRST=0 skips this for torch-free processes."""
+    if os.environ.get("MEV_TORCH_FIRST", "1") == "0":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _torch_runtime_first():
-    """PyTorch-ROCm ships its own HIP runtime (torch/lib/libamdhip64.so, no
-    soname), distinct from the /opt/rocm libamdhip64.so.7 this library links.
-    Both coexist in one process (same KFD process, one GPU address space, so
-    torch tensors are valid kernel arguments here) only when torch's runtime
-    initialises first; ours initialising first makes torch report "No HIP
-    GPUs".  So before our first HIP call, let torch initialise if it is
-    installed.  Set MEV_TORCH_FIRST=0 for torch-free processes."""
+    """With torch present, let its runtime initialise the device before the
+    library's first HIP call (the same single runtime, see _one_runtime).
+    Set MEV_TORCH_FIRST=0 for torch-free processes."""
     global _torch_first_done
     if _torch_first_done:
         return

@@ -54,3 +54,20 @@ def test_invalid_config_is_rejected(mev):
     h = ctypes.c_void_p()
     assert lib.mev_create(ctypes.byref(c), ctypes.byref(h)) == -1
     assert b"num_agents" in lib.mev_last_error()
+
+
+def test_one_hip_runtime_with_torch():
+    """With PyTorch installed, loading the library leaves ONE HIP runtime in the
+    process: torch's libamdhip64 / librccl (imported first by _capi) satisfy the
+    library's NEEDED libamdhip64.so.7 / librccl.so.1 (checked in a fresh
+    process, from /proc/self/maps; no GPU call)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import pkgload; pkgload.load()._capi.load_library(); "
+            "libs = sorted({l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l or 'librccl' in l}); "
+            "print('\\n'.join(libs))") % ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, check=True).stdout
+    hip = [l for l in out.split() if "libamdhip64" in l]
+    rccl = [l for l in out.split() if "librccl" in l]
+    assert len(hip) == 1, hip
+    assert len(rccl) == 1, rccl
