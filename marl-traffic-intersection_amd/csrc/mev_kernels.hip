@@ -1446,12 +1446,17 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     wave_lds_sync();
 
     STAMP(2);
+    // one ego per env and no NPCs: no car can touch another, and no LiDAR beam can
+    // meet another car (configs 1 and 2) -- the SAT pairs, obstacle table and
+    // candidate masks below are skipped (the masks stay empty)
+    const bool lone = !TRAFFIC && NE == 1;
     // ---- car-car SAT (:292-318): ego pairs (i<j) and ego x NPC, one pair per lane
 #ifndef MEV_EXP_NOSAT  // timing-only: no car-car SAT
-    for (int pbase = 0; pbase < N * N; pbase += WAVE) {
+    for (int pbase = 0; pbase < (lone ? 0 : N * N); pbase += WAVE) {
         const int pi = pbase + tid;
-        if (pi < N * N) {
-            const int a = pi / N, b = pi % N;
+        // (a, b) = (pi / N, pi % N); lane = 8a + b without the integer division when N <= 8
+        const int a = N <= 8 ? (tid >> 3) : pi / N, b = N <= 8 ? (tid & 7) : pi % N;
+        if (N <= 8 ? (a < N && b < N) : pi < N * N) {
             if (a < b && (PK == 1 || a / NE == b / NE) && el.alive[a] && el.alive[b] &&
                 sat_collide(reinterpret_cast<const float*>(&el.cx[a]), reinterpret_cast<const float*>(&el.cy[a]),
                             el.c[a], el.s[a], reinterpret_cast<const float*>(&el.cx[b]),
@@ -1523,7 +1528,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     STAMP(4);
     // ---- LiDAR obstacle table (:374-388): every ego (alive or not), then NPCs,
     // published to HBM for k_lidar together with each agent's candidate mask
-    const int nob = N + ncnt;
+    const int nob = lone ? 0 : N + ncnt;  // lone egos: no obstacle anyone could see
     const int OB = p.ob_stride;
     for (int o = tid; o < nob; o += WAVE) {
         float x, y, h, c, s;
@@ -1542,8 +1547,9 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // beyond max_dist exists, truncation moves a probe < 1 px)
     for (int pbase = 0; pbase < N * nob; pbase += WAVE) {
         const int pi = pbase + tid;
-        if (pi < N * nob) {
-            const int a = pi / nob, o = pi - a * nob;
+        const bool small = N <= 8 && nob <= 8;  // lane = 8a + o, no integer division
+        const int a = small ? (tid >> 3) : pi / nob, o = small ? (tid & 7) : pi - a * nob;
+        if (small ? (a < N && o < nob) : pi < N * nob) {
             const float cx = el.x[a], cy = el.y[a];
             if (o != a && (PK == 1 || a / NE == o / NE) && el.alive[a] &&
                 !(fabs_f(el.px[o] - cx) < 1e-3f && fabs_f(el.py[o] - cy) < 1e-3f && fabs_f(el.ph[o] - el.h[a]) < 1e-3f)) {
