@@ -126,6 +126,18 @@ __device__ inline int32_t* npci(const SimParams& p, int k) {
 }
 __device__ inline unsigned long long ballot(bool p) { return __ballot(p); }
 
+// atan2f for wave code: the branch-free atan2f_bf unless a lane of the wave has a
+// zero / infinite / NaN operand (then fdlibm's atan2f for the wave); bit-identical
+// either way (mev_math.h).  The branchy form runs every range and quadrant the
+// wave's lanes fall into one after another.
+#ifndef MEV_ATAN_BF
+#define MEV_ATAN_BF 1
+#endif
+__device__ inline float atan2f_wave(float y, float x) {
+    if (!MEV_ATAN_BF || ballot(atan2f_special(y, x))) return atan2f(y, x);
+    return atan2f_bf(y, x);
+}
+
 // LDS visibility between the lanes of one wave.  k_cars, k_reset and the NPC
 // phase run as single-wave workgroups and k_lidar's waves are independent, so
 // no s_barrier is needed -- and unlike __syncthreads() this does not wait for
@@ -652,7 +664,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const float h = nl.h[k], v = nl.v[k];
             const float tdx = t.x - x;
             const float tdy = t.y - y;
-            const float heading_err = wrap_angle(atan2f(-tdy, tdx) - h);
+            const float heading_err = wrap_angle(atan2f_wave(-tdy, tdx) - h);
             float steer_cmd = heading_err * 3.0f;
             steer_cmd = (1.0f < steer_cmd) ? 1.0f : steer_cmd;    // std::min(1, .)
             steer_cmd = (steer_cmd < -1.0f) ? -1.0f : steer_cmd;  // std::max(-1, .)
@@ -1733,7 +1745,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             const bool self = js == ii;
             const float dxd = el.tgx[ii] - x, dyd = el.tgy[ii] - y;  // path[min(idx + 10, 159)] (:444-452)
             const float f4 = __builtin_sqrtf(dxd * dxd + dyd * dyd) / float(WIDTH);
-            const float f5 = wrap_angle(atan2f(-dyd, dxd) - h) / PI_F;
+            const float f5 = wrap_angle(atan2f_wave(-dyd, dxd) - h) / PI_F;
             const float f0 = (self ? x : ox - x) / float(WIDTH);
             const float f1 = (self ? y : oy - y) / float(HEIGHT);
             const float f2 = (self ? v : ov - v) / PHYSICS_MAX_SPEED;

@@ -370,6 +370,69 @@ MEV_HD float atan2f(float y, float x) {
     }
 }
 
+// Branch-free forms of atanf / atan2f for wave code: the same operations in the
+// same order as above, with fdlibm's range reduction chosen by selects instead
+// of branches -- in a wave whose lanes fall into different ranges or quadrants
+// the branchy form runs every taken path one after another.  The reduction's
+// four quotients are one (p*|x| - q) / (r + s*|x|):
+//   id 0: (2|x| - 1) / (2 + |x|)   id 1: (|x| - 1) / (1 + |x|)
+//   id 2: (|x| - 1.5) / (1 + 1.5|x|)   id 3: (0|x| - 1) / (0 + |x|) = -1/|x|
+// (1*a and 0 + a are exact, addition commutes: the same roundings as fdlibm's).
+// atan2f_bf is exact for every input atan2f_special() rejects (zero, infinite
+// or NaN operands); tests/native/devmath_check.cpp checks both against glibc.
+MEV_HD float atanf_bf(float x) {
+    const float atanhi[4] = {u2f(0x3eed6338u), u2f(0x3f490fdau), u2f(0x3f7b985eu), u2f(0x3fc90fdau)};
+    const float atanlo[4] = {u2f(0x31ac3769u), u2f(0x33222168u), u2f(0x33140fb4u), u2f(0x33a22168u)};
+    const float aT0 = u2f(0x3eaaaaabu), aT1 = u2f(0xbe4ccccdu), aT2 = u2f(0x3e124925u), aT3 = u2f(0xbde38e38u),
+                aT4 = u2f(0x3dba2e6eu), aT5 = u2f(0xbd9d8795u), aT6 = u2f(0x3d886b35u), aT7 = u2f(0xbd6ef16bu),
+                aT8 = u2f(0x3d4bda59u), aT9 = u2f(0xbd15a221u), aT10 = u2f(0x3c8569d7u);
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    const float ax = fabs_f(x);
+    const bool small = ix < 0x3ee00000;  // id -1: no reduction
+    const int id = ix < 0x3f300000 ? 0 : (ix < 0x3f980000 ? 1 : (ix < 0x401c0000 ? 2 : 3));
+    const float pp = id == 0 ? 2.0f : (id == 3 ? 0.0f : 1.0f);
+    const float qq = id == 2 ? 1.5f : 1.0f;
+    const float rr = id == 0 ? 2.0f : (id == 3 ? 0.0f : 1.0f);
+    const float ss = id == 2 ? 1.5f : 1.0f;
+    const float red = (pp * ax - qq) / (rr + ss * ax);
+    const float xr = small ? x : red;
+    const float z = xr * xr;
+    const float w = z * z;
+    const float s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const float s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    const float hi = id == 0 ? atanhi[0] : (id == 1 ? atanhi[1] : (id == 2 ? atanhi[2] : atanhi[3]));
+    const float lo = id == 0 ? atanlo[0] : (id == 1 ? atanlo[1] : (id == 2 ? atanlo[2] : atanlo[3]));
+    const float r_small = xr - xr * (s1 + s2);
+    const float zz = hi - ((xr * (s1 + s2) - lo) - xr);
+    float r = small ? r_small : (hx < 0 ? -zz : zz);
+    if (ix < 0x31000000) r = x;                                                   // tiny: atan x = x
+    if (ix >= 0x4c000000) r = hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];  // |x| >= 2^25
+    return ix > 0x7f800000 ? x + x : r;
+}
+
+// operands atan2f_bf does not handle (its caller takes atan2f for the wave)
+MEV_HD bool atan2f_special(float y, float x) {
+    const uint32_t ax = f2u(x) & 0x7fffffffu, ay = f2u(y) & 0x7fffffffu;
+    return ax == 0u || ay == 0u || ax >= 0x7f800000u || ay >= 0x7f800000u;
+}
+
+MEV_HD float atan2f_bf(float y, float x) {
+    const float pi = u2f(0x40490fdbu), pi_o_2 = u2f(0x3fc90fdbu), pi_lo = u2f(0xb3bbbd2eu);
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)f2u(y);
+    const int32_t iy = hy & 0x7fffffff;
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    const int32_t k = (iy - ix) >> 23;
+    float z = atanf_bf(fabs_f(y / x));
+    z = (hx < 0 && k < -60) ? 0.0f : z;
+    z = k > 60 ? pi_o_2 + 0.5f * pi_lo : z;
+    const float r2 = pi - (z - pi_lo), r3 = (z - pi_lo) - pi;
+    const float r = m == 0 ? z : (m == 1 ? u2f(f2u(z) ^ 0x80000000u) : (m == 2 ? r2 : r3));
+    return hx == 0x3f800000 ? atanf_bf(y) : r;  // x == 1: fdlibm returns atanf(y)
+}
+
 // ---------------------------------------------------------------- hypotf ---
 MEV_HD float hypotf(float x, float y) {
     // glibc 2.35 e_hypotf.c (finite inputs): one double evaluation, one rounding.

@@ -107,6 +107,45 @@ int main(int argc, char** argv) {
         return same(mev::atanf(x), ::atanf(x)) ? 0 : 1;
     }), 2ull * 0x7f800000ull / stride);
 
+    // the branch-free forms (wave code): atanf_bf over every float, atan2f_bf wherever
+    // atan2f_special does not send the wave to atan2f
+    report("atanf_bf all", sweep_abs(u2f_(0x7fffffffu), stride, [&](float x) -> uint64_t {
+        return same(mev::atanf_bf(x), ::atanf(x)) ? 0 : 1;
+    }), 2ull * 0x7fffffffull / stride);
+    {
+        const uint64_t N = exhaustive ? 2000000000ull : 40000000ull;
+        const int T = std::max(1u, std::thread::hardware_concurrency());
+        std::atomic<uint64_t> bad{0}, cov{0};
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                std::mt19937_64 rng(4321 + t);
+                std::uniform_real_distribution<float> big(-1200.0f, 1200.0f), small(-2.0f, 2.0f);
+                std::uniform_int_distribution<uint32_t> bits;
+                uint64_t b = 0, c = 0;
+                for (uint64_t k = t; k < N; k += T) {
+                    float y, x;
+                    switch (k % 5) {
+                        case 0: y = big(rng); x = big(rng); break;
+                        case 1: y = small(rng); x = small(rng); break;
+                        case 2: y = big(rng); x = small(rng) * 1e-3f; break;
+                        case 3: y = small(rng); x = (k & 8) ? 1.0f : -1.0f; break;
+                        default: y = u2f_(bits(rng)); x = u2f_(bits(rng)); break;
+                    }
+                    if (mev::atan2f_special(y, x)) {
+                        c += (x == 0.0f || y == 0.0f || std::isinf(x) || std::isinf(y) || x != x || y != y) ? 0 : 1;
+                        continue;
+                    }
+                    if (!same(mev::atan2f_bf(y, x), ::atan2f(y, x))) ++b;
+                }
+                bad += b;
+                cov += c;
+            });
+        for (auto& x : th) x.join();
+        report("atan2f_bf random", bad, N);
+        report("atan2f_special only specials", cov, N);
+    }
+
     // atan2f / hypotf: random pairs at simulator scales plus special values
     {
         const uint64_t N = exhaustive ? 2000000000ull : 40000000ull;
