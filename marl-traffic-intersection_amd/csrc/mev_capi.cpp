@@ -51,6 +51,7 @@ struct mev_handle {
     int D = 0, lidar_slots = 0, P = 0, nroutes = 0;
     std::vector<mev::LanePoint> pts;
     std::vector<float> h_paths, h_spawn;
+    std::vector<float> h_pbox;  // [nroutes][3][4] piece bounding boxes (RouteTab::pbox)
     std::vector<int32_t> h_intent;
     std::vector<int32_t> h_traffic;
     hipStream_t own_stream = nullptr;
@@ -66,6 +67,7 @@ struct mev_handle {
     int32_t* d_spawn = nullptr;
     uint8_t* d_mask = nullptr;
     float* d_paths = nullptr;
+    float* d_pbox = nullptr;
     float* d_spawn_tab = nullptr;
     int32_t* d_intent = nullptr;
     float* d_rel = nullptr;
@@ -239,6 +241,21 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
             h->h_spawn[size_t(3 * r + 1)] = h->pts[size_t(s)].y;
             h->h_spawn[size_t(3 * r + 2)] = mev::spawn_heading(path);
         }
+    // each route's pieces [0, 50), [50, 110), [110, 160): bounding boxes of the float points
+    h->h_pbox.resize(size_t(h->nroutes) * 12);
+    for (int r = 0; r < h->nroutes; ++r) {
+        const float* path = &h->h_paths[size_t(r) * 2 * mev::PATH_LEN];
+        const int cut[4] = {0, 50, 110, mev::PATH_LEN};
+        for (int q = 0; q < 3; ++q) {
+            float x0 = path[2 * cut[q]], x1 = x0, y0 = path[2 * cut[q] + 1], y1 = y0;
+            for (int i = cut[q]; i < cut[q + 1]; ++i) {
+                x0 = std::min(x0, path[2 * i]); x1 = std::max(x1, path[2 * i]);
+                y0 = std::min(y0, path[2 * i + 1]); y1 = std::max(y1, path[2 * i + 1]);
+            }
+            float* b = &h->h_pbox[size_t(r) * 12 + size_t(q) * 4];
+            b[0] = x0; b[1] = x1; b[2] = y0; b[3] = y1;
+        }
+    }
     // LiDAR beam offsets, cpp/IntersectionEnv.cpp:119-127 (== Lidar.cpp:4-14)
     std::vector<float> rel(size_t(c.lidar_rays));
     {
@@ -294,7 +311,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&h->internal.step, size_t(E));
     // inputs & tables
     A(&h->d_actions, EN * 2); A(&h->d_spawn, size_t(E)); A(&h->d_mask, size_t(E));
-    A(&h->d_paths, h->h_paths.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
+    A(&h->d_paths, h->h_paths.size()); A(&h->d_pbox, h->h_pbox.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
     A(&h->d_rel, rel.size()); A(&h->d_traffic, size_t(h->P) * size_t(h->P));
     A(&h->d_reset_routes, size_t(h->P) * size_t(h->P));
     A(reinterpret_cast<uint8_t**>(&h->d_sp), sizeof(mev::SimParams));
@@ -309,6 +326,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     // upload tables
     err = hipMemcpyAsync(h->d_paths, h->h_paths.data(), h->h_paths.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_spawn_tab, h->h_spawn.data(), h->h_spawn.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(h->d_pbox, h->h_pbox.data(), h->h_pbox.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_intent, h->h_intent.data(), h->h_intent.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_rel, rel.data(), rel.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess && d_dist) err = hipMemcpyAsync(d_dist, dists.data(), dists.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
@@ -358,6 +376,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     p.rt.path = h->d_paths;
     p.rt.intent = h->d_intent;
     p.rt.spawn = h->d_spawn_tab;
+    p.rt.pbox = reinterpret_cast<const float4*>(h->d_pbox);
     p.rt.nroutes = h->nroutes;
     p.rel_angles = h->d_rel;
     p.traffic_routes = h->d_traffic;

@@ -44,6 +44,10 @@ struct RouteTab {
     const float* path;      // [nroutes][160][2]
     const int32_t* intent;  // [nroutes]
     const float* spawn;     // [nroutes][3]  x, y, heading
+    // [nroutes][3] bounding boxes (min x, max x, min y, max y) of each route's three
+    // pieces -- points [0, 50), [50, 110), [110, 160) (RouteGen.cpp:160-237) -- for
+    // the NPC ghost scan's prefilter
+    const float4* pbox;
     int32_t nroutes;
 };
 

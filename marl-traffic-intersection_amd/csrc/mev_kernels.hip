@@ -133,6 +133,10 @@ __device__ inline unsigned long long ballot(bool p) { return __ballot(p); }
 #ifndef MEV_ATAN_BF
 #define MEV_ATAN_BF 1
 #endif
+// the NPC ghost scans skip others no scanned path point can reach (route piece boxes)
+#ifndef MEV_NPC_PREFILTER
+#define MEV_NPC_PREFILTER 1
+#endif
 __device__ inline float atan2f_wave(float y, float x) {
     if (!MEV_ATAN_BF || ballot(atan2f_special(y, x))) return atan2f(y, x);
     return atan2f_bf(y, x);
@@ -745,10 +749,30 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const float oxj = newj ? nl.xn[jj] : nl.x[jj], oyj = newj ? nl.yn[jj] : nl.y[jj];
             const float ohj = newj ? nl.hn[jj] : nl.h[jj], ovj = newj ? nl.vn[jj] : nl.v[jj];
             const float ocj = newj ? nl.cn[jj] : nl.c[jj], osj = newj ? nl.sn[jj] : nl.s[jj];
+            // k's route pieces (bounding boxes), in flight during the pair tests
+            const float4* PB = p.rt.pbox + (size_t)nl.route[kk] * 3;
+            const float4 pb0 = PB[0], pb1 = PB[1], pb2 = PB[2];
             const NpcPair pr = npc_pair(k, nl.x[kk], nl.y[kk], nl.h[kk], nl.v[kk], nl.c[kk], nl.s[kk], nl.mdc[kk],
                                         jvalid, j, oxj, oyj, ohj, ovj, ocj, osj);
+            // prefilter of the ghost scan: j can only stop k's scan if it lies within
+            // SAFE of one of k's scanned path points path[idx0, idx0 + 120); the points
+            // of each route piece lie in its bounding box, so j farther than SAFE + 0.01
+            // (beyond any float rounding of the squared distance) from every box the
+            // scan window overlaps never hits, and leaves the scan's candidates
+            bool reach = false;
+            if (MEV_NPC_PREFILTER && pr.pok) {
+                const int g0 = nl.pidx0[kk], g1 = g0 + 120 < PATH_LEN ? g0 + 120 : PATH_LEN;
+                const float R2 = (CAR_WIDTH * 2.0f + 0.01f) * (CAR_WIDTH * 2.0f + 0.01f);
+                auto near_box = [&](float4 b) {
+                    const float dx = fmaxf(fmaxf(b.x - oxj, oxj - b.y), 0.0f);
+                    const float dy = fmaxf(fmaxf(b.z - oyj, oyj - b.w), 0.0f);
+                    return dx * dx + dy * dy < R2;
+                };
+                reach = (g0 < 50 && near_box(pb0)) || (g0 < 110 && g1 > 50 && near_box(pb1)) ||
+                        (g1 > 110 && near_box(pb2));
+            }
             const unsigned long long b30 = ballot(pr.f30), b50 = ballot(pr.f50);
-            const unsigned long long bok = ballot(pr.pok), byf = ballot(pr.yfar);
+            const unsigned long long bok = ballot(MEV_NPC_PREFILTER ? reach : pr.pok), byf = ballot(pr.yfar);
             const int sh = kl << lk;
             float acc_thr = nl.accb[kk];
             if ((b30 >> sh) & seg) acc_thr = -1.0f;
