@@ -331,6 +331,7 @@ def main():
 
     # ---- phase 2: the same steps with every step's outputs gathered to rank 0 (RCCL, xGMI)
     gather = None
+    comm_stuck = [False]  # a rank whose RCCL init never returned: exit without tearing the handle down
     if not args.no_gather:
         gather = {}
         try:
@@ -341,8 +342,26 @@ def main():
                 uid = bytes(store.get("mev_comm_id"))
             else:
                 uid = _capi.comm_unique_id()
-            with stdout_to_stderr():
-                env.comm_init(uid, world, rank, root=0, slots=E)
+            # ncclCommInitRank blocks until every rank has joined: bounded here so that a
+            # rank that never joins costs the gather phase, not the bench line
+            import threading
+            init_err = []
+
+            def _init():
+                try:
+                    with stdout_to_stderr():
+                        env.comm_init(uid, world, rank, root=0, slots=E)
+                except Exception as exc:  # reported below
+                    init_err.append(exc)
+
+            th = threading.Thread(target=_init, daemon=True)
+            th.start()
+            th.join(args.gather_timeout)
+            if th.is_alive():
+                comm_stuck[0] = True
+                raise RuntimeError(f"RCCL communicator init did not finish within {args.gather_timeout:.0f} s")
+            if init_err:
+                raise init_err[0]
             env.reset(device=True)
             for t in range(W):
                 env.step(actions[t].data_ptr(), 1.0 / 60.0, auto_reset=True, device=True, gather=True)
@@ -467,6 +486,10 @@ def main():
             except Exception as exc:  # never let the baseline kill the bench line
                 res["cpu_baseline"] = {"error": str(exc)[:200]}
         print(json.dumps(res), flush=True)
+    if comm_stuck[0]:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)  # the init thread is stuck inside RCCL; nothing else to clean up safely
     env.close()
     if dist is not None:
         dist.barrier()
