@@ -314,10 +314,14 @@ class IntersectionEnv:
         s = np.asarray(steerings, np.float32).reshape(-1)[:n]
         act[0, : len(t), 0] = t
         act[0, : len(s), 1] = s
-        out = h.step(act, float(dt))
+        # one output dict per handle (its args struct is reused by Handle.step); the
+        # result's arrays are copies, like the reference's pybind conversions
+        if getattr(self, "_out_h", None) is not h:
+            self._out_h, self._out = h, h.alloc_outputs()
+        out = h.step(act, float(dt), out=self._out)
         self._fresh = False
-        res.obs = out["obs"][0]
-        res.rewards = out["reward"][0]
+        res.obs = out["obs"][0].copy()
+        res.rewards = out["reward"][0].copy()
         res.done = [int(x) for x in out["done"][0]]
         res.status = [STATUS[int(x)] for x in out["status"][0]]
         res.agent_ids = list(self._agent_ids)

@@ -34,6 +34,19 @@ def main():
     dt = (time.perf_counter() - t0) / a.steps
     res["env.py (1 agent, 96 beams)"] = round(1.0 / dt, 1)
     e.close()
+    # config 1's shape through env.py: 16 beams set through the bound Lidar objects,
+    # as the survey's reference measurement did
+    from marl_traffic_intersection_amd import cpp_backend
+    e = envmod.IntersectionEnv({"num_agents": 1, "traffic_flow": False})
+    e.env.lidars = [cpp_backend.Lidar(rays=16)]
+    for t in range(200):
+        e.step(acts[t])
+    t0 = time.perf_counter()
+    for t in range(a.steps):
+        e.step(acts[t])
+    dt = (time.perf_counter() - t0) / a.steps
+    res["env.py (1 agent, 16 beams; reference 54,869 in the survey container)"] = round(1.0 / dt, 1)
+    e.close()
     for kernel in (0, 1, 2):
         hh = mev.Handle(num_envs=1, num_agents=1, lidar_rays=16)
         if kernel:
