@@ -1049,20 +1049,26 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         nl.col[lane] = 0ull;
     }
     wave_lds_sync();
-    for (int pbase = 0; pbase < cnt * cnt; pbase += WAVE) {
-        const int pi = pbase + lane;
-        if (pi < cnt * cnt) {
-            const int a = pi / cnt, b = pi % cnt;
-            if (a < b && sat_collide(nl.cx[a], nl.cy[a], nl.c[a], nl.s[a], nl.cx[b], nl.cy[b], nl.c[b], nl.s[b]))
+    unsigned long long alive_m = ballot(lane < cnt && nl.alive[lane < cnt ? lane : 0]);
+    if (cnt >= 2) {  // (one NPC cannot collide)
+        for (int pbase = 0; pbase < cnt * cnt; pbase += WAVE) {
+            const int pi = pbase + lane;
+            // (a, b) = (pi / cnt, pi % cnt); lane = 8a + b without the integer division when cnt <= 8
+            const int a = cnt <= 8 ? (lane >> 3) : pi / cnt, b = cnt <= 8 ? (lane & 7) : pi % cnt;
+            if ((cnt <= 8 ? (a < cnt && b < cnt) : pi < cnt * cnt) && a < b &&
+                sat_collide(nl.cx[a], nl.cy[a], nl.c[a], nl.s[a], nl.cx[b], nl.cy[b], nl.c[b], nl.s[b]))
                 atomicOr(&nl.col[a], 1ull << b);
         }
-    }
-    wave_lds_sync();
-    unsigned long long alive_m = ballot(lane < cnt && nl.alive[lane]);
-    for (int i = 0; i < cnt; ++i) {
-        if (!((alive_m >> i) & 1ull)) continue;
-        const unsigned long long hits = nl.col[i] & alive_m;  // col[i] holds only j > i
-        if (hits) alive_m &= ~(hits | (1ull << i));
+        wave_lds_sync();
+        // greedy in (i, j) order on the masks, lane i holding col[i] (only j > i)
+        const unsigned long long colv = lane < cnt ? nl.col[lane] : 0ull;
+        if (ballot(colv != 0ull)) {
+            for (int i = 0; i < cnt; ++i) {
+                if (!((alive_m >> i) & 1ull)) continue;
+                const unsigned long long hits = readlane64(colv, i) & alive_m;
+                if (hits) alive_m &= ~(hits | (1ull << i));
+            }
+        }
     }
     // -- erase dead / arrived / out-of-screen, order preserving (:359-366)
     bool keep = false;
