@@ -63,6 +63,8 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # exact variant: fdlibm's branchy atan2f in the observation head and NPC steering
                "noatanbf": ["-DMEV_ATAN_BF=0"],
                "noprefilter": ["-DMEV_NPC_PREFILTER=0"],
+               # fused traffic: the rest of the step at a level by the env's NPC count (product: 3)
+               "trafprio0": ["-DMEV_TRAFFIC_PRIO=0"], "trafprio2": ["-DMEV_TRAFFIC_PRIO=2"],
                "npcprio1": ["-DMEV_NPC_PRIO=1"], "npcprio3": ["-DMEV_NPC_PRIO=3"],
                "npcprio0": ["-DMEV_NPC_PRIO=0"],
                # timing-only (wrong results): NPC controller without ghost scans / without round B

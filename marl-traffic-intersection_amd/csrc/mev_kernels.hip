@@ -1346,7 +1346,17 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     STAMP(0);
     int ncnt = 0;
     if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg);
-    if (TRAFFIC && MEV_NPC_PRIO) __builtin_amdgcn_s_setprio(FUSED ? MEV_PRIO_CARS : 0);
+#ifndef MEV_TRAFFIC_PRIO  // fused traffic: the rest of the step at a level by the env's NPC count (0: MEV_PRIO_CARS; 3: +1.4 % at config 4)
+#define MEV_TRAFFIC_PRIO 3
+#endif
+    if (TRAFFIC && FUSED && MEV_TRAFFIC_PRIO) {
+        // the envs with many NPCs set the kernel's end: the rest of their step goes first
+        if (ncnt >= 2 * MEV_TRAFFIC_PRIO) __builtin_amdgcn_s_setprio(3);
+        else if (ncnt >= MEV_TRAFFIC_PRIO) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
+    } else if (TRAFFIC && MEV_NPC_PRIO) {
+        __builtin_amdgcn_s_setprio(FUSED ? MEV_PRIO_CARS : 0);
+    }
     STAMP(1);
 
     // ---- phase 1: kinematics (:151-163), path index, base reward (:15-46),
