@@ -73,7 +73,9 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "stop1": ["-DMEV_EXP_STOP=1"], "stop2": ["-DMEV_EXP_STOP=2"], "stop3": ["-DMEV_EXP_STOP=3"],
                "stop4": ["-DMEV_EXP_STOP=4"], "stop0": ["-DMEV_EXP_STOP=0"],
                # timing-only: k_step without the observation head / the car-car SAT
-               "nohead": ["-DMEV_EXP_NOHEAD"], "nosat": ["-DMEV_EXP_NOSAT"],
+               "nohead": ["-DMEV_EXP_NOHEAD"], "nosat": ["-DMEV_EXP_NOSAT"], "nowb": ["-DMEV_EXP_NOWB"],
+               # exact variant: k_step's ego state write-back at its end (product: in cars_post)
+               "wblate": ["-DMEV_WB_LATE=1"],
                # exact variants: k_step's cars_post after the LiDAR (product: before it), at the LiDAR's last
                # issue priority or a fixed one
                "postlate": ["-DMEV_POST_AFTER_LIDAR=1"],

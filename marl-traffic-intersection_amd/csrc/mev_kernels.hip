@@ -1255,6 +1255,29 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
 #define MEV_FUSED_STAGED 0
 #endif
 
+// k_step writes the final ego state back at its end, after the LiDAR (1), or in
+// cars_post before it (0)
+#ifndef MEV_WB_LATE
+#define MEV_WB_LATE 0
+#endif
+
+// the final ego state of the wave's N agent slots back to HBM (lane = slot; agent
+// slot i is global agent e * NE + i); spawn poses, intent, alive and route only
+// for envs reset this step (do_reset: the lane's env)
+__device__ __forceinline__ void ego_writeback(const SimParams& p, int e, int NE, int N, const CarsLDS& el,
+                                              bool do_reset, int tid) {
+    for (int i = tid; i < N; i += WAVE) {
+        const int g = e * NE + i;
+        egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
+        egof(p, EF_ACC)[g] = el.acc[i]; egof(p, EF_STEER)[g] = el.steer[i]; egoi(p, EF_PIDX)[g] = el.pidx[i];
+        egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
+        if (do_reset) {
+            egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
+            egoi(p, EF_INTENT)[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
+        }
+    }
+}
+
 // What the two halves of the car part share (cars_pre -> cars_post).
 struct CarsCtx {
     int step_no;    // step counter after this step
@@ -1717,17 +1740,12 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
     }
     // ---- the final ego state back to HBM (lane = agent); k_step's staged variant
     // writes it at its end (fused_store)
-    if (!STAGE) {
-        for (int i = tid; i < N; i += WAVE) {
-            const int g = e * NE + i;
-            egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
-            egof(p, EF_ACC)[g] = el.acc[i]; egof(p, EF_STEER)[g] = el.steer[i]; egoi(p, EF_PIDX)[g] = el.pidx[i];
-            egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
-            if (do_reset) {
-                egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
-                egoi(p, EF_INTENT)[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
-            }
-        }
+#ifdef MEV_EXP_NOWB  // timing-only: no state write-back
+    if (false) {
+#else
+    if (!STAGE && !(FUSED && MEV_WB_LATE)) {
+#endif
+        ego_writeback(p, e, NE, N, el, do_reset, tid);
     }
     STAMPY(4);
     if (FUSED && MEV_PRIO_HEAD >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_HEAD < 0 ? 0 : MEV_PRIO_HEAD);
@@ -2679,6 +2697,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
         if (MEV_PRIO_POST >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_POST);
         cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
     }
+    if (MEV_WB_LATE && !MEV_FUSED_STAGED) ego_writeback(p, e, p.N, NS, el, cx.do_reset, lane);
     if (MEV_FUSED_STAGED) {
         wave_lds_sync();
         fused_store<TAB>(p, out, e, el, reinterpret_cast<const int*>(lbase + lay.res), lane);

@@ -136,7 +136,12 @@ int main(int argc, char** argv) {
                         c += (x == 0.0f || y == 0.0f || std::isinf(x) || std::isinf(y) || x != x || y != y) ? 0 : 1;
                         continue;
                     }
-                    if (!same(mev::atan2f_bf(y, x), ::atan2f(y, x))) ++b;
+                    if (!same(mev::atan2f_bf(y, x), ::atan2f(y, x))) {
+                        if (b < 4)
+                            std::printf("  atan2f_bf(%a, %a) = %a, glibc %a\n", y, x, mev::atan2f_bf(y, x),
+                                        ::atan2f(y, x));
+                        ++b;
+                    }
                 }
                 bad += b;
                 cov += c;

@@ -42,6 +42,7 @@ def main():
         if t < a.steps // 2:
             continue
         r = h.debug_stamps().astype(np.uint64).reshape(a.envs, 8)
+        r = r[r[:, 0] != 0]  # packed waves stamp only their first env's slots
         t_in = (r[:, 0] & M40).astype(np.int64)
         t_out = (r[:, 7] & M40).astype(np.int64)
         where = (r[:, 7] >> np.uint64(40)).astype(np.int64)
