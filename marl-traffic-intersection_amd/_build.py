@@ -76,6 +76,14 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "nohead": ["-DMEV_EXP_NOHEAD"], "nosat": ["-DMEV_EXP_NOSAT"], "nowb": ["-DMEV_EXP_NOWB"],
                # exact variant: k_step's ego state write-back at its end (product: in cars_post)
                "wblate": ["-DMEV_WB_LATE=1"],
+               # the road march's tail (queue empty) with more probes per step
+               # (product: 6; 2 = off)
+               "nprt2": ["-DMEV_LIDAR_NPR_TAIL=2"], "nprt4": ["-DMEV_LIDAR_NPR_TAIL=4"],
+               "nprt8": ["-DMEV_LIDAR_NPR_TAIL=8"],
+               # phase 1's first probes (product: 2)
+               "npr1_1": ["-DMEV_LIDAR_NPR1=1"], "npr1_3": ["-DMEV_LIDAR_NPR1=3"],
+               # the road march's steps with 3 probes before the tail (product: 2)
+               "npr3": ["-DMEV_LIDAR_NPR=3"],
                # exact variants: k_step's cars_post after the LiDAR (product: before it), at the LiDAR's last
                # issue priority or a fixed one
                "postlate": ["-DMEV_POST_AFTER_LIDAR=1"],

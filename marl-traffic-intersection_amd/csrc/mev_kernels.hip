@@ -1971,6 +1971,18 @@ __device__ inline int lane_rank(unsigned long long mask) {
 #define MEV_LIDAR_NPR 2
 #endif
 constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
+// probes per march step once the queue is empty (the tail: the few longest beams
+// still running, lanes mostly idle): more probes per step, fewer steps.  k_step
+// without traffic: 6 (config 3 39.4 -> 38.0 us, config 2 19.4 -> 18.1 us; 4, 8, 12,
+// 16 measured slower); with traffic and in k_lidar the plain LIDAR_NPR (config 4: 6
+// measured 1.6 % slower)
+#ifndef MEV_LIDAR_NPR_TAIL
+#define MEV_LIDAR_NPR_TAIL 6
+#endif
+// probes phase 1 tests after a beam's safe stretch from the car centre
+#ifndef MEV_LIDAR_NPR1
+#define MEV_LIDAR_NPR1 MEV_LIDAR_NPR
+#endif
 
 struct LidarLayout {
     int ag, dir, res, seg_jo, seg_rg, seg_bx, queue, scr, bytes;
@@ -2051,7 +2063,7 @@ struct LidarSrcLds {
 // longest beam of its agent is done (lockstep cost = max over the agent's
 // beams, pooled cost ~ their mean); phase 3 resolves the cars as packed
 // (agent, box, beam) pairs and writes the observation's LiDAR block.
-template <bool TAB, int ILP, class Src>
+template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR>
 __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& out, const Src& src, const int G,
                                            const int a0, const int na, const int lane, unsigned char* base,
                                            const LidarLayout& lay) {
@@ -2112,14 +2124,17 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     };
     // probes k_ .. k_ + NPR - 1 in march order: the first stop wins; (fx, fy) is
     // the last probe's point
-    auto probes = [&](float cx_, float cy_, float dx_, float dy_, int k_, float& fx, float& fy) -> int {
+    auto probes_n = [&](auto np, float cx_, float cy_, float dx_, float dy_, int k_, float& fx, float& fy) -> int {
         int r = -1;
 #pragma unroll
-        for (int t = 0; t < LIDAR_NPR; ++t) {
+        for (int t = 0; t < decltype(np)::value; ++t) {
             const int c = probe(cx_, cy_, dx_, dy_, k_ + t, fx, fy);
             r = r >= 0 ? r : c;
         }
         return r;
+    };
+    auto probes = [&](float cx_, float cy_, float dx_, float dy_, int k_, float& fx, float& fy) -> int {
+        return probes_n(std::integral_constant<int, LIDAR_NPR>{}, cx_, cy_, dx_, dy_, k_, fx, fy);
     };
 
     // directions; then the first probes of each beam: probe 0 is only
@@ -2152,8 +2167,8 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         // probes 1 .. j lie within j*step <= safe of the centre (car centre on screen)
         const int k1 = pmax < (unsigned)WIDTH ? 1 + ((safe >= stp) ? (int)(safe * inv_stp) : 0) : 0;
         float fx, fy;
-        const int r = probes(a.x, a.y, dx, dy, k1, fx, fy);
-        return r >= 0 ? r : -(k1 + LIDAR_NPR) - 1;
+        const int r = probes_n(std::integral_constant<int, MEV_LIDAR_NPR1>{}, a.x, a.y, dx, dy, k1, fx, fy);
+        return r >= 0 ? r : -(k1 + MEV_LIDAR_NPR1) - 1;
 #endif
     };
     // ILP = 2: two agents per pass, two independent dependency chains (sincosf's
@@ -2237,10 +2252,16 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         // branch-free body: every lane evaluates its probes; idle lanes only skip the store
         const bool act = slot >= 0;
         float fx, fy;
-        const int r = probes(cx, cy, dx, dy, k, fx, fy);
+        int r, npr = LIDAR_NPR;
+        if (NPT != LIDAR_NPR && next >= qn) {  // wave-uniform: the queue is empty
+            r = probes_n(std::integral_constant<int, NPT>{}, cx, cy, dx, dy, k, fx, fy);
+            npr = NPT;
+        } else {
+            r = probes(cx, cy, dx, dy, k, fx, fy);
+        }
         const float safe = road_safe(fx, fy, dx, dy, idx, idy, iadx, iady, rwm, ccen, crf);
-        // probes kl+1 .. kl+j lie within j*step <= safe of the last probe kl = k + NPR - 1
-        const int kn = k + LIDAR_NPR + ((safe >= stp) ? (int)(safe * inv_stp) : 0);
+        // probes kl+1 .. kl+j lie within j*step <= safe of the last probe kl = k + npr - 1
+        const int kn = k + npr + ((safe >= stp) ? (int)(safe * inv_stp) : 0);
         const bool fin = act & ((r >= 0) | (kn >= S));
         if (fin) res[slot] = r >= 0 ? r : (S << 1);
         k = kn;
@@ -2691,7 +2712,8 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
         if (j0 > 0) wave_lds_sync();
         if (j0 > 0 || MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);  // each pool
         const int na = NS - j0 < G ? NS - j0 : G;
-        lidar_body<TAB, MEV_PHASE1_ILP>(p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
+        lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, TRAFFIC ? LIDAR_NPR : MEV_LIDAR_NPR_TAIL>(
+            p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
     }
     if (MEV_POST_AFTER_LIDAR) {  // experiment (variant postlate): measured slower, 41.6 -> 44.1 us
         if (MEV_PRIO_POST >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_POST);

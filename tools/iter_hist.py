@@ -17,14 +17,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--step-kernel", type=int, default=2)
     ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--rays", type=int, default=64)
+    ap.add_argument("--pack", type=int, default=0)
     a = ap.parse_args()
     mev = pkgload.load()
     mev._capi.VARIANT = "exp_iters"
-    h = mev.Handle(num_envs=a.envs, num_agents=8, lidar_rays=64, use_team_reward=1)
+    h = mev.Handle(num_envs=a.envs, num_agents=a.agents, lidar_rays=a.rays, use_team_reward=1)
     h.set_step_kernel(a.step_kernel)
+    h.set_step_pack(a.pack)
     rng = np.random.default_rng(0)
     for t in range(300):
-        h.step(rng.uniform(-1, 1, (a.envs, 8, 2)).astype(np.float32), auto_reset=True)
+        h.step(rng.uniform(-1, 1, (a.envs, a.agents, 2)).astype(np.float32), auto_reset=True)
     d = h.debug_stamps().reshape(a.envs, 8).astype(np.int64)
     it, qn, dry, busy = d[:, 0], d[:, 1], d[:, 2], d[:, 3]
     ok = it > 0
