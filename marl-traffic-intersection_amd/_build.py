@@ -53,6 +53,7 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                           "-DMEV_PRIO_P3=-1"],
                "prio3210": ["-DMEV_PRIO_CARS=3", "-DMEV_PRIO_LIDAR=2", "-DMEV_PRIO_P1B=-1"],
                "prio_half": ["-DMEV_PRIO_P1B_AT=2"],
+               "p2prio0": ["-DMEV_PRIO_P2=0"], "p2prio2": ["-DMEV_PRIO_P2=2"], "p3prio1": ["-DMEV_PRIO_P3=1"],
                "priohbm0": ["-DMEV_PRIO_HBM=0"],  # k_lidar without the LiDAR phases' priorities
                # the compiler's default machine scheduler instead of SCHED (k_step 41.6 -> 41.9 us)
                "sch_default": [],
@@ -76,10 +77,10 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "nohead": ["-DMEV_EXP_NOHEAD"], "nosat": ["-DMEV_EXP_NOSAT"], "nowb": ["-DMEV_EXP_NOWB"],
                # exact variant: k_step's ego state write-back at its end (product: in cars_post)
                "wblate": ["-DMEV_WB_LATE=1"],
-               # the road march's tail (queue empty) with more probes per step
-               # (product: 6; 2 = off)
-               "nprt2": ["-DMEV_LIDAR_NPR_TAIL=2"], "nprt4": ["-DMEV_LIDAR_NPR_TAIL=4"],
-               "nprt8": ["-DMEV_LIDAR_NPR_TAIL=8"],
+               # the road march's tail (product: helper groups from 16 beams, 3 probes per lane)
+               "nohelp": ["-DMEV_MARCH_HELP=0"], "nprt6": ["-DMEV_MARCH_HELP=0", "-DMEV_LIDAR_NPR_TAIL=6"],
+               "h8_3": ["-DMEV_MARCH_HELP=8"], "h32_3": ["-DMEV_MARCH_HELP=32"],
+               "h16_2": ["-DMEV_NPT_HELP=2"], "h16_4": ["-DMEV_NPT_HELP=4"],
                # phase 1's first probes (product: 2)
                "npr1_1": ["-DMEV_LIDAR_NPR1=1"], "npr1_3": ["-DMEV_LIDAR_NPR1=3"],
                # the road march's steps with 3 probes before the tail (product: 2)

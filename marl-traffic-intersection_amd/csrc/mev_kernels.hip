@@ -1971,14 +1971,23 @@ __device__ inline int lane_rank(unsigned long long mask) {
 #define MEV_LIDAR_NPR 2
 #endif
 constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
-// probes per march step once the queue is empty (the tail: the few longest beams
-// still running, lanes mostly idle): more probes per step, fewer steps.  k_step
-// without traffic: 6 (config 3 39.4 -> 38.0 us, config 2 19.4 -> 18.1 us; 4, 8, 12,
-// 16 measured slower); with traffic and in k_lidar the plain LIDAR_NPR (config 4: 6
-// measured 1.6 % slower)
+// The march's tail (the queue empty, the few longest beams still running, lanes
+// mostly idle).  k_step without traffic: once at most MEV_MARCH_HELP beams run, each
+// gets a group of 2-8 lanes that test MEV_NPT_HELP consecutive probes each per step
+// (config 3 39.4 -> 35.6 us, config 2 19.4 -> 15.6 us).  Measured around it: a plain
+// tail with more probes per lane and step (MEV_LIDAR_NPR_TAIL 6: 38.0 / 18.1 us),
+// groups from 8 or 32 beams, 2 or 4 probes per helper lane.  With traffic and in
+// k_lidar the plain march (config 4: the 6-probe tail measured 1.6 % slower).
 #ifndef MEV_LIDAR_NPR_TAIL
-#define MEV_LIDAR_NPR_TAIL 6
+#define MEV_LIDAR_NPR_TAIL MEV_LIDAR_NPR
 #endif
+#ifndef MEV_MARCH_HELP
+#define MEV_MARCH_HELP 16
+#endif
+#ifndef MEV_NPT_HELP
+#define MEV_NPT_HELP 3
+#endif
+static_assert(MEV_MARCH_HELP <= 32, "helper groups have at least 2 lanes");
 // probes phase 1 tests after a beam's safe stretch from the car centre
 #ifndef MEV_LIDAR_NPR1
 #define MEV_LIDAR_NPR1 MEV_LIDAR_NPR
@@ -2063,7 +2072,7 @@ struct LidarSrcLds {
 // longest beam of its agent is done (lockstep cost = max over the agent's
 // beams, pooled cost ~ their mean); phase 3 resolves the cars as packed
 // (agent, box, beam) pairs and writes the observation's LiDAR block.
-template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR>
+template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR, bool HELP = false>
 __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& out, const Src& src, const int G,
                                            const int a0, const int na, const int lane, unsigned char* base,
                                            const LidarLayout& lay) {
@@ -2241,10 +2250,17 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         k = res[qq];
     };
     if (slot >= 0) load_beam(slot);
+    int* hscr = reinterpret_cast<int*>(base + lay.scr);  // phase 3's scratch, free until then
 #ifdef MEV_ITERS
     int iters = 0, drained = -1, lanes_busy = 0;
 #endif
+    bool help = false;
     while (ballot(slot >= 0) != 0ull) {
+        // the tail down to <= 16 beams: continue with 4 lanes per beam (below)
+        if (HELP && MEV_MARCH_HELP && next >= qn && __popcll(ballot(slot >= 0)) <= MEV_MARCH_HELP) {
+            help = true;
+            break;
+        }
 #ifdef MEV_ITERS
         lanes_busy += __popcll(ballot(slot >= 0));
         if (drained < 0 && next >= qn) drained = iters;
@@ -2277,6 +2293,62 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             }
             next += __popcll(fm);
         }
+    }
+    if (HELP && MEV_MARCH_HELP && help) {
+        // The last running beams (<= MEV_MARCH_HELP), GS lanes each (GS = 64 / the
+        // beams rounded up to a power of two, 2..8): lane j of a beam's group tests
+        // probes k + j*NPH .. k + (j+1)*NPH - 1, the earliest stop of the group wins
+        // (results are ordered by k: DPP min), and the group jumps from its last lane's
+        // last probe (DPP broadcast) -- the same probes and jumps, in march order.
+        constexpr int NPH = MEV_NPT_HELP > 0 ? MEV_NPT_HELP : NPT;
+        const unsigned long long am = ballot(slot >= 0);
+        const int nb = __popcll(am);
+        if (slot >= 0) {
+            const int rk = lane_rank(am);
+            hscr[2 * rk] = slot;
+            hscr[2 * rk + 1] = k;
+        }
+        wave_lds_sync();
+        auto group_march = [&](auto gs_c) {
+            constexpr int GS = decltype(gs_c)::value;
+            const int gi = lane / GS, j = lane & (GS - 1);
+            slot = gi < nb ? hscr[2 * gi] : -1;
+            const int k_h = gi < nb ? hscr[2 * gi + 1] : 0;
+            if (slot >= 0) load_beam(slot);
+            k = k_h;
+            while (ballot(slot >= 0) != 0ull) {
+#ifdef MEV_ITERS
+                lanes_busy += __popcll(ballot(slot >= 0));
+                ++iters;
+#endif
+                float fx, fy;
+                const int k0 = k + j * NPH;
+                int r = probes_n(std::integral_constant<int, NPH>{}, cx, cy, dx, dy, k0, fx, fy);
+                r = r >= 0 ? r : 0x7fffffff;
+                const float safe = road_safe(fx, fy, dx, dy, idx, idy, iadx, iady, rwm, ccen, crf);
+                int kn = k0 + NPH + ((safe >= stp) ? (int)(safe * inv_stp) : 0);
+                r = min(r, __builtin_amdgcn_mov_dpp(r, 0xB1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
+                if constexpr (GS == 2) {
+                    kn = __builtin_amdgcn_mov_dpp(kn, 0xF5, 0xf, 0xf, false);  // quad_perm [1,1,3,3]
+                } else {
+                    r = min(r, __builtin_amdgcn_mov_dpp(r, 0x4E, 0xf, 0xf, false));  // quad_perm [2,3,0,1]
+                    kn = __builtin_amdgcn_mov_dpp(kn, 0xFF, 0xf, 0xf, false);        // quad_perm [3,3,3,3]
+                    if constexpr (GS == 8) {
+                        // the other quad's minimum and lane 7's jump by the half-row mirror
+                        r = min(r, __builtin_amdgcn_mov_dpp(r, 0x141, 0xf, 0xf, false));
+                        const int km = __builtin_amdgcn_mov_dpp(kn, 0x141, 0xf, 0xf, false);
+                        kn = j < 4 ? km : kn;
+                    }
+                }
+                const bool fin = slot >= 0 && (r != 0x7fffffff || kn >= S);
+                if (fin && j == 0) res[slot] = r != 0x7fffffff ? r : (S << 1);
+                slot = fin ? -1 : slot;
+                k = kn;
+            }
+        };
+        if (nb <= 8) group_march(std::integral_constant<int, 8>{});
+        else if (nb <= 16) group_march(std::integral_constant<int, 4>{});
+        else group_march(std::integral_constant<int, 2>{});
     }
 #ifdef MEV_ITERS  // per pool: iterations, queued beams, iteration at which the queue ran dry, busy lane-iterations
     if (lane == 0 && a0 / G < p.E) {
@@ -2712,7 +2784,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
         if (j0 > 0) wave_lds_sync();
         if (j0 > 0 || MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);  // each pool
         const int na = NS - j0 < G ? NS - j0 : G;
-        lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, TRAFFIC ? LIDAR_NPR : MEV_LIDAR_NPR_TAIL>(
+        lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, TRAFFIC ? LIDAR_NPR : MEV_LIDAR_NPR_TAIL, !TRAFFIC>(
             p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
     }
     if (MEV_POST_AFTER_LIDAR) {  // experiment (variant postlate): measured slower, 41.6 -> 44.1 us
