@@ -1187,6 +1187,12 @@ __device__ void write_obs_head(const SimParams& p, int i, const EL& el, const NL
 }
 
 // ------------------------------------------------------------- the step ---
+// the car part's per-agent physics without divergent branches: the kinematics, the
+// reward terms and the corner tests are evaluated by every lane and selected
+#ifndef MEV_BF_PHYS
+#define MEV_BF_PHYS 1
+#endif
+
 // Dynamic LDS of k_cars, carved for the handle's N egos and K NPC slots.
 struct CarsLDS {
     float *x, *y, *v, *h, *c, *s, *acc, *steer, *prev_dist, *pa0, *pa1;
@@ -1405,8 +1411,19 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         Kin k{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
         const bool alive = act && el.alive[ii] != 0;
         float cH, sH;
+#if MEV_BF_PHYS
+        {
+            // every lane runs the update; a dead agent keeps its state (one sincosf)
+            Kin ku = k;
+            car_update_heading(ku, el.a0[ii], el.a1[ii], in.dt);
+            sincosf(alive ? ku.h : k.h, &sH, &cH);
+            car_update_move(ku, cH, sH);
+            if (alive) k = ku;
+        }
+#else
         if (alive) car_update(k, el.a0[ii], el.a1[ii], in.dt, &cH, &sH);
         else sincosf(k.h, &sH, &cH);
+#endif
         STAMPX(1);
         // Car::update_path_index (Car.cpp:47-74): first minimum over the window, in order
         float bd = __builtin_inff();
@@ -1449,7 +1466,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         bool succ = false;
         float ccx[4], ccy[4];
         car_corners(k.x, k.y, cH, sH, ccx, ccy);
-        if (alive) {
+        if (MEV_BF_PHYS || alive) {
             // compute_progress / compute_stuck / compute_smooth (:15-46)
             cur = hypotf(k.x - pend.x, k.y - pend.y);
             const float prev = el.prev_dist[ii];
@@ -1469,14 +1486,37 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             rew = r_prog + r_stuck + r_smooth;
             // SUCCESS by the last path segment's axis
             const float dxr = pend.x - pprev.x, dyr = pend.y - pprev.y;
-            if (fabs_f(dxr) > fabs_f(dyr)) succ = fabs_f(k.y - pend.y) < 15.0f && fabs_f(k.x - pend.x) < 40.0f;
-            else succ = fabs_f(k.x - pend.x) < 15.0f && fabs_f(k.y - pend.y) < 40.0f;
+            const bool sx_ = fabs_f(k.y - pend.y) < 15.0f && fabs_f(k.x - pend.x) < 40.0f;
+            const bool sy_ = fabs_f(k.x - pend.x) < 15.0f && fabs_f(k.y - pend.y) < 40.0f;
+            succ = fabs_f(dxr) > fabs_f(dyr) ? sx_ : sy_;
+            if (MEV_BF_PHYS && !alive) { rew = 0.0f; cur = 0.0f; an = 0.0f; sn = 0.0f; succ = false; }
         }
         STAMPX(3);
         // corner tests, one per lane: sub 0-3 corner q (screen margin, road, yellow line,
         // line mask), sub 4-7 edge midpoint q (line mask)
         bool oos_q = false, off_q = false, line_q = false;
+#if MEV_BF_PHYS
+        {
+            // lane sub < 4: corner q (screen margin, road, yellow line, line mask);
+            // sub >= 4: the midpoint of edge (q, q + 1) (line mask only)
+            const int q = sub & 3;
+            float qx = ccx[0], qy = ccy[0], rx = ccx[1], ry = ccy[1];
+#pragma unroll
+            for (int u = 1; u < 4; ++u) {
+                if (q == u) { qx = ccx[u]; qy = ccy[u]; rx = ccx[(u + 1) & 3]; ry = ccy[(u + 1) & 3]; }
+            }
+            const bool corner = sub < 4;
+            const float px_ = corner ? qx : 0.5f * (qx + rx), py_ = corner ? qy : 0.5f * (qy + ry);
+            const float M = 100.0f;
+            const bool lm = is_line_px((int)px_, (int)py_, p.line_stop);
+            oos_q = alive && corner && (qx < -M || qx > float(WIDTH) + M || qy < -M || qy > float(HEIGHT) + M);
+            off_q = alive && corner && !is_on_road(qx, qy, p.rw);
+            line_q = alive && ((corner && hits_yellow_line(qx, qy, p.rw)) || lm);
+        }
+        if (false) {
+#else
         if (alive) {
+#endif
             const int q = sub & 3;
             float qx = ccx[0], qy = ccy[0], rx = ccx[1], ry = ccy[1];
 #pragma unroll

@@ -169,6 +169,31 @@ MEV_HD void car_update(Kin& k, float throttle, float steer_input, float dt, floa
     *sinH = s;
 }
 
+// Car::update up to its new heading (steering, speed, heading, wrapped): the
+// caller takes sincosf of the heading and moves the position with
+// car_update_move -- car_update's operations in its order, split so that a
+// wave whose agents are partly dead (heading unchanged) runs one sincosf.
+MEV_HD void car_update_heading(Kin& k, float throttle, float steer_input, float dt) {
+    k.acc = throttle * MAX_ACC;
+    const float target_steering = steer_input * MAX_STEERING_ANGLE;
+    k.steer += (target_steering - k.steer) * 0.2f;
+    if (throttle == 0.0f) k.v *= 0.95f;
+    k.v += k.acc * dt;
+    if (k.v < 0.0f) k.v = 0.0f;
+    if (k.v > PHYSICS_MAX_SPEED) k.v = PHYSICS_MAX_SPEED;
+    if (fabs_f(k.v) > 0.1f) {
+        const float ang_vel = (k.v / WHEELBASE) * tanf(k.steer);
+        k.h += ang_vel;
+    }
+    k.h = fmodf(k.h + PI_F, 2.0f * PI_F);
+    if (k.h < 0) k.h += 2.0f * PI_F;
+    k.h -= PI_F;
+}
+MEV_HD void car_update_move(Kin& k, float c, float s) {
+    k.x += k.v * c;
+    k.y -= k.v * s;
+}
+
 // Car::update split for the NPC controller, whose steering input is known
 // before its throttle: car_steer is the steering part (its new angle), and
 // car_update_steered the rest given that angle and its tangent -- the same
