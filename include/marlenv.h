@@ -237,6 +237,14 @@ int mev_get_step_kernel(const mev_handle* h, int32_t* kernel);
  * nothing in the reference (one env per IntersectionEnv object). */
 int mev_set_step_pack(mev_handle* h, int32_t envs_per_wave);
 int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave);
+/* Scheduling (results are identical either way): two waves per fused k_step
+ * workgroup -- the car part, then the LiDAR in one wave beside the rest of the
+ * car part (rewards, flags, observation head) in the other.  0 = automatic (on
+ * when the batch needs <= 2048 workgroups, i.e. <= 4 waves per SIMD, no traffic),
+ * 1 = off, 2 = on (no traffic).  mev_get_step_split returns 1 when the next step
+ * uses it.  Replaces nothing in the reference. */
+int mev_set_step_split(mev_handle* h, int32_t mode);
+int mev_get_step_split(const mev_handle* h, int32_t* split);
 
 /* ---- Multi-GPU: the per-step RCCL gather of the stacked outputs ----------
  * envs are sharded over the GPUs of a node, one process and

@@ -39,6 +39,7 @@ EXPORTED = (
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
     "mev_kernel_timing", "mev_kernel_times", "mev_set_reset_routes", "mev_snapshot_size", "mev_snapshot",
     "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel", "mev_set_step_pack", "mev_get_step_pack",
+    "mev_set_step_split", "mev_get_step_split",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
     "mev_gather_wait", "mev_output_dlpack",
 )
@@ -146,6 +147,8 @@ def load_library(variant: str = None):
     L.mev_get_step_kernel.argtypes = [_vp, i32p]
     L.mev_set_step_pack.argtypes = [_vp, ctypes.c_int32]
     L.mev_get_step_pack.argtypes = [_vp, i32p]
+    L.mev_set_step_split.argtypes = [_vp, ctypes.c_int32]
+    L.mev_get_step_split.argtypes = [_vp, i32p]
     L.mev_configure.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.mev_configure_traffic.argtypes = [_vp, ctypes.c_int32, ctypes.c_float]
     L.mev_set_reward.argtypes = [_vp, f32p]
@@ -510,6 +513,16 @@ class Handle:
         v = ctypes.c_int32()
         _check(self._lib.mev_get_step_pack(self._h, ctypes.byref(v)))
         return v.value
+
+    def set_step_split(self, mode: int = 0):
+        """Two waves per fused workgroup: 0 automatic, 1 off, 2 on (scheduling only; results identical)."""
+        _check(self._lib.mev_set_step_split(self._h, int(mode)))
+
+    def step_split(self) -> bool:
+        """Whether the next step runs two waves per fused workgroup."""
+        v = ctypes.c_int32()
+        _check(self._lib.mev_get_step_split(self._h, ctypes.byref(v)))
+        return bool(v.value)
 
     def set_reset_routes(self, routes):
         """Draw every agent's route from `routes` at each reset (empty: fixed routes)."""

@@ -927,6 +927,21 @@ int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave) {
     return MEV_OK;
 }
 
+int mev_set_step_split(mev_handle* h, int32_t mode) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (mode < 0 || mode > 2) return fail(MEV_E_INVALID, "split mode must be 0 (auto), 1 (off) or 2 (on)");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->sp.step_split = mode;
+    return MEV_OK;
+}
+
+int mev_get_step_split(const mev_handle* h, int32_t* split) {
+    if (!h || !split) return fail(MEV_E_INVALID, "null argument");
+    *split = mev::step_kernel_for(h->sp) == 2 && mev::step_split(h->sp) ? 1 : 0;
+    return MEV_OK;
+}
+
 int mev_set_reset_routes(mev_handle* h, const int32_t* routes, int32_t count) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (count < 0 || count > h->nroutes) return fail(MEV_E_INVALID, "count must be in [0, number of routes]");

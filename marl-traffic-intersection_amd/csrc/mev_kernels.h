@@ -97,6 +97,8 @@ struct SimParams {
     int32_t step_kernel;
     // envs per fused k_step wave (host side): 0 auto, 1, 2 or 4 (reduced to fit 8 agent slots)
     int32_t step_pack;
+    // two waves per fused workgroup (host side): 0 auto (<= 2048 workgroups), 1 off, 2 on
+    int32_t step_split;
 };
 
 struct StepInputs {
@@ -114,6 +116,8 @@ struct StepInputs {
 int step_kernel_for(const SimParams& p);
 // envs per k_step wave the fused path uses for p (1, 2 or 4)
 int step_pack(const SimParams& p);
+// whether the fused path runs two waves per workgroup (car part / LiDAR overlap)
+bool step_split(const SimParams& p);
 // ev (nullable): three events recorded before k_cars, between k_cars and k_lidar, after k_lidar
 // (with k_step: before it, and twice after it)
 // dp: a device copy of p (k_step reads its parameters through it)

@@ -2779,10 +2779,19 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // live through the whole kernel and the SGPR allocator spills them into VGPR
 // lanes (a v_readlane per reload); through the pointer each field is an s_load
 // next to its use.
-template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1>
-__global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
+//
+// SPLIT (small batches, <= 2048 workgroups: <= 4 waves per SIMD): two waves per
+// workgroup share its LDS; wave 0 runs cars_pre, then both pass a barrier and
+// wave 1 runs the LiDAR while wave 0 runs cars_post -- the two latency chains
+// after the car part overlap instead of following each other.
+template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false>
+__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimParams* __restrict__ pp, StepInputs in,
+                                                                     Outputs out) {
+    static_assert(!SPLIT || (!TRAFFIC && !MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE),
+                  "split waves: the plain fused step");
     const SimParams& p = *pp;
     extern __shared__ __align__(16) unsigned char step_lds[];
+    const int wv = SPLIT ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
     // PK envs per wave (few agents per env): envs e .. e + PK - 1, see cars_pre
     const int e = xcd_env((int)blockIdx.x, (int)gridDim.x) * PK;
 #if defined(MEV_STAMPS_R)
@@ -2798,13 +2807,16 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
     NpcLDST<KM>* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
     if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
-    const CarsCtx cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK>(p, in, out, e, el, nl);
-    wave_lds_sync();
+    CarsCtx cx{};
+    if (wv == 0) cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK>(p, in, out, e, el, nl);
+    if (SPLIT) __syncthreads();
+    else wave_lds_sync();
 #if !defined(MEV_EXP_STOP) || MEV_EXP_STOP != 0  // timing-only stop0: the car part without cars_post
-    if (!MEV_POST_AFTER_LIDAR) {
+    if (!MEV_POST_AFTER_LIDAR && wv == 0) {
         cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
         wave_lds_sync();
     }
+    if (SPLIT && wv == 0) return;  // wave 1 runs the LiDAR
 #else
     return;
 #endif
@@ -2837,7 +2849,7 @@ __global__ __launch_bounds__(WAVE, 4) void k_step(const SimParams* __restrict__ 
         fused_store<TAB>(p, out, e, el, reinterpret_cast<const int*>(lbase + lay.res), lane);
     }
 #if defined(MEV_STAMPS_R)  // slot 7: end of the wave (low 40 bits) | where it ran (HW_ID[15:0], XCC_ID[2:0]) << 40
-    {
+    if (!SPLIT || wv == 1) {
         const unsigned long long t = __builtin_amdgcn_s_memrealtime() & ((1ull << 40) - 1);
         const unsigned hw = __builtin_amdgcn_s_getreg((15 << 11) | 4) & 0xffffu;
         const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
@@ -2988,6 +3000,18 @@ int step_pack(const SimParams& p) {
     return pk;
 }
 
+// two waves per fused workgroup (k_step SPLIT) when that keeps <= 4 waves per SIMD
+// (<= 2048 workgroups; 256 CUs x 4 SIMDs)
+#ifndef MEV_SPLIT_MAX_WG
+#define MEV_SPLIT_MAX_WG 2048
+#endif
+bool step_split(const SimParams& p) {
+    if (p.traffic || !fixed_fits<8, 0>(p) || p.step_split == 1) return false;
+    if (p.step_split == 2) return true;
+    const int pk = step_pack(p);
+    return (p.E + pk - 1) / pk <= MEV_SPLIT_MAX_WG;
+}
+
 template <bool TAB>
 static void launch_fused(const SimParams& p, const SimParams* dp, const StepInputs& in, const Outputs& out,
                          hipStream_t s) {
@@ -3003,9 +3027,16 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
     } else if (fixed_fits<8, 0>(p)) {  // compile-time LDS layout
         const unsigned lds = (unsigned)FixedLayout<8>::bytes;
         const int pk = step_pack(p);
-        if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3((p.E + 3) / 4), dim3(WAVE), lds, s, dp, in, out);
-        else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2>), dim3((p.E + 1) / 2), dim3(WAVE), lds, s, dp, in, out);
-        else hipLaunchKernelGGL((k_step<false, TAB, 8>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
+        const int wg = (p.E + pk - 1) / pk;
+        if (step_split(p)) {  // two waves per workgroup (<= 4 waves per SIMD)
+            if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            return;
+        }
+        if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else hipLaunchKernelGGL((k_step<false, TAB, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
     } else {
         const unsigned lds = (unsigned)step_layout(p).bytes;
         hipLaunchKernelGGL((k_step<false, TAB, 0>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);

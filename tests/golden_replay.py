@@ -79,7 +79,7 @@ def make_handle(mod, meta, num_envs: int, device: int = 0):
 
 
 def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: int = 0,
-           pack: int = 0) -> List[Report]:
+           pack: int = 0, split: int = 0) -> List[Report]:
     """Run the scenarios `names` (identical configs) as envs 0..B-1 of one handle
     (kernel: the step kernel path, 0 = automatic; None is returned when the
     requested path does not apply to the scenario's configuration)."""
@@ -102,6 +102,8 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
             return None
     if pack:
         h.set_step_pack(pack)  # envs per fused wave (scheduling only)
+    if split:
+        h.set_step_split(split)  # two waves per fused workgroup: 1 off, 2 on (scheduling only)
     troutes = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["traffic_routes"]]
     h.set_traffic_routes(troutes)
     n = int(meta["n_agents"])

@@ -70,6 +70,16 @@ def test_golden_scenario_packed_waves(mev, name, pack):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("name", [n for n in SINGLE if not G.load(n)["meta"]["traffic"]])
+def test_golden_scenario_split_waves(mev, name, split):
+    """Each non-traffic golden on the fused kernel with one wave per workgroup
+    (split 1) and with the car part and the LiDAR in two waves (split 2) -- the
+    small-batch default, forced off and on here; both bit-exact."""
+    (rep,) = G.replay(mev, name, kernel=2, split=split)
+    assert rep.ok, f"{name}: {rep.mismatches[:5]} (steps checked {rep.steps})"
+
+
 @pytest.mark.parametrize("pack", [2, 4])
 def test_golden_routes_packed_in_one_handle(mev, pack):
     """The 12 config-2 route scenarios as 12 envs of ONE handle, 2 or 4 envs per

@@ -79,13 +79,18 @@ def test_packed_waves_agree_full_size(mev, pack):
     bit for bit, step after step with auto-reset on."""
     for n in (1, 2):
         cfg = dict(num_envs=E, num_agents=n, lidar_rays=64, use_team_reward=1, max_steps=90, seed=5)
-        hs = [mev.Handle(**cfg) for _ in range(3)]
+        hs = [mev.Handle(**cfg) for _ in range(4)]
         hs[0].set_step_kernel(1)
         hs[1].set_step_kernel(2)
         hs[1].set_step_pack(1)
         hs[2].set_step_kernel(2)
         hs[2].set_step_pack(pack)
+        hs[2].set_step_split(1)
+        hs[3].set_step_kernel(2)
+        hs[3].set_step_pack(pack)
+        hs[3].set_step_split(2)  # two waves per workgroup
         assert hs[2].step_pack() == pack and hs[1].step_pack() == 1
+        assert hs[3].step_split() and not hs[2].step_split()
         rng = np.random.default_rng(13)
         for t in range(120):
             a = rng.uniform(-1, 1, (E, n, 2)).astype(np.float32)
@@ -93,9 +98,11 @@ def test_packed_waves_agree_full_size(mev, pack):
             for k in o[0]:
                 assert np.array_equal(o[0][k], o[1][k]), (n, t, k)
                 assert np.array_equal(o[0][k], o[2][k]), (n, t, k)
+                assert np.array_equal(o[0][k], o[3][k]), (n, t, k)
         s = [h.get_state() for h in hs]
         for k in s[0]:
             assert np.array_equal(s[0][k], s[2][k]), (n, k)
+            assert np.array_equal(s[0][k], s[3][k]), (n, k)
         for h in hs:
             h.close()
 

@@ -55,10 +55,11 @@ def run(cfg, steps, warmup, step_kernel=0, pack=0):
     c, l_, n = h.kernel_times()
     npc = float(h.get_state()["npc_count"].mean()) if cfg.get("traffic") else 0.0
     pk = h.step_pack()
+    split = h.step_split()
     h.close()
     r = dict(name=cfg["name"], workload=cfg["desc"], agent_steps_per_s=round(E * N / dt, 1),
              ms_per_step=round(dt * 1e3, 5), step_kernel="k_step (fused)" if fused else "k_cars + k_lidar",
-             envs_per_wave=pk,
+             envs_per_wave=pk, waves_per_workgroup=2 if split else 1,
              mean_npcs=round(npc, 3))
     if fused:
         r["k_step_ms_events"] = round(c / n, 5)
