@@ -78,8 +78,10 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # exact variant: k_step's ego state write-back at its end (product: in cars_post)
                "wblate": ["-DMEV_WB_LATE=1"],
                # the road march's tail (product: helper groups from 16 beams, 3 probes per lane)
-               "bfphys0": ["-DMEV_BF_PHYS=0"],
-               "nosplit": ["-DMEV_SPLIT_MAX_WG=0"],
+               "bfphys0": ["-DMEV_BF_PHYS=0"], "nostraight": ["-DMEV_LIDAR_STRAIGHT=0"],
+               "nosplit": ["-DMEV_SPLIT_MAX_WG=0"], "nohelptraf": ["-DMEV_HELP_TRAFFIC=0"],
+               "skew1": ["-DMEV_EXP_SKEW=1"], "skew2": ["-DMEV_EXP_SKEW=2"], "skew4": ["-DMEV_EXP_SKEW=4"],
+               "skewprio": ["-DMEV_EXP_SKEWPRIO"],
                "nohelp": ["-DMEV_MARCH_HELP=0"], "nprt6": ["-DMEV_MARCH_HELP=0", "-DMEV_LIDAR_NPR_TAIL=6"],
                "h8_3": ["-DMEV_MARCH_HELP=8"], "h32_3": ["-DMEV_MARCH_HELP=32"],
                "h16_2": ["-DMEV_NPT_HELP=2"], "h16_4": ["-DMEV_NPT_HELP=4"],

@@ -1924,6 +1924,25 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 // accumulated distances is absorbed by the slab margins and by one extra probe
 // index at each end of the range, so a real hit is never dropped.
 
+// Straight-line LiDAR arithmetic: the value is computed on every lane (an empty
+// volatile asm statement the compiler cannot sink into a branch), so a select
+// replaces the divergent branch -- exec-mask bookkeeping and a pipeline break --
+// the compiler would otherwise wrap around a short computation.  No instruction
+// is emitted for it.
+#ifndef MEV_LIDAR_STRAIGHT
+#define MEV_LIDAR_STRAIGHT 1
+#endif
+template <class T>
+__device__ __forceinline__ T lidar_keep(T v) {
+    if (MEV_LIDAR_STRAIGHT) asm volatile("" : "+v"(v));
+    return v;
+}
+// beam steps over a provably safe stretch (0 when it is shorter than one step)
+__device__ __forceinline__ int safe_steps(float safe, float stp, float inv_stp) {
+    const int j = lidar_keep((int)(safe * inv_stp));
+    return (safe >= stp) ? j : 0;
+}
+
 // Distance along a beam from its real point (fx, fy) over which every probe is
 // provably on screen and on the road (the truncated pixel is within 1 px per
 // axis, < 1.42 px, of the real point).  Each bound below alone guarantees its
@@ -1949,7 +1968,8 @@ __device__ inline float road_safe(float fx, float fy, float dx, float dy, float 
     const float bq = ocx * dx + ocy * dy;
     const float cq = ocx * ocx + ocy * ocy - rg * rg;
     const float disc = bq * bq - cq;
-    const float tdisc = cq <= 0.0f ? 0.0f : ((disc < 0.0f || bq >= 0.0f) ? big : -bq - __builtin_amdgcn_sqrtf(disc));
+    const float troot = lidar_keep(-bq - __builtin_amdgcn_sqrtf(disc));
+    const float tdisc = cq <= 0.0f ? 0.0f : ((disc < 0.0f || bq >= 0.0f) ? big : troot);
     const float tsq = fminf(sqm * iadx - rx * idx, sqm * iady - ry * idy);
     const float tq = fminf(rx * dx < 0.0f ? -rx * idx : big, ry * dy < 0.0f ? -ry * idy : big);
     const float sc = fmaxf(ax, ay) < sqm ? fminf(tdisc, fminf(tsq, tq)) : 0.0f;
@@ -2028,6 +2048,9 @@ constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
 #define MEV_NPT_HELP 3
 #endif
 static_assert(MEV_MARCH_HELP <= 32, "helper groups have at least 2 lanes");
+#ifndef MEV_HELP_TRAFFIC  // the helper groups in the traffic kernel too (config 4 +0.6 %)
+#define MEV_HELP_TRAFFIC 1
+#endif
 // probes phase 1 tests after a beam's safe stretch from the car centre
 #ifndef MEV_LIDAR_NPR1
 #define MEV_LIDAR_NPR1 MEV_LIDAR_NPR
@@ -2169,7 +2192,8 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const float qdx = iax - ccen, qdy = iay - ccen;
         const float onv = fmaxf(fminf(fminf(iax, iay) - rwf, fmaxf(iax, iay) - ccen), cr2p1 - (qdx * qdx + qdy * qdy));
         const bool stop = off_screen | ((k_ > 0) & (onv > 0.0f));
-        return past ? (S << 1) : (stop ? ((k_ << 1) | (off_screen ? 0 : 1)) : -1);
+        const int code = lidar_keep(stop ? ((k_ << 1) | (off_screen ? 0 : 1)) : -1);
+        return past ? (S << 1) : code;
     };
     // probes k_ .. k_ + NPR - 1 in march order: the first stop wins; (fx, fy) is
     // the last probe's point
@@ -2214,7 +2238,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
         const float safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
         // probes 1 .. j lie within j*step <= safe of the centre (car centre on screen)
-        const int k1 = pmax < (unsigned)WIDTH ? 1 + ((safe >= stp) ? (int)(safe * inv_stp) : 0) : 0;
+        const int k1 = pmax < (unsigned)WIDTH ? 1 + safe_steps(safe, stp, inv_stp) : 0;
         float fx, fy;
         const int r = probes_n(std::integral_constant<int, MEV_LIDAR_NPR1>{}, a.x, a.y, dx, dy, k1, fx, fy);
         return r >= 0 ? r : -(k1 + MEV_LIDAR_NPR1) - 1;
@@ -2317,7 +2341,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         }
         const float safe = road_safe(fx, fy, dx, dy, idx, idy, iadx, iady, rwm, ccen, crf);
         // probes kl+1 .. kl+j lie within j*step <= safe of the last probe kl = k + npr - 1
-        const int kn = k + npr + ((safe >= stp) ? (int)(safe * inv_stp) : 0);
+        const int kn = k + npr + safe_steps(safe, stp, inv_stp);
         const bool fin = act & ((r >= 0) | (kn >= S));
         if (fin) res[slot] = r >= 0 ? r : (S << 1);
         k = kn;
@@ -2366,7 +2390,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 int r = probes_n(std::integral_constant<int, NPH>{}, cx, cy, dx, dy, k0, fx, fy);
                 r = r >= 0 ? r : 0x7fffffff;
                 const float safe = road_safe(fx, fy, dx, dy, idx, idy, iadx, iady, rwm, ccen, crf);
-                int kn = k0 + NPH + ((safe >= stp) ? (int)(safe * inv_stp) : 0);
+                int kn = k0 + NPH + safe_steps(safe, stp, inv_stp);
                 r = min(r, __builtin_amdgcn_mov_dpp(r, 0xB1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
                 if constexpr (GS == 2) {
                     kn = __builtin_amdgcn_mov_dpp(kn, 0xF5, 0xf, 0xf, false);  // quad_perm [1,1,3,3]
@@ -2807,6 +2831,14 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
     NpcLDST<KM>* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
     if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
+#ifdef MEV_EXP_SKEW  // experiment: odd workgroups start MEV_EXP_SKEW x 64 x 127 cycles late
+    if (blockIdx.x & 1) {
+        for (int t = 0; t < MEV_EXP_SKEW; ++t) __builtin_amdgcn_s_sleep(127);
+    }
+#endif
+#ifdef MEV_EXP_SKEWPRIO  // experiment: odd workgroups run the car part one priority level lower
+    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS - 1);
+#endif
     CarsCtx cx{};
     if (wv == 0) cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK>(p, in, out, e, el, nl);
     if (SPLIT) __syncthreads();
@@ -2836,7 +2868,8 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
         if (j0 > 0) wave_lds_sync();
         if (j0 > 0 || MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);  // each pool
         const int na = NS - j0 < G ? NS - j0 : G;
-        lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, TRAFFIC ? LIDAR_NPR : MEV_LIDAR_NPR_TAIL, !TRAFFIC>(
+        lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, TRAFFIC ? LIDAR_NPR : MEV_LIDAR_NPR_TAIL,
+                   !TRAFFIC || MEV_HELP_TRAFFIC>(
             p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
     }
     if (MEV_POST_AFTER_LIDAR) {  // experiment (variant postlate): measured slower, 41.6 -> 44.1 us

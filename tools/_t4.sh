@@ -1,5 +1,6 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -2 gpurun_out/pytest_gpu.log
-for p in 1 2 4; do timeout -k 10 120 python tools/bench_sweep.py --only cfg2 --pack $p --steps 1000 2>/dev/null | tail -1; done
+timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py tests/test_lidar_stress_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread 2>&1 | tail -1
+bash tools/ab_sweep.sh cfg3 2 "" nostraight
+bash tools/ab_sweep.sh cfg2 2 "" nostraight
+bash tools/ab_sweep.sh cfg4 1 "" nostraight
