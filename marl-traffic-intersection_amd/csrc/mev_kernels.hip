@@ -514,6 +514,12 @@ __device__ __forceinline__ float npc_throttle(float acc_thr, float min_conflict)
     return thr;
 }
 
+#ifndef MEV_NPC_SOLO  // at most one alive NPC: part 1 moves it too (measured 2 % slower at config 4: off)
+#define MEV_NPC_SOLO 0
+#endif
+#ifndef MEV_NPC_KEEPSKIP  // no compaction pass when no NPC is erased
+#define MEV_NPC_KEEPSKIP 1
+#endif
 template <class NL>
 __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NL& nl, int lane,
                           const float* ego_x, const float* ego_y, const NpcRegs& nr) {
@@ -639,7 +645,11 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // part 1: the first path index, the steering command towards path[idx + 12]
     // (:50-63) and Car::update's steering part with its tangent (Car.cpp:11-23;
     // the steering input is known before the throttle), the cruise throttle
-    // (:66-70) and the distance to the centre (:83)
+    // (:66-70) and the distance to the centre (:83).
+    // solo (at most one alive NPC: nobody to plan against, the throttle is the
+    // cruise one): part 1 also moves it (round A's move) from a 128-point window
+    // loaded with the first one -- no second path load round trip.
+    const bool solo = MEV_NPC_SOLO && cnt <= 8 && __popcll(ballot(lane < cnt && nl.alive[lane < cnt ? lane : 0] != 0)) < 2;
     for (int k0 = 0; k0 < cnt; k0 += 8) {
         const int k = k0 + grp;
         const bool act = k < cnt;
@@ -655,7 +665,13 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             pf0 = P[s0 < PATH_LEN ? s0 : PATH_LEN - 1];
             pf1 = P[s0 + 8 < PATH_LEN ? s0 + 8 : PATH_LEN - 1];
         }
-        float2 pt[8];
+        float2 pt[8], pt2[8];
+        if (solo) {  // path[start_i + 64 .. start_i + 127], in flight with the first window
+            const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+            const int s2 = (nl.pidx[kk] < 0 ? 0 : nl.pidx[kk]) + 64 + sub * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pt2[j] = P[s2 + j < PATH_LEN ? s2 + j : PATH_LEN - 1];
+        }
         int start_i;
         const int pidx0 = npc_window(kk, nl.pidx[kk], x, y, pt, start_i);
         // the look-ahead point min(pidx0 + 12, 159) lies in the 64-point window
@@ -679,6 +695,54 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             nl.accb[k] = (v < target_speed) ? 0.5f : ((v > target_speed + 1.0f) ? -0.1f : 0.0f);
             nl.mdc[k] = hypotf(x - CXf, y - CYf);
             nl.pidx0[k] = pidx0;
+        }
+        if (solo) {
+            // every lane of the group: the target point (from the lane holding it), the
+            // steering, Car::update with the cruise throttle and the second path index
+            // over path[pidx0, pidx0 + 50) among the 128 window points (first minimum)
+            float2 tl = pt[0];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) tl = ((toff & 7) == j) ? pt[j] : tl;
+            const int src = (grp * 8 + (toff >> 3)) * 4;
+            const float tx = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(tl.x)));
+            const float ty = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(tl.y)));
+            const float h = nl.h[kk], v = nl.v[kk];
+            const float heading_err = wrap_angle(atan2f_wave(-(ty - y), tx - x) - h);
+            float steer_cmd = heading_err * 3.0f;
+            steer_cmd = (1.0f < steer_cmd) ? 1.0f : steer_cmd;
+            steer_cmd = (steer_cmd < -1.0f) ? -1.0f : steer_cmd;
+            const float ns = car_steer(nl.steer[kk], steer_cmd);
+            const float nt = tanf(ns);
+            const float target_speed = PHYSICS_MAX_SPEED * 0.4f;
+            const float accb = (v < target_speed) ? 0.5f : ((v > target_speed + 1.0f) ? -0.1f : 0.0f);
+            Kin kin{x, y, v, h, nl.acc[kk], nl.steer[kk]};
+            float cn, sn;
+            car_update_steered(kin, accb, ns, nt, in.dt, &cn, &sn);
+            float bd = __builtin_inff();
+            int bi = 0x7fffffff;
+            auto scan_pt = [&](float2 w, int q) {
+                if (q >= pidx0 && q < pidx0 + 50 && q < PATH_LEN) {
+                    const float wdx = w.x - kin.x, wdy = w.y - kin.y;
+                    const float d = wdx * wdx + wdy * wdy;
+                    if (d < bd) { bd = d; bi = q; }
+                }
+            };
+#pragma unroll
+            for (int j = 0; j < 8; ++j) scan_pt(pt[j], start_i + sub * 8 + j);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) scan_pt(pt2[j], start_i + 64 + sub * 8 + j);
+            auto take = [&](float od, int oi) {
+                if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+            };
+            take(dpp_f(bd, 0xB1), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xf, 0xf, false));    // quad_perm [1,0,3,2]
+            take(dpp_f(bd, 0x4E), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xf, 0xf, false));    // quad_perm [2,3,0,1]
+            take(dpp_f(bd, 0x141), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xf, 0xf, false));  // row_half_mirror
+            if (act && sub == 0 && nl.alive[k]) {
+                nl.thr_a[k] = accb;
+                nl.xn[k] = kin.x; nl.yn[k] = kin.y; nl.vn[k] = kin.v; nl.hn[k] = kin.h;
+                nl.accn[k] = kin.acc; nl.steern[k] = kin.steer; nl.cn[k] = cn; nl.sn[k] = sn;
+                nl.pidxn[k] = bi == 0x7fffffff ? (pidx0 < 0 ? 0 : pidx0) : bi;
+            }
         }
         if (act && sub == 7) {  // the route's end point, for the arrival test after the turns
             const float2 pe = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[k] * (2 * PATH_LEN))[PATH_LEN - 1];
@@ -959,12 +1023,12 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     if (__popcll(alive_k) >= 2) {
 #endif
         plan_all(false, nl.thr_a);
-    } else if (lane < cnt) {
+    } else if (lane < cnt && !solo) {
         nl.thr_a[lane] = nl.accb[lane];  // no other NPC to plan against: the cruise throttle
         wave_lds_sync();
     }
     NT(2);  // round A: plans (pairs)
-    move_all(nl.thr_a, alive_k, true);
+    if (!solo) move_all(nl.thr_a, alive_k, true);  // (solo: moved in part 1)
     NT(3);  // round A: moves
     unsigned long long done_m = alive_k;  // NPCs whose round-A move is final
     int kseq = cnt;                       // the first NPC left to the sequential turns
@@ -1081,20 +1145,23 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         keep = !arrived && !oos;
     }
     const unsigned long long keep_m = ballot(keep);
-    const int dst = __builtin_popcountll(keep_m & ((1ull << lane) - 1ull));
-    float kx = 0, ky = 0, kv = 0, kh = 0, ka = 0, ks = 0, kc = 0, ksn = 0;
-    int kp = 0, kr = 0, ki = 0;
-    if (keep) {
-        kx = nl.x[lane]; ky = nl.y[lane]; kv = nl.v[lane]; kh = nl.h[lane]; ka = nl.acc[lane]; ks = nl.steer[lane];
-        kc = nl.c[lane]; ksn = nl.s[lane]; kp = nl.pidx[lane]; kr = nl.route[lane]; ki = nl.intent[lane];
-    }
-    wave_lds_sync();
-    if (keep) {
-        nl.x[dst] = kx; nl.y[dst] = ky; nl.v[dst] = kv; nl.h[dst] = kh; nl.acc[dst] = ka; nl.steer[dst] = ks;
-        nl.c[dst] = kc; nl.s[dst] = ksn; nl.pidx[dst] = kp; nl.route[dst] = kr; nl.intent[dst] = ki; nl.alive[dst] = 1;
-    }
     const int newcnt = __builtin_popcountll(keep_m);
-    wave_lds_sync();
+    // (most steps erase nothing: the survivors already are the prefix 0 .. cnt - 1)
+    if (!MEV_NPC_KEEPSKIP || keep_m != (cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull))) {
+        const int dst = __builtin_popcountll(keep_m & ((1ull << lane) - 1ull));
+        float kx = 0, ky = 0, kv = 0, kh = 0, ka = 0, ks = 0, kc = 0, ksn = 0;
+        int kp = 0, kr = 0, ki = 0;
+        if (keep) {
+            kx = nl.x[lane]; ky = nl.y[lane]; kv = nl.v[lane]; kh = nl.h[lane]; ka = nl.acc[lane]; ks = nl.steer[lane];
+            kc = nl.c[lane]; ksn = nl.s[lane]; kp = nl.pidx[lane]; kr = nl.route[lane]; ki = nl.intent[lane];
+        }
+        wave_lds_sync();
+        if (keep) {
+            nl.x[dst] = kx; nl.y[dst] = ky; nl.v[dst] = kv; nl.h[dst] = kh; nl.acc[dst] = ka; nl.steer[dst] = ks;
+            nl.c[dst] = kc; nl.s[dst] = ksn; nl.pidx[dst] = kp; nl.route[dst] = kr; nl.intent[dst] = ki; nl.alive[dst] = 1;
+        }
+        wave_lds_sync();
+    }
     // store back + corners of the survivors (for ego-NPC SAT)
     if (lane < newcnt) {
         const int g = e * K + lane;
