@@ -514,6 +514,9 @@ __device__ __forceinline__ float npc_throttle(float acc_thr, float min_conflict)
     return thr;
 }
 
+#ifndef MEV_SAT_CIRCLE  // the car-car SAT behind a circumcircle test
+#define MEV_SAT_CIRCLE 1
+#endif
 #ifndef MEV_NPC_SOLO  // at most one alive NPC: part 1 moves it too (measured 2 % slower at config 4: off)
 #define MEV_NPC_SOLO 0
 #endif
@@ -1119,7 +1122,10 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const int pi = pbase + lane;
             // (a, b) = (pi / cnt, pi % cnt); lane = 8a + b without the integer division when cnt <= 8
             const int a = cnt <= 8 ? (lane >> 3) : pi / cnt, b = cnt <= 8 ? (lane & 7) : pi % cnt;
-            if ((cnt <= 8 ? (a < cnt && b < cnt) : pi < cnt * cnt) && a < b &&
+            const int aa = a < cnt ? a : 0, bb = b < cnt ? b : 0;
+            const float cdx = nl.x[aa] - nl.x[bb], cdy = nl.y[aa] - nl.y[bb];
+            const bool close = !MEV_SAT_CIRCLE || !(cdx * cdx + cdy * cdy > 3600.0f);  // circumcircles (cars_pre)
+            if ((cnt <= 8 ? (a < cnt && b < cnt) : pi < cnt * cnt) && a < b && close &&
                 sat_collide(nl.cx[a], nl.cy[a], nl.c[a], nl.s[a], nl.cx[b], nl.cy[b], nl.c[b], nl.s[b]))
                 atomicOr(&nl.col[a], 1ull << b);
         }
@@ -1639,7 +1645,12 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         // (a, b) = (pi / N, pi % N); lane = 8a + b without the integer division when N <= 8
         const int a = N <= 8 ? (tid >> 3) : pi / N, b = N <= 8 ? (tid & 7) : pi % N;
         if (N <= 8 ? (a < N && b < N) : pi < N * N) {
-            if (a < b && (PK == 1 || a / NE == b / NE) && el.alive[a] && el.alive[b] &&
+            // two cars whose centres are more than the sum of their circumradii apart
+            // (2 x 29.55 px; 60 px with margin for the rounding of the corners) cannot
+            // overlap: the SAT runs only for lanes (and waves) with a close pair
+            const float cdx = el.x[a] - el.x[b], cdy = el.y[a] - el.y[b];
+            const bool close = !MEV_SAT_CIRCLE || !(cdx * cdx + cdy * cdy > 3600.0f);
+            if (a < b && (PK == 1 || a / NE == b / NE) && el.alive[a] && el.alive[b] && close &&
                 sat_collide(reinterpret_cast<const float*>(&el.cx[a]), reinterpret_cast<const float*>(&el.cy[a]),
                             el.c[a], el.s[a], reinterpret_cast<const float*>(&el.cx[b]),
                             reinterpret_cast<const float*>(&el.cy[b]), el.c[b], el.s[b]))
@@ -1652,7 +1663,9 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             const int pi = pbase + tid;
             if (pi < N * ncnt) {
                 const int a = pi / ncnt, b = pi % ncnt;
-                if (el.alive[a] && sat_collide(reinterpret_cast<const float*>(&el.cx[a]),
+                const float cdx = el.x[a] - nl->x[b], cdy = el.y[a] - nl->y[b];
+                const bool close = !MEV_SAT_CIRCLE || !(cdx * cdx + cdy * cdy > 3600.0f);  // as for the ego pairs
+                if (el.alive[a] && close && sat_collide(reinterpret_cast<const float*>(&el.cx[a]),
                                                reinterpret_cast<const float*>(&el.cy[a]), el.c[a], el.s[a],
                                                nl->cx[b], nl->cy[b], nl->c[b], nl->s[b]))
                     el.colnpc[a] = 1;
