@@ -305,6 +305,7 @@ struct NpcLDST {
         };
         struct {  // the controller's round-A states (npc_phase part 2), dead once committed
             float xn[KM], yn[KM], vn[KM], hn[KM], accn[KM], steern[KM], cn[KM], sn[KM];
+            float mdcn[KM];  // the round-A state's distance to the centre
         };
     };
     unsigned long long col[KM];
@@ -393,9 +394,10 @@ __device__ inline int wave_argmin_dpp(float d, int i) {
 struct NpcPair {
     bool f30, f50, pok, yfar;
 };
+// odcj: j's distance to the centre, hypotf(oxj - 375, oyj - 375) (precomputed per NPC)
 __device__ __forceinline__ NpcPair npc_pair(int k, float x, float y, float h, float v, float ck, float sk,
                                             float my_dist_to_center, bool jvalid, int j, float oxj, float oyj,
-                                            float ohj, float ovj, float ocj, float osj) {
+                                            float ohj, float ovj, float ocj, float osj, float odcj) {
     const float CXf = WIDTH * 0.5f, CYf = HEIGHT * 0.5f;
     NpcPair r{false, false, false, false};
     const float vx = ck, vy = -sk;
@@ -458,7 +460,7 @@ __device__ __forceinline__ NpcPair npc_pair(int k, float x, float y, float h, fl
             }
         }
         if (pok) {
-            const float odc = hypotf(oxj - CXf, oyj - CYf);
+            const float odc = odcj;
             if (v < 1.0f && ovj > 3.0f && odc < my_dist_to_center + 25.0f) yfar = true;
             else if (odc < my_dist_to_center - 5.0f) yfar = true;
             else if (fabs_f(odc - my_dist_to_center) <= 5.0f) yfar = k < j;  // address order
@@ -516,6 +518,9 @@ __device__ __forceinline__ float npc_throttle(float acc_thr, float min_conflict)
 
 #ifndef MEV_SAT_CIRCLE  // the car-car SAT behind a circumcircle test
 #define MEV_SAT_CIRCLE 1
+#endif
+#ifndef MEV_NPC_ODC  // the others' distances to the centre precomputed per NPC, not per pair
+#define MEV_NPC_ODC 1
 #endif
 #ifndef MEV_NPC_SOLO  // at most one alive NPC: part 1 moves it too (measured 2 % slower at config 4: off)
 #define MEV_NPC_SOLO 0
@@ -816,11 +821,12 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const float oxj = newj ? nl.xn[jj] : nl.x[jj], oyj = newj ? nl.yn[jj] : nl.y[jj];
             const float ohj = newj ? nl.hn[jj] : nl.h[jj], ovj = newj ? nl.vn[jj] : nl.v[jj];
             const float ocj = newj ? nl.cn[jj] : nl.c[jj], osj = newj ? nl.sn[jj] : nl.s[jj];
+            const float odcj = MEV_NPC_ODC ? (newj ? nl.mdcn[jj] : nl.mdc[jj]) : hypotf(oxj - CXf, oyj - CYf);
             // k's route pieces (bounding boxes), in flight during the pair tests
             const float4* PB = p.rt.pbox + (size_t)nl.route[kk] * 3;
             const float4 pb0 = PB[0], pb1 = PB[1], pb2 = PB[2];
             const NpcPair pr = npc_pair(k, nl.x[kk], nl.y[kk], nl.h[kk], nl.v[kk], nl.c[kk], nl.s[kk], nl.mdc[kk],
-                                        jvalid, j, oxj, oyj, ohj, ovj, ocj, osj);
+                                        jvalid, j, oxj, oyj, ohj, ovj, ocj, osj, odcj);
             // prefilter of the ghost scan: j can only stop k's scan if it lies within
             // SAFE of one of k's scanned path points path[idx0, idx0 + 120); the points
             // of each route piece lie in its bounding box, so j farther than SAFE + 0.01
@@ -1015,6 +1021,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             if (act && sub == 0) {
                 nl.xn[k] = kin.x; nl.yn[k] = kin.y; nl.vn[k] = kin.v; nl.hn[k] = kin.h;
                 nl.accn[k] = kin.acc; nl.steern[k] = kin.steer; nl.cn[k] = cn; nl.sn[k] = sn;
+                nl.mdcn[k] = hypotf(kin.x - CXf, kin.y - CYf);
                 nl.pidxn[k] = bi == 0x7fffffff ? (pidx0 < 0 ? 0 : pidx0) : bi;
             }
         }
@@ -1079,7 +1086,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                 oxj = nl.x[j]; oyj = nl.y[j]; ohj = nl.h[j]; ovj = nl.v[j]; ocj = nl.c[j]; osj = nl.s[j];
             }
             const NpcPair pr = npc_pair(k, x, y, h, v, nl.c[k], nl.s[k], nl.mdc[k], jvalid, j, oxj, oyj, ohj, ovj,
-                                        ocj, osj);
+                                        ocj, osj, hypotf(oxj - CXf, oyj - CYf));
             float acc_thr = nl.accb[k];
             if (ballot(pr.f30)) acc_thr = -1.0f;
             else if (ballot(pr.f50)) acc_thr = (-0.2f < acc_thr) ? -0.2f : acc_thr;
