@@ -391,6 +391,9 @@ __device__ inline int wave_argmin_dpp(float d, int i) {
 // terms: pose, speed, cos/sin of its heading, distance to the centre.  The
 // front-car and ghost-scan tests need only these thresholds, so a turn's plan
 // is ballots over j, not reductions.
+#ifndef MEV_NPC_FAR  // no exact distance for NPC pairs farther than 130 px (exact, within noise: off)
+#define MEV_NPC_FAR 0
+#endif
 struct NpcPair {
     bool f30, f50, pok, yfar;
 };
@@ -405,7 +408,11 @@ __device__ __forceinline__ NpcPair npc_pair(int k, float x, float y, float h, fl
     // ghost-scan filters (the same expressions in the reference, :37/:101/:107)
     const float dxj = oxj - x;
     const float dyj = oyj - y;
-    const float dist_j = hypotf(dxj, dyj);
+    // the exact distance decides only for pairs within 125.1 px (the front-car test
+    // at 80, the side-by-side test at |lon| < 108 and |lat| < 63); a pair whose f32
+    // squared distance exceeds 130^2 takes none of those branches with either value
+    float dist_j = 1.0e30f;
+    if (!MEV_NPC_FAR || !(dxj * dxj + dyj * dyj > 16900.0f)) dist_j = hypotf(dxj, dyj);
     const float adiff_j = fabs_f(wrap_angle(h - ohj));
     if (jvalid) {
         const float dist = dist_j;
