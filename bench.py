@@ -429,7 +429,7 @@ def main():
             pb = algorithmic_bytes_per_agent_step(RAYS) * E * N
             achieved = pb / (stream_ms * 1e-3) / 1e9
             tab = 'true' if dist_table_needed() else 'false'
-            kname = f"mev::k_step<false, {tab}, {8 if N_AGENTS <= 8 and RAYS <= 128 else 0}, 64, 1>"
+            kname = f"mev::k_step<false, {tab}, {8 if N_AGENTS <= 8 and RAYS <= 128 else 0}, 64, 1, false>"
             roofline = {
                 "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic_of.get("k_step"),

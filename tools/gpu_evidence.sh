@@ -41,4 +41,8 @@ fi
 if [ "$what" = sweep ] || [ "$what" = all ]; then
   timeout -k 10 300 python tools/bench_sweep.py --out $OUT/sweep.json > $OUT/sweep.txt 2>&1
   tail -12 $OUT/sweep.txt
+  timeout -k 10 300 python tools/env_latency.py > $OUT/env_latency.txt 2>&1
+  tail -12 $OUT/env_latency.txt
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.txt 2>&1
+  tail -2 $OUT/smoke.txt
 fi
