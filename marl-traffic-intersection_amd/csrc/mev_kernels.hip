@@ -2031,6 +2031,15 @@ __device__ __forceinline__ T lidar_keep(T v) {
     if (MEV_LIDAR_STRAIGHT) asm volatile("" : "+v"(v));
     return v;
 }
+// the probe's integer road test / packed position (exact; measured 0.5-1.4 % slower
+// together at configs 2-3: off, the float forms)
+#ifndef MEV_PROBE_INT
+#define MEV_PROBE_INT 0
+#endif
+#ifndef MEV_PROBE_PK
+#define MEV_PROBE_PK 0
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
 // beam steps over a provably safe stretch (0 when it is shorter than one step)
 __device__ __forceinline__ int safe_steps(float safe, float stp, float inv_stp) {
     const int j = lidar_keep((int)(safe * inv_stp));
@@ -2266,6 +2275,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     const float crf = CORNER_RADIUS, ccen = rwf + crf;
     const float cr2p1 = crf * crf + 1.0f;
     const float rwm = rwf - 1.5f;
+    const int irw_i = p.irw, icen = p.irw + 84;
     // the reference's stop test of march probe k at (cx_, cy_) + d_k (dx_, dy_):
     // returns the beam's result (k << 1 | hit; S << 1 past the last probe) or -1
     // to go on, and the probe's real point
@@ -2273,8 +2283,16 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const bool past = k_ >= S;
         const int kc = past ? S - 1 : k_;
         const float d = TAB ? p.dist_tab[kc] : (float)kc * stp;
+#if MEV_PROBE_PK
+        // the probe point as one packed multiply and add (v_pk_mul_f32, v_pk_add_f32:
+        // the same IEEE roundings as the scalar pair)
+        const f2v fp = f2v{cx_, cy_} + f2v{dx_, dy_} * d;
+        fx = fp.x;
+        fy = fp.y;
+#else
         fx = cx_ + dx_ * d;
         fy = cy_ + dy_ * d;
+#endif
         const int px = (int)fx, py = (int)fy;
         // exact reference predicates at the truncated pixel: screen, then
         // (k > 0) road == RoadGeometry::is_on_road at integer pixels:
@@ -2282,10 +2300,21 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         //               and (in a strip: min(ax, ay) <= rw  or  corner square: max <= rw + cr)
         const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
         const bool off_screen = pmax >= (unsigned)WIDTH;
+#if MEV_PROBE_INT
+        // in integers (every term is an integer below 2^12 on screen; off screen the
+        // road test is not used): off road <=> in the grass disc, or outside both the
+        // strips and the corner square
+        const int iax = abs(px - 375), iay = abs(py - 375);
+        const int qdx = iax - icen, qdy = iay - icen;
+        const int qd2 = __mul24(qdx, qdx) + __mul24(qdy, qdy);
+        const bool offroad = (min(iax, iay) > irw_i && max(iax, iay) > icen) || qd2 <= 84 * 84;
+        const bool stop = off_screen | ((k_ > 0) & offroad);
+#else
         const float iax = fabs_f((float)(px - 375)), iay = fabs_f((float)(py - 375));
         const float qdx = iax - ccen, qdy = iay - ccen;
         const float onv = fmaxf(fminf(fminf(iax, iay) - rwf, fmaxf(iax, iay) - ccen), cr2p1 - (qdx * qdx + qdy * qdy));
         const bool stop = off_screen | ((k_ > 0) & (onv > 0.0f));
+#endif
         const int code = lidar_keep(stop ? ((k_ << 1) | (off_screen ? 0 : 1)) : -1);
         return past ? (S << 1) : code;
     };
