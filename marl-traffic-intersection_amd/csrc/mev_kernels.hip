@@ -115,14 +115,48 @@ constexpr int MAXOB = MAXN + MAXK;
 #endif
 
 // --------------------------------------------------------------- helpers ---
-// SoA field k of the ego / NPC blocks (one base pointer + stride, see EgoSoA)
-__device__ inline float* egof(const SimParams& p, int k) { return p.ego.x + p.ego.stride * k; }
-__device__ inline int32_t* egoi(const SimParams& p, int k) {
-    return reinterpret_cast<int32_t*>(p.ego.x + p.ego.stride * k);
+// A pointer the kernel reads through SimParams as a global-memory pointer.  The
+// compiler cannot tell where a pointer loaded from memory points, so it would emit
+// FLAT loads and stores, which count on lgkmcnt like LDS operations: every later
+// s_waitcnt lgkmcnt for an LDS read would then also wait for them (a path load in
+// flight could not overlap the LDS work after it).  Every array in SimParams is a
+// device (global) allocation.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gmem(T* q) {
+    return (__attribute__((address_space(1))) T*)q;
 }
-__device__ inline float* npcf(const SimParams& p, int k) { return p.npc.x + p.npc.stride * k; }
-__device__ inline int32_t* npci(const SimParams& p, int k) {
-    return reinterpret_cast<int32_t*>(p.npc.x + p.npc.stride * k);
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+// float2 / float4 arrays in global memory (HIP's vector classes cannot be accessed
+// through an address-space-qualified pointer; their native vector types can)
+struct GF2 {
+    const __attribute__((address_space(1))) f2v* q;
+    __device__ __forceinline__ float2 operator[](int i) const {
+        const f2v v = q[i];
+        return make_float2(v.x, v.y);
+    }
+};
+struct GF4 {
+    const __attribute__((address_space(1))) f4v* q;
+    __device__ __forceinline__ float4 operator[](int i) const {
+        const f4v v = q[i];
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+};
+__device__ __forceinline__ GF2 gf2(const float* base) { return GF2{(const __attribute__((address_space(1))) f2v*)base}; }
+__device__ __forceinline__ GF4 gf4(const float4* base) { return GF4{(const __attribute__((address_space(1))) f4v*)base}; }
+// SoA field k of the ego / NPC blocks (one base pointer + stride, see EgoSoA)
+__device__ inline __attribute__((address_space(1))) float* egof(const SimParams& p, int k) {
+    return gmem(p.ego.x + p.ego.stride * k);
+}
+__device__ inline __attribute__((address_space(1))) int32_t* egoi(const SimParams& p, int k) {
+    return gmem(reinterpret_cast<int32_t*>(p.ego.x + p.ego.stride * k));
+}
+__device__ inline __attribute__((address_space(1))) float* npcf(const SimParams& p, int k) {
+    return gmem(p.npc.x + p.npc.stride * k);
+}
+__device__ inline __attribute__((address_space(1))) int32_t* npci(const SimParams& p, int k) {
+    return gmem(reinterpret_cast<int32_t*>(p.npc.x + p.npc.stride * k));
 }
 __device__ inline unsigned long long ballot(bool p) { return __ballot(p); }
 
@@ -232,7 +266,7 @@ __device__ inline int reset_route(const SimParams& p, uint64_t ctr, int e, int i
     if (p.n_reset_routes <= 0) return fixed;
     uint32_t r0, r1;
     philox((uint32_t)ctr, (uint32_t)(ctr >> 32) ^ 0x9E3779B9u, (uint32_t)e * 64u + (uint32_t)i, p.seed, &r0, &r1);
-    return p.reset_routes[(int)(((uint64_t)r0 * (uint32_t)p.n_reset_routes) >> 32)];
+    return gmem(p.reset_routes)[(int)(((uint64_t)r0 * (uint32_t)p.n_reset_routes) >> 32)];
 }
 
 // dist of march probe k: the reference accumulates `dist += step_size` in
@@ -242,7 +276,7 @@ __device__ inline int reset_route(const SimParams& p, uint64_t ctr, int e, int i
 // dist += step like Lidar.cpp:33), read them from the table
 template <bool TAB>
 __device__ inline float march_dist(const SimParams& p, int k) {
-    if constexpr (TAB) return p.dist_tab[k];
+    if constexpr (TAB) return gmem(p.dist_tab)[k];
     else return (float)k * p.lidar_step;
 }
 
@@ -343,7 +377,7 @@ __device__ inline NpcRegs npc_load(const SimParams& p, int e, int lane) {
         r.x = npcf(p, NF_X)[g]; r.y = npcf(p, NF_Y)[g]; r.v = npcf(p, NF_V)[g]; r.h = npcf(p, NF_H)[g];
         r.acc = npcf(p, NF_ACC)[g]; r.steer = npcf(p, NF_STEER)[g];
         r.pidx = npci(p, NF_PIDX)[g]; r.route = npci(p, NF_ROUTE)[g]; r.intent = npci(p, NF_INTENT)[g];
-        r.alive = p.npc.alive[g];
+        r.alive = gmem(p.npc.alive)[g];
     }
     return r;
 }
@@ -562,8 +596,8 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         }
     }
     if (r >= 0) {
-        const int rid = p.traffic_routes[r];
-        const float sx = p.rt.spawn[3 * rid], sy = p.rt.spawn[3 * rid + 1];
+        const int rid = gmem(p.traffic_routes)[r];
+        const float sx = gmem(p.rt.spawn)[3 * rid], sy = gmem(p.rt.spawn)[3 * rid + 1];
         const float min_dist = CAR_LENGTH * 2.5f;
         const float min_d2 = min_dist * min_dist;
         // is_spawn_blocked (:240-259): every ego (alive or not) and every NPC
@@ -593,12 +627,12 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                     nl.x[cnt] = sx;
                     nl.y[cnt] = sy;
                     nl.v[cnt] = 0.0f;
-                    nl.h[cnt] = p.rt.spawn[3 * rid + 2];
+                    nl.h[cnt] = gmem(p.rt.spawn)[3 * rid + 2];
                     nl.acc[cnt] = 0.0f;
                     nl.steer[cnt] = 0.0f;
                     nl.pidx[cnt] = 0;
                     nl.route[cnt] = rid;
-                    nl.intent[cnt] = p.rt.intent[rid];
+                    nl.intent[cnt] = gmem(p.rt.intent)[rid];
                     nl.alive[cnt] = 1;
                 }
                 ++cnt;
@@ -630,7 +664,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // each, 8 window points per lane, first minimum wins); returns the new index
     // and leaves the 64-point window in pt
     auto npc_window = [&](int kk, int idx, float x, float y, float2* pt, int& start_i) -> int {
-        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
         start_i = idx < 0 ? 0 : idx;
         const int wcnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
 #pragma unroll
@@ -675,14 +709,14 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
 #endif
         float2 pf0 = make_float2(0.0f, 0.0f), pf1 = pf0;
         if (MEV_NPC_PREFETCH) {
-            const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+            const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
             const int s0 = (nl.pidx[kk] < 0 ? 0 : nl.pidx[kk]) + 64 + sub * 16;
             pf0 = P[s0 < PATH_LEN ? s0 : PATH_LEN - 1];
             pf1 = P[s0 + 8 < PATH_LEN ? s0 + 8 : PATH_LEN - 1];
         }
         float2 pt[8], pt2[8];
         if (solo) {  // path[start_i + 64 .. start_i + 127], in flight with the first window
-            const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+            const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
             const int s2 = (nl.pidx[kk] < 0 ? 0 : nl.pidx[kk]) + 64 + sub * 8;
 #pragma unroll
             for (int j = 0; j < 8; ++j) pt2[j] = P[s2 + j < PATH_LEN ? s2 + j : PATH_LEN - 1];
@@ -760,7 +794,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             }
         }
         if (act && sub == 7) {  // the route's end point, for the arrival test after the turns
-            const float2 pe = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[k] * (2 * PATH_LEN))[PATH_LEN - 1];
+            const float2 pe = gf2(p.rt.path + (size_t)nl.route[k] * (2 * PATH_LEN))[PATH_LEN - 1];
             nl.endx[k] = pe.x;
             nl.endy[k] = pe.y;
         }
@@ -791,7 +825,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // NPC kk's ghost points path[idx0 + lane] and path[idx0 + 64 + lane] (clamped;
     // only indices below min(idx0 + 120, 160) are used)
     auto fetch_ghost = [&](int kk, float2& a, float2& b) {
-        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
         const int i0 = nl.pidx0[kk] + lane, i1 = i0 + WAVE;
         a = P[i0 < PATH_LEN ? i0 : PATH_LEN - 1];
         b = P[i1 < PATH_LEN ? i1 : PATH_LEN - 1];
@@ -800,7 +834,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // path[idx0 + 8t .. idx0 + 8t + 7] (clamped; only indices below min(idx0 + 120,
     // 160) are used)
     auto load_ghost8 = [&](int kk, float2* gp) {
-        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
         const int q0 = nl.pidx0[kk] + 8 * (lane & 15);
 #pragma unroll
         for (int i = 0; i < 8; ++i) gp[i] = P[q0 + i < PATH_LEN ? q0 + i : PATH_LEN - 1];
@@ -830,7 +864,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const float ocj = newj ? nl.cn[jj] : nl.c[jj], osj = newj ? nl.sn[jj] : nl.s[jj];
             const float odcj = MEV_NPC_ODC ? (newj ? nl.mdcn[jj] : nl.mdc[jj]) : hypotf(oxj - CXf, oyj - CYf);
             // k's route pieces (bounding boxes), in flight during the pair tests
-            const float4* PB = p.rt.pbox + (size_t)nl.route[kk] * 3;
+            const GF4 PB = gf4(p.rt.pbox + (size_t)nl.route[kk] * 3);
             const float4 pb0 = PB[0], pb1 = PB[1], pb2 = PB[2];
             const NpcPair pr = npc_pair(k, nl.x[kk], nl.y[kk], nl.h[kk], nl.v[kk], nl.c[kk], nl.s[kk], nl.mdc[kk],
                                         jvalid, j, oxj, oyj, ohj, ovj, ocj, osj, odcj);
@@ -976,7 +1010,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // per NPC (7 window points each, first minimum wins).  pre: the window points
     // of the first 8 NPCs, loaded before the plans
     auto load_window = [&](int kk, float2* w) {
-        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
         const int pidx0 = nl.pidx0[kk];
 #pragma unroll
         for (int t = 0; t < 7; ++t) {
@@ -1187,10 +1221,10 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         const int g = e * K + lane;
         npcf(p, NF_X)[g] = nl.x[lane]; npcf(p, NF_Y)[g] = nl.y[lane]; npcf(p, NF_V)[g] = nl.v[lane]; npcf(p, NF_H)[g] = nl.h[lane];
         npcf(p, NF_ACC)[g] = nl.acc[lane]; npcf(p, NF_STEER)[g] = nl.steer[lane]; npci(p, NF_PIDX)[g] = nl.pidx[lane];
-        npci(p, NF_ROUTE)[g] = nl.route[lane]; npci(p, NF_INTENT)[g] = nl.intent[lane]; p.npc.alive[g] = 1;
+        npci(p, NF_ROUTE)[g] = nl.route[lane]; npci(p, NF_INTENT)[g] = nl.intent[lane]; gmem(p.npc.alive)[g] = 1;
         car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
     }
-    if (lane == 0) p.npc.count[e] = newcnt;
+    if (lane == 0) gmem(p.npc.count)[e] = newcnt;
     wave_lds_sync();
 #ifdef MEV_STAMPS_N
     NT(7);  // collisions, erase, store
@@ -1366,7 +1400,7 @@ __device__ __forceinline__ void ego_writeback(const SimParams& p, int e, int NE,
         egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
         if (do_reset) {
             egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
-            egoi(p, EF_INTENT)[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
+            egoi(p, EF_INTENT)[g] = el.intent[i]; gmem(p.ego.alive)[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
         }
     }
 }
@@ -1414,14 +1448,14 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // Every load is issued up front (one round trip); only an env being reset
     // waits a second round for its spawn poses.
     const int ee = PK == 1 ? e : e + (tid < N ? tid : 0) / NE;  // the lane's env (lane = agent slot)
-    const bool pending = p.pending_reset[ee] != 0;
-    const int step_prev = p.step_count[ee];
-    const int npcs_prev = TRAFFIC ? p.npc.count[e] : 0;
+    const bool pending = gmem(p.pending_reset)[ee] != 0;
+    const int step_prev = gmem(p.step_count)[ee];
+    const int npcs_prev = TRAFFIC ? gmem(p.npc.count)[e] : 0;
     const bool do_reset = in.auto_reset && pending;
     const int prev_step = do_reset ? 0 : step_prev;
     const int prev_npcs = TRAFFIC ? (do_reset ? 0 : npcs_prev) : 0;
     if constexpr (FUSED) {
-        for (int b = tid; b < p.R; b += WAVE) el.rel[b] = p.rel_angles[b];
+        for (int b = tid; b < p.R; b += WAVE) el.rel[b] = gmem(p.rel_angles)[b];
     }
     NpcRegs nreg{};
     if constexpr (TRAFFIC) nreg = npc_load(p, e, tid);  // in flight with the ego loads
@@ -1434,17 +1468,17 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         const float pa0 = egof(p, EF_PA0)[g], pa1 = egof(p, EF_PA1)[g];
         const float sx = egof(p, EF_SX)[g], sy = egof(p, EF_SY)[g], sv = egof(p, EF_SV)[g], sh = egof(p, EF_SH)[g];
         const int pidx = egoi(p, EF_PIDX)[g], intent = egoi(p, EF_INTENT)[g];
-        const uint8_t alive = p.ego.alive[g];
+        const uint8_t alive = gmem(p.ego.alive)[g];
         el.a0[i] = a0;
         el.a1[i] = a1;
         if (do_reset) {
             const int rid = reset_route(p, in.rng_counter, ee, PK == 1 ? i : i - (ee - e) * NE, route_l);
-            const float rx = p.rt.spawn[3 * rid], ry = p.rt.spawn[3 * rid + 1], rh = p.rt.spawn[3 * rid + 2];
+            const float rx = gmem(p.rt.spawn)[3 * rid], ry = gmem(p.rt.spawn)[3 * rid + 1], rh = gmem(p.rt.spawn)[3 * rid + 2];
             el.route[i] = rid;
             el.x[i] = rx; el.y[i] = ry; el.v[i] = 0.0f; el.h[i] = rh;
             el.acc[i] = 0.0f; el.steer[i] = 0.0f; el.prev_dist[i] = 0.0f; el.pa0[i] = 0.0f; el.pa1[i] = 0.0f;
             el.sx[i] = rx; el.sy[i] = ry; el.sv[i] = 0.0f; el.sh[i] = rh;
-            el.pidx[i] = 0; el.intent[i] = p.rt.intent[rid]; el.alive[i] = 1;
+            el.pidx[i] = 0; el.intent[i] = gmem(p.rt.intent)[rid]; el.alive[i] = 1;
         } else {
             el.route[i] = route_l;
             el.x[i] = x; el.y[i] = y; el.v[i] = v; el.h[i] = h;
@@ -1455,7 +1489,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         }
     }
     const int step_no = prev_step + 1;  // res.step = ++step_count (:137)
-    // p.step_count[e] = step_no is stored with the other env flags (a store this
+    // gmem(p.step_count)[e] = step_no is stored with the other env flags (a store this
     // early would be drained by the vmcnt waits of every later load)
     wave_lds_sync();
 
@@ -1483,7 +1517,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         const int i = i0 + grp;
         const bool act = i < N;
         const int ii = act ? i : 0;  // idle groups mirror agent 0 so every lane reaches the ballots
-        const float2* P = reinterpret_cast<const float2*>(p.rt.path + (size_t)el.route[ii] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)el.route[ii] * (2 * PATH_LEN));
         const int pidx0 = el.pidx[ii];
         const int start_i = pidx0 < 0 ? 0 : pidx0;
         const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
@@ -1774,8 +1808,8 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     if (!FUSED) {
         for (int i = tid; i < N; i += WAVE) {
             const int g = e * NE + i;
-            p.ob_cand[2 * g] = el.cand[2 * i];
-            p.ob_cand[2 * g + 1] = el.cand[2 * i + 1];
+            gmem(p.ob_cand)[2 * g] = el.cand[2 * i];
+            gmem(p.ob_cand)[2 * g + 1] = el.cand[2 * i + 1];
         }
     }
 
@@ -1863,12 +1897,12 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
                 el.envw[5] = do_reset;
             } else {
                 const int ev = e + (PK > 1 ? tid : 0);
-                p.step_count[ev] = step_e;
+                gmem(p.step_count)[ev] = step_e;
                 out.term[ev] = terminated;
                 out.trunc[ev] = truncated;
                 out.alive_cnt[ev] = alive_cnt;
                 out.step[ev] = step_e;
-                p.pending_reset[ev] = (terminated || truncated) ? 1 : 0;
+                gmem(p.pending_reset)[ev] = (terminated || truncated) ? 1 : 0;
             }
         }
     }
@@ -2039,7 +2073,6 @@ __device__ __forceinline__ T lidar_keep(T v) {
 #ifndef MEV_PROBE_PK
 #define MEV_PROBE_PK 0
 #endif
-typedef float f2v __attribute__((ext_vector_type(2)));
 // beam steps over a provably safe stretch (0 when it is shorter than one step)
 __device__ __forceinline__ int safe_steps(float safe, float stp, float inv_stp) {
     const int j = lidar_keep((int)(safe * inv_stp));
@@ -2203,12 +2236,12 @@ struct LidarSrcHbm {
     static constexpr bool kStaged = false;  // writes the LiDAR block (and dead rows) itself
     static constexpr bool kBoxLds = false;  // boxes come from HBM: cache one per segment in LDS
     const SimParams& p;
-    __device__ float rel(int b) const { return p.rel_angles[b]; }
-    __device__ bool alive(int g) const { return p.ego.alive[g] != 0; }
+    __device__ float rel(int b) const { return gmem(p.rel_angles)[b]; }
+    __device__ bool alive(int g) const { return gmem(p.ego.alive)[g] != 0; }
     __device__ float4 pose(int g) const { return make_float4(egof(p, EF_X)[g], egof(p, EF_Y)[g], egof(p, EF_H)[g], __int_as_float(g)); }
     __device__ void cand(int g, unsigned long long& c0, unsigned long long& c1) const {
-        c0 = p.ob_cand[2 * g];
-        c1 = p.ob_cand[2 * g + 1];
+        c0 = gmem(p.ob_cand)[2 * g];
+        c1 = gmem(p.ob_cand)[2 * g + 1];
     }
     __device__ int4 box(int g, int o) const { return p.ob_box[(size_t)(g / p.N) * p.ob_stride + o]; }
 };
@@ -2282,7 +2315,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     auto probe = [&](float cx_, float cy_, float dx_, float dy_, int k_, float& fx, float& fy) -> int {
         const bool past = k_ >= S;
         const int kc = past ? S - 1 : k_;
-        const float d = TAB ? p.dist_tab[kc] : (float)kc * stp;
+        const float d = TAB ? gmem(p.dist_tab)[kc] : (float)kc * stp;
 #if MEV_PROBE_PK
         // the probe point as one packed multiply and add (v_pk_mul_f32, v_pk_add_f32:
         // the same IEEE roundings as the scalar pair)
@@ -2718,7 +2751,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                     // a runtime table test here, not march_dist<TAB>: measured 4 us per
                     // step faster in k_step, and without it k_lidar's 64-VGPR
                     // allocation spills ~180 registers
-                    const float d = p.dist_tab ? p.dist_tab[kk] : (float)kk * p.lidar_step;
+                    const float d = p.dist_tab ? gmem(p.dist_tab)[kk] : (float)kk * p.lidar_step;
                     const int px = (int)(a.x + dd.x * d), py = (int)(a.y + dd.y * d);
                     if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) {
                         atomicMin(&res[slot], (kk << 1) | 1);
@@ -2834,7 +2867,7 @@ __device__ __forceinline__ void fused_store(const SimParams& p, const Outputs& o
         egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
         if (do_reset) {
             egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
-            egoi(p, EF_INTENT)[g] = el.intent[i]; p.ego.alive[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
+            egoi(p, EF_INTENT)[g] = el.intent[i]; gmem(p.ego.alive)[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
         }
     }
     if (lane == 0) {
@@ -2842,8 +2875,8 @@ __device__ __forceinline__ void fused_store(const SimParams& p, const Outputs& o
         out.trunc[e] = el.envw[1];
         out.alive_cnt[e] = el.envw[2];
         out.step[e] = el.envw[3];
-        p.step_count[e] = el.envw[3];
-        p.pending_reset[e] = el.envw[4];
+        gmem(p.step_count)[e] = el.envw[3];
+        gmem(p.pending_reset)[e] = el.envw[4];
     }
 }
 
@@ -3033,31 +3066,31 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
         if (do_reset) {
             const int rid = reset_route(p, rng_counter, e, i, egoi(p, EF_ROUTE)[g]);
             egoi(p, EF_ROUTE)[g] = rid;
-            egof(p, EF_X)[g] = p.rt.spawn[3 * rid];
-            egof(p, EF_Y)[g] = p.rt.spawn[3 * rid + 1];
+            egof(p, EF_X)[g] = gmem(p.rt.spawn)[3 * rid];
+            egof(p, EF_Y)[g] = gmem(p.rt.spawn)[3 * rid + 1];
             egof(p, EF_V)[g] = 0.0f;
-            egof(p, EF_H)[g] = p.rt.spawn[3 * rid + 2];
+            egof(p, EF_H)[g] = gmem(p.rt.spawn)[3 * rid + 2];
             egof(p, EF_SX)[g] = egof(p, EF_X)[g]; egof(p, EF_SY)[g] = egof(p, EF_Y)[g]; egof(p, EF_SV)[g] = 0.0f; egof(p, EF_SH)[g] = egof(p, EF_H)[g];
             egof(p, EF_ACC)[g] = 0.0f; egof(p, EF_STEER)[g] = 0.0f; egof(p, EF_PREV_DIST)[g] = 0.0f;
             egof(p, EF_PA0)[g] = 0.0f; egof(p, EF_PA1)[g] = 0.0f; egoi(p, EF_PIDX)[g] = 0;
-            egoi(p, EF_INTENT)[g] = p.rt.intent[rid]; p.ego.alive[g] = 1;
+            egoi(p, EF_INTENT)[g] = gmem(p.rt.intent)[rid]; gmem(p.ego.alive)[g] = 1;
         }
         el.x[i] = egof(p, EF_X)[g]; el.y[i] = egof(p, EF_Y)[g]; el.v[i] = egof(p, EF_V)[g]; el.h[i] = egof(p, EF_H)[g];
-        el.alive[i] = p.ego.alive[g]; el.intent[i] = egoi(p, EF_INTENT)[g]; el.pidx[i] = egoi(p, EF_PIDX)[g];
+        el.alive[i] = gmem(p.ego.alive)[g]; el.intent[i] = egoi(p, EF_INTENT)[g]; el.pidx[i] = egoi(p, EF_PIDX)[g];
     }
     int ncnt = 0;
     if (do_reset) {
         if (lane == 0) {
-            p.step_count[e] = 0;
-            p.pending_reset[e] = 0;
-            if (TRAFFIC) p.npc.count[e] = 0;
+            gmem(p.step_count)[e] = 0;
+            gmem(p.pending_reset)[e] = 0;
+            if (TRAFFIC) gmem(p.npc.count)[e] = 0;
         }
     } else if constexpr (TRAFFIC) {
-        ncnt = p.npc.count[e];
+        ncnt = gmem(p.npc.count)[e];
         if (lane < ncnt) {
             const int g = e * p.K + lane;
             nl->x[lane] = npcf(p, NF_X)[g]; nl->y[lane] = npcf(p, NF_Y)[g]; nl->v[lane] = npcf(p, NF_V)[g]; nl->h[lane] = npcf(p, NF_H)[g];
-            nl->intent[lane] = npci(p, NF_INTENT)[g]; nl->alive[lane] = p.npc.alive[g];
+            nl->intent[lane] = npci(p, NF_INTENT)[g]; nl->alive[lane] = gmem(p.npc.alive)[g];
         }
     }
     wave_lds_sync();

@@ -1,4 +1,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-bash tools/ab_sweep.sh cfg3 2 "" probepk probeint1
-bash tools/ab_sweep.sh cfg2 1 "" probepk probeint1
+timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py tests/test_gpu_vs_oracle.py -m gpu -x -q --timeout 180 --timeout-method thread 2>&1 | tail -1
+bash tools/ab_sweep.sh cfg3 2 "" flatold
+bash tools/ab_sweep.sh cfg2 1 "" flatold
+bash tools/ab_sweep.sh cfg4 1 "" flatold
+bash tools/ab_sweep.sh cfg1 1 "" flatold
