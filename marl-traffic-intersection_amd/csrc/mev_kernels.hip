@@ -1375,6 +1375,10 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
     return L;
 }
 
+#ifndef MEV_EARLY_PATH  // measured slower everywhere (VGPRs 101 -> 128 with spills): off
+#define MEV_EARLY_PATH 0
+#endif
+
 // k_step's output strategy: 0 = each part stores its outputs as it produces
 // them (the car part its rows' heads, the LiDAR part its blocks); 1 = staged in
 // LDS and written once at the end as whole coalesced rows (fused_store)
@@ -1459,6 +1463,33 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     }
     NpcRegs nreg{};
     if constexpr (TRAFFIC) nreg = npc_load(p, e, tid);  // in flight with the ego loads
+    // MEV_EARLY_PATH (N <= 8: one pass of phase 1): lane (grp, sub) reads agent grp's
+    // route and path index with the state and issues its path window loads right
+    // away, before the state goes through LDS (phase 1 would otherwise read them
+    // back from LDS first, one more round trip in front of the path loads)
+    const bool early = MEV_EARLY_PATH && N <= 8;
+    float2 ept[8], epend = make_float2(0.0f, 0.0f), epprev = epend, ep10 = epend;
+    int eroute = 0, epidx = 0;
+    if (early) {
+        const int ga = (tid >> 3) < N ? (tid >> 3) : 0;
+        const int eea = PK == 1 ? e : e + ga / NE;
+        eroute = egoi(p, EF_ROUTE)[e * NE + ga];
+        epidx = egoi(p, EF_PIDX)[e * NE + ga];
+        if (in.auto_reset && gmem(p.pending_reset)[eea] != 0) {
+            eroute = reset_route(p, in.rng_counter, eea, PK == 1 ? ga : ga - (eea - e) * NE, eroute);
+            epidx = 0;
+        }
+        const GF2 P = gf2(p.rt.path + (size_t)eroute * (2 * PATH_LEN));
+        const int start_i = epidx < 0 ? 0 : epidx;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int q = start_i + (tid & 7) * 8 + j;
+            ept[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+        }
+        epend = P[PATH_LEN - 1];
+        epprev = P[PATH_LEN - 2];
+        ep10 = P[10];
+    }
     for (int i = tid; i < N; i += WAVE) {
         const int g = e * NE + i;
         const int route_l = egoi(p, EF_ROUTE)[g];
@@ -1517,18 +1548,25 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         const int i = i0 + grp;
         const bool act = i < N;
         const int ii = act ? i : 0;  // idle groups mirror agent 0 so every lane reaches the ballots
-        const GF2 P = gf2(p.rt.path + (size_t)el.route[ii] * (2 * PATH_LEN));
-        const int pidx0 = el.pidx[ii];
+        const GF2 P = gf2(p.rt.path + (size_t)(early ? eroute : el.route[ii]) * (2 * PATH_LEN));
+        const int pidx0 = early ? epidx : el.pidx[ii];
         const int start_i = pidx0 < 0 ? 0 : pidx0;
         const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
         // the 50-point window and the look-ahead target lie in [start_i, start_i + 64): 8 points per lane
         float2 pt[8];
+        float2 pend, pprev, p10;
+        if (early) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int q = start_i + sub * 8 + j;
-            pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+            for (int j = 0; j < 8; ++j) pt[j] = ept[j];
+            pend = epend; pprev = epprev; p10 = ep10;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int q = start_i + sub * 8 + j;
+                pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+            }
+            pend = P[PATH_LEN - 1]; pprev = P[PATH_LEN - 2]; p10 = P[10];
         }
-        const float2 pend = P[PATH_LEN - 1], pprev = P[PATH_LEN - 2], p10 = P[10];
         Kin k{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
         const bool alive = act && el.alive[ii] != 0;
         float cH, sH;

@@ -1,6 +1,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for v in stamps stampsx stampsy; do
-MEV_LIB_VARIANT=$v timeout -k 10 120 python tools/phase_profile.py --envs 256 --agents 1 --step-kernel 2 2>&1 | grep -v amdgpu.ids
-done
-MEV_LIB_VARIANT=stampsr timeout -k 10 120 python tools/simd_balance.py --envs 4096 2>&1 | grep -v amdgpu.ids
+timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread 2>&1 | tail -1
+bash tools/ab_sweep.sh cfg3 1 "" noearlypath
+bash tools/ab_sweep.sh cfg2 1 "" noearlypath
+bash tools/ab_sweep.sh cfg1 1 "" noearlypath
+bash tools/ab_sweep.sh cfg4 1 "" noearlypath
