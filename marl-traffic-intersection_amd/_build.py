@@ -94,7 +94,8 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "npr3": ["-DMEV_LIDAR_NPR=3"],
                # exact variants: k_step's cars_post after the LiDAR (product: before it), at the LiDAR's last
                # issue priority or a fixed one
-               "postlate": ["-DMEV_POST_AFTER_LIDAR=1"],
+               "postlate": ["-DMEV_POST_AFTER_LIDAR=1"], "postlate2": ["-DMEV_POST_AFTER_LIDAR=1", "-DMEV_PRIO_POST=2"],
+               "headprio2": ["-DMEV_PRIO_HEAD=2"], "headprio1": ["-DMEV_PRIO_HEAD=1"],
                # exact variant: k_step's plain block -> env order (product: XCD-aware)
                "noxcd": ["-DMEV_XCD_REMAP=0"],
                "post1": ["-DMEV_POST_AFTER_LIDAR=1", "-DMEV_PRIO_POST=1"],

@@ -3255,6 +3255,7 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         const unsigned lds = (unsigned)FixedLayout<8>::bytes;
         const int pk = step_pack(p);
         const int wg = (p.E + pk - 1) / pk;
+        if constexpr (!MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE)  // (experiment builds: no split)
         if (step_split(p)) {  // two waves per workgroup (<= 4 waves per SIMD)
             if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
