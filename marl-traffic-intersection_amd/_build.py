@@ -81,7 +81,7 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "bfphys0": ["-DMEV_BF_PHYS=0"], "nostraight": ["-DMEV_LIDAR_STRAIGHT=0"],
                "nokeepskip": ["-DMEV_NPC_KEEPSKIP=0"], "solo": ["-DMEV_NPC_SOLO=1"], "nocircle": ["-DMEV_SAT_CIRCLE=0"], "noodc": ["-DMEV_NPC_ODC=0"], "far": ["-DMEV_NPC_FAR=1"], "probeint": ["-DMEV_PROBE_INT=1", "-DMEV_PROBE_PK=1"],
                "probepk": ["-DMEV_PROBE_PK=1"], "probeint1": ["-DMEV_PROBE_INT=1"],
-               "earlypath": ["-DMEV_EARLY_PATH=1"],
+               "earlypath": ["-DMEV_EARLY_PATH=1"], "scanpf": ["-DMEV_NPC_SCANPF=1"],
                "nosplit": ["-DMEV_SPLIT_MAX_WG=0"], "nohelptraf": ["-DMEV_HELP_TRAFFIC=0"],
                "skew1": ["-DMEV_EXP_SKEW=1"], "skew2": ["-DMEV_EXP_SKEW=2"], "skew4": ["-DMEV_EXP_SKEW=4"],
                "skewprio": ["-DMEV_EXP_SKEWPRIO"],

@@ -425,6 +425,9 @@ __device__ inline int wave_argmin_dpp(float d, int i) {
 // terms: pose, speed, cos/sin of its heading, distance to the centre.  The
 // front-car and ghost-scan tests need only these thresholds, so a turn's plan
 // is ballots over j, not reductions.
+#ifndef MEV_NPC_SCANPF  // ghost points of the next scan pass loaded during this one (1.5 % slower: off)
+#define MEV_NPC_SCANPF 0
+#endif
 #ifndef MEV_NPC_FAR  // no exact distance for NPC pairs farther than 130 px (exact, within noise: off)
 #define MEV_NPC_FAR 0
 #endif
@@ -921,25 +924,52 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
 #ifdef MEV_X_NOSCAN
         scan_m = 0;
 #endif
-        while (scan_m) {
+        // the next (up to) four NPCs of scan_m: ks, their count, this lane's NPC
+        auto next_batch = [&](int* ksv, int& nbv) {
+            nbv = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                ksv[u] = scan_m ? __builtin_ctzll(scan_m) : 0;
+                if (scan_m) { scan_m &= scan_m - 1ull; ++nbv; }
+            }
+        };
+        auto lane_npc = [&](const int* ksv) {
+            const int u = lane >> 4;
+            return u == 0 ? ksv[0] : (u == 1 ? ksv[1] : (u == 2 ? ksv[2] : ksv[3]));
+        };
+        // MEV_NPC_SCANPF: the next pass's ghost points are loaded before this pass's
+        // tests (their path loads in flight meanwhile)
+        int ks[4], nb = 0;
+        float2 gpn[8];
+        if (MEV_NPC_SCANPF) {
+            next_batch(ks, nb);
+            if (nb) load_ghost8(lane_npc(ks), gpn);
+        } else if (scan_m) {
+            nb = 1;  // (the loop picks its batch itself)
+        }
+        while (nb) {
 #ifdef MEV_STAMPS_N
             nt_acc[5] += 1;  // scan passes
 #endif
-            int ks[4];
-            int nb = 0;
+            float2 gp[8];
+            if (MEV_NPC_SCANPF) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                ks[u] = scan_m ? __builtin_ctzll(scan_m) : 0;
-                if (scan_m) { scan_m &= scan_m - 1ull; ++nb; }
+                for (int i = 0; i < 8; ++i) gp[i] = gpn[i];
+            } else {
+                next_batch(ks, nb);
+                load_ghost8(lane_npc(ks), gp);
+            }
+            int ks2[4], nb2 = 0;
+            if (MEV_NPC_SCANPF) {
+                next_batch(ks2, nb2);
+                if (nb2) load_ghost8(lane_npc(ks2), gpn);
             }
             const int u = lane >> 4;
-            const int k = u == 0 ? ks[0] : (u == 1 ? ks[1] : (u == 2 ? ks[2] : ks[3]));
+            const int k = lane_npc(ks);
             const bool act = u < nb;
             const int g_start = nl.pidx0[k];
             const int g_end = g_start + 120 < PATH_LEN ? g_start + 120 : PATH_LEN;
             const int q0 = g_start + 8 * (lane & 15);
-            float2 gp[8];
-            load_ghost8(k, gp);
             const float x = nl.x[k], y = nl.y[k];
             const unsigned long long em = act ? nl.em[k] : 0ull, ym = nl.ym[k];
             // per point: some filtered other within SAFE (near), one of them yielded to (near_y)
@@ -1001,6 +1031,13 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                 if (!mixed) nl.mc_a[kq] = mc;
             }
             wave_lds_sync();
+            if (MEV_NPC_SCANPF) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) ks[v] = ks2[v];
+                nb = nb2;
+            } else {
+                nb = scan_m ? 1 : 0;
+            }
         }
         NT(6);  // the ghost scans
     };
