@@ -36,9 +36,9 @@ def _inputs():
 
 
 VARIANTS = {"": [], "stamps": ["-DMEV_STAMPS"]}
-# machine scheduling for instruction-level parallelism over occupancy: k_step's
-# wave count is fixed by the batch (one per env), its registers fit either way
-SCHED = ["-mllvm", "--amdgpu-sched-strategy=max-ilp"]
+# machine scheduling: LLVM's default strategy (max-ilp was +0.7 % in round 1; with the round-2 kernel the
+# default is +0.5 % at config 3, even at config 4: variant sch_maxilp)
+SCHED = []
 # timing-only experiment builds (wrong results by construction; never used by the product)
 EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOCARS"],
                "exp_none": ["-DMEV_EXP_NOROAD", "-DMEV_EXP_NOCARS"], "exp_iters": ["-DMEV_ITERS"],
@@ -56,7 +56,7 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "p2prio0": ["-DMEV_PRIO_P2=0"], "p2prio2": ["-DMEV_PRIO_P2=2"], "p3prio1": ["-DMEV_PRIO_P3=1"],
                "priohbm0": ["-DMEV_PRIO_HBM=0"],  # k_lidar without the LiDAR phases' priorities
                # the compiler's default machine scheduler instead of SCHED (k_step 41.6 -> 41.9 us)
-               "sch_default": [],
+               "sch_maxilp": [], "ilp1": ["-DMEV_PHASE1_ILP=1"],
                # k_cars' NPC-count priorities (product: level = NPCs left / 2): off / per NPC / per 3 NPCs
                # exact variant: the NPC controller's first move pass loads its path windows before the plans
                "npcprewin": ["-DMEV_NPC_PREWIN=1"],
@@ -124,7 +124,7 @@ def build(force: bool = False, verbose: bool = False, variant: str = "") -> str:
     if not force and up_to_date(variant):
         return path
     tmp = path + ".tmp"
-    sched = [] if variant == "sch_default" else SCHED
+    sched = ["-mllvm", "--amdgpu-sched-strategy=max-ilp"] if variant == "sch_maxilp" else SCHED
     cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC", "-shared",
            "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC] + sched + VARIANTS[variant]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
