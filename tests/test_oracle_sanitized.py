@@ -31,9 +31,12 @@ def exe():
     src = os.path.join(ORACLE, "sanitize_replay.c")
     if not os.path.exists(EXE) or os.path.getmtime(EXE) < max(os.path.getmtime(src),
                                                                os.path.getmtime(os.path.join(ORACLE, "marl_oracle.c"))):
+        # per-process temporary + atomic rename: pytest-xdist workers may build it at the same time
+        tmp = f"{EXE}.{os.getpid()}.tmp"
         subprocess.run(["gcc", "-O1", "-g", "-std=c11", "-ffp-contract=off", "-fno-omit-frame-pointer",
-                        "-fsanitize=address,undefined", "-fno-sanitize-recover=all", src, "-o", EXE, "-lm"],
+                        "-fsanitize=address,undefined", "-fno-sanitize-recover=all", src, "-o", tmp, "-lm"],
                        check=True, capture_output=True)
+        os.replace(tmp, EXE)
     return EXE
 
 
