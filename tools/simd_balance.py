@@ -31,17 +31,33 @@ def main():
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--agents", type=int, default=8)
     ap.add_argument("--rays", type=int, default=64)
+    ap.add_argument("--traffic", type=float, default=0.0, help="traffic density (config 4: --agents 1 --traffic 0.5)")
+    ap.add_argument("--warmup", type=int, default=0, help="untimed steps first (traffic reaches steady state)")
     a = ap.parse_args()
     mev = pkgload.load()
-    h = mev.Handle(num_envs=a.envs, num_agents=a.agents, lidar_rays=a.rays, use_team_reward=1)
+    h = mev.Handle(num_envs=a.envs, num_agents=a.agents, lidar_rays=a.rays, use_team_reward=int(a.agents > 1),
+                   traffic_flow=int(a.traffic > 0), traffic_density=a.traffic, max_npcs=32)
     h.set_step_kernel(2)
     rng = np.random.default_rng(0)
     slots, entries, ph, spans, fin, life, simd_sum, simd_max, simd_mean, nw, first_end = [], [], [], [], [], [], [], [], [], Counter(), []
+    by_k = {}
+    for t in range(a.warmup):
+        h.step(rng.uniform(-1, 1, (a.envs, a.agents, 2)).astype(np.float32), auto_reset=True)
     for t in range(a.steps):
+        k_after = None
         h.step(rng.uniform(-1, 1, (a.envs, a.agents, 2)).astype(np.float32), auto_reset=True)
         if t < a.steps // 2:
             continue
+        if a.traffic > 0:
+            k_after = h.get_state()["npc_count"].copy()
         r = h.debug_stamps().astype(np.uint64).reshape(a.envs, 8)
+        if k_after is not None:
+            lt_all = ((r[:, 7] & M40).astype(np.int64) - (r[:, 0] & M40).astype(np.int64)) / 100.0
+            t0_all = (r[:, 0] & M40).astype(np.int64).min()
+            end_all = ((r[:, 7] & M40).astype(np.int64) - t0_all) / 100.0
+            for k in np.unique(k_after):
+                m = k_after == k
+                by_k.setdefault(int(k), []).append(np.stack([lt_all[m], end_all[m]], 1))
         r = r[r[:, 0] != 0]  # packed waves stamp only their first env's slots
         t_in = (r[:, 0] & M40).astype(np.int64)
         t_out = (r[:, 7] & M40).astype(np.int64)
@@ -86,6 +102,12 @@ def main():
     for k in np.unique(S):
         m = S == k
         print(f"    {k:2d}: {m.sum():7d} {E[m].mean():7.2f} {L[m].mean():7.2f} {(E[m] + L[m]).mean():7.2f}")
+    if by_k:
+        print("  by NPCs after the step: envs per step, wave lifetime p50 / p100, wave end p50 / p100 (us)")
+        for k in sorted(by_k):
+            X = np.concatenate(by_k[k])
+            print(f"    {k:2d}: {len(X) / len(spans):8.1f} {np.percentile(X[:, 0], 50):7.2f} {X[:, 0].max():7.2f}"
+                  f" {np.percentile(X[:, 1], 50):7.2f} {X[:, 1].max():7.2f}")
     c = np.corrcoef(simd_sum, fin)[0, 1]
     print(f"  corr(SIMD sum of lifetimes, SIMD finish) = {c:.3f}")
 
