@@ -913,8 +913,8 @@ int mev_get_step_kernel(const mev_handle* h, int32_t* kernel) {
 
 int mev_set_step_pack(mev_handle* h, int32_t envs_per_wave) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
-    if (envs_per_wave != 0 && envs_per_wave != 1 && envs_per_wave != 2 && envs_per_wave != 4)
-        return fail(MEV_E_INVALID, "envs per wave must be 0 (auto), 1, 2 or 4");
+    if (envs_per_wave != 0 && envs_per_wave != 1 && envs_per_wave != 2 && envs_per_wave != 4 && envs_per_wave != 8)
+        return fail(MEV_E_INVALID, "envs per wave must be 0 (auto), 1, 2, 4 or 8");
     HIP_TRY(hipSetDevice(h->cfg.device));
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->sp.step_pack = envs_per_wave;

@@ -3256,7 +3256,7 @@ int step_kernel_for(const SimParams& p) {
 int step_pack(const SimParams& p) {
     if (p.traffic || !fixed_fits<8, 0>(p)) return 1;
     int pk = p.step_pack;
-    if (pk != 1 && pk != 2 && pk != 4) {
+    if (pk != 1 && pk != 2 && pk != 4 && pk != 8) {
         pk = 4;
         while (pk > 1 && p.E / pk < 2048) pk /= 2;
     }
@@ -3294,12 +3294,14 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         const int wg = (p.E + pk - 1) / pk;
         if constexpr (!MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE)  // (experiment builds: no split)
         if (step_split(p)) {  // two waves per workgroup (<= 4 waves per SIMD)
-            if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             return;
         }
-        if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else hipLaunchKernelGGL((k_step<false, TAB, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
     } else {

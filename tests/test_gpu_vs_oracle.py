@@ -138,7 +138,7 @@ def test_random_states_match_oracle(mev, cfg, kernel):
 PACKED = [c for c in CONFIGS if c["n"] <= 4 and not c.get("traffic")]
 
 
-@pytest.mark.parametrize("pack", [2, 4])
+@pytest.mark.parametrize("pack", [2, 4, 8])
 @pytest.mark.parametrize("cfg", PACKED, ids=[c["name"] for c in PACKED])
 def test_random_states_match_oracle_packed_waves(mev, cfg, pack):
     """Several envs per fused k_step wave (mev_set_step_pack), each env from its

@@ -58,7 +58,7 @@ def test_dense_traffic_goldens_cover_sequential_fallback(mev, kernel):
 PACKABLE = [n for n in SINGLE if G.load(n)["meta"]["n_agents"] <= 4 and not G.load(n)["meta"]["traffic"]]
 
 
-@pytest.mark.parametrize("pack", [2, 4])
+@pytest.mark.parametrize("pack", [2, 4, 8])
 @pytest.mark.parametrize("name", PACKABLE)
 def test_golden_scenario_packed_waves(mev, name, pack):
     """Several envs per fused k_step wave (mev_set_step_pack): each golden
@@ -80,7 +80,7 @@ def test_golden_scenario_split_waves(mev, name, split):
     assert rep.ok, f"{name}: {rep.mismatches[:5]} (steps checked {rep.steps})"
 
 
-@pytest.mark.parametrize("pack", [2, 4])
+@pytest.mark.parametrize("pack", [2, 4, 8])
 def test_golden_routes_packed_in_one_handle(mev, pack):
     """The 12 config-2 route scenarios as 12 envs of ONE handle, 2 or 4 envs per
     fused wave: neighbours in a wave hold different states, each env bit-exact."""

@@ -24,7 +24,7 @@ CONFIGS = [
 ]
 
 
-def run(cfg, steps, warmup, step_kernel=0, pack=0):
+def run(cfg, steps, warmup, step_kernel=0, pack=0, split=0):
     import torch
     import pkgload
     mev = pkgload.load()
@@ -37,6 +37,8 @@ def run(cfg, steps, warmup, step_kernel=0, pack=0):
         h.set_step_kernel(step_kernel)
     if pack:
         h.set_step_pack(pack)
+    if split:
+        h.set_step_split(split)
     st = torch.cuda.Stream(dev)
     torch.cuda.set_stream(st)
     h.set_stream(st.cuda_stream)
@@ -76,12 +78,13 @@ def main():
     ap.add_argument("--only", default=None, help="comma-separated config names (e.g. cfg4)")
     ap.add_argument("--step-kernel", type=int, default=0, help="0 auto, 1 k_cars + k_lidar, 2 fused k_step")
     ap.add_argument("--pack", type=int, default=0, help="envs per fused wave: 0 auto, 1, 2, 4")
+    ap.add_argument("--split", type=int, default=0, help="two waves per fused workgroup: 0 auto, 1 off, 2 on")
     a = ap.parse_args()
     res = []
     for cfg in CONFIGS:
         if a.only and cfg["name"] not in a.only.split(","):
             continue
-        r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup, a.step_kernel, a.pack)
+        r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup, a.step_kernel, a.pack, a.split)
         print(json.dumps(r), flush=True)
         res.append(r)
     if a.out:
