@@ -505,7 +505,7 @@ class Handle:
         return v.value
 
     def set_step_pack(self, envs_per_wave: int = 0):
-        """Envs per fused k_step wave: 0 automatic, 1, 2 or 4 (scheduling only; results identical)."""
+        """Envs per fused k_step wave: 0 automatic, 1, 2, 4 or 8 (scheduling only; results identical)."""
         _check(self._lib.mev_set_step_pack(self._h, int(envs_per_wave)))
 
     def step_pack(self) -> int:
