@@ -102,6 +102,9 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "post3": ["-DMEV_POST_AFTER_LIDAR=1", "-DMEV_PRIO_POST=3"],
                # exact variant: k_step stages every output in LDS and writes whole rows at the end
                "staged": ["-DMEV_FUSED_STAGED=1"],
+               # exact variant: the leading kernel arguments preloaded into SGPRs at wave launch (no kernarg
+               # s_load round trip in front of the parameter loads)
+               "kpreload": ["-mllvm", "-amdgpu-kernarg-preload-count=16"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
                "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 VARIANTS.update(EXPERIMENTS)
