@@ -205,7 +205,8 @@ def dry_run(args):
     if os.environ.get("MEV_DRYRUN_FAIL_RANK") == str(rank):
         sys.exit(3)  # test hook: a rank that dies before the rendezvous (the launcher must stop the rest)
     if world > 1:
-        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
+        with stdout_to_stderr():
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=60))
         store = dist.distributed_c10d._get_default_store()
         if rank == 0:
             store.set("mev_comm_id", bytes(range(128)))  # stands in for mev_comm_unique_id()
@@ -256,6 +257,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MEV_BENCH_SHARE_DEVICE") == "1":
+        # rehearsal of the N-rank path on fewer GPUs (ranks share devices round-robin); never the
+        # default: on a node with N GPUs every rank owns its own device
+        local_rank %= max(1, torch.cuda.device_count())
     dist = None
     torch.cuda.set_device(local_rank)
     if world > 1:
@@ -263,7 +268,9 @@ def main():
         # data-path collective is the library's own RCCL gather (mev_comm_init)
         import datetime
         import torch.distributed as dist
-        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(60.0, args.gather_timeout + 60.0)))
+        with stdout_to_stderr():  # gloo's C++ "connected to N peer ranks" banner: stdout carries only the line
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(60.0, args.gather_timeout + 60.0)))
+            dist.barrier()
     dev = torch.device("cuda", local_rank)
     E, N, D = args.envs, N_AGENTS, OBS_DIM
     K, W = args.steps, args.warmup

@@ -26,6 +26,7 @@ def test_launcher_spawns_n_ranks(n):
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout  # ONE line, from rank 0
+    assert r.stdout.strip() == lines[0], r.stdout  # and nothing else (gloo's banner goes to stderr)
     d = json.loads(lines[0])
     assert d["dry_run"] and d["n_gpus"] == n and d["max_over_ranks"] == float(n)
     assert d["steps"] == 3 and d["warmup"] == 1
