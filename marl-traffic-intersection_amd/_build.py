@@ -105,6 +105,11 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # exact variant: the leading kernel arguments preloaded into SGPRs at wave launch (no kernarg
                # s_load round trip in front of the parameter loads)
                "kpreload": ["-mllvm", "-amdgpu-kernarg-preload-count=16"],
+               # machine-scheduler options (exact): AMDGPU register-pressure trackers, no unclustered
+               # high-pressure reschedule stage, latency over occupancy
+               "trk": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+               "nounclust": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule=1"],
+               "bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
                "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 VARIANTS.update(EXPERIMENTS)
