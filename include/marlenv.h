@@ -174,7 +174,11 @@ int mev_get_outputs(mev_handle* h, float* obs, float* reward, uint8_t* done, uin
 int mev_get_state(mev_handle* h, const mev_state* out);
 int mev_set_state(mev_handle* h, const mev_state* in);
 
-/* Device pointers of the handle's internal output buffers (zero-copy consumers). */
+/* Device pointers of the handle's internal output buffers (zero-copy consumers),
+ * holding the last step's / reset's outputs: a step that wrote elsewhere (caller
+ * buffers, the pinned block of a small host-mode step, a packed gather row) is
+ * first copied into them on the handle's stream.  Device-mode steps without
+ * output pointers write them in place. */
 int mev_device_outputs(mev_handle* h, float** obs, float** reward, uint8_t** done, uint8_t** status,
                        uint8_t** terminated, uint8_t** truncated);
 
@@ -318,10 +322,12 @@ typedef struct mev_dl_managed {
 enum { MEV_OUT_OBS = 0, MEV_OUT_REWARD, MEV_OUT_DONE, MEV_OUT_STATUS, MEV_OUT_TERMINATED, MEV_OUT_TRUNCATED,
        MEV_OUT_AGENTS_ALIVE, MEV_OUT_STEP, MEV_OUT_GATHERED /* root: [world][bytes] u8 of the last gather */,
        MEV_OUT_COUNT };
-/* The handle's internal output buffer `which` (what steps without output
- * pointers write, and what mev_device_outputs returns) as a DLPack tensor:
+/* The handle's internal output buffer `which` (what mev_device_outputs returns,
+ * brought up to the last outputs the same way) as a DLPack tensor:
  * obs [E][N][D] f32, reward [E][N] f32, done/status [E][N] u8,
- * terminated/truncated [E] u8, agents_alive/step [E] i32. */
+ * terminated/truncated [E] u8, agents_alive/step [E] i32.  MEV_OUT_GATHERED
+ * (root): the last gather's buffer; the handle's stream is made to wait for its
+ * RCCL receives, as mev_gather_result does. */
 int mev_output_dlpack(mev_handle* h, int32_t which, mev_dl_managed** out);
 
 #ifdef __cplusplus

@@ -101,7 +101,7 @@ def load_library(variant: str = None):
         return _libs[variant]
     path = _build.lib_path(variant)
     _one_runtime()
-    if not _build.up_to_date(variant):
+    if not _build.up_to_date(variant) and variant in _build.VARIANTS:  # experiments: tools/variants.py builds them
         try:
             _build.build(variant=variant)
         except Exception as exc:  # no hipcc on this machine: use a prebuilt library if it is there
@@ -183,6 +183,41 @@ def _check(rc: int):
 
 
 _OUT_KEYS = ("obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step")
+
+
+class _DLTensor(ctypes.Structure):  # mev_dl_tensor (include/marlenv.h), DLPack's DLTensor
+    _fields_ = [("data", ctypes.c_void_p), ("device_type", ctypes.c_int32), ("device_id", ctypes.c_int32),
+                ("ndim", ctypes.c_int32), ("dtype_code", ctypes.c_uint8), ("dtype_bits", ctypes.c_uint8),
+                ("dtype_lanes", ctypes.c_uint16), ("shape", ctypes.c_void_p), ("strides", ctypes.c_void_p),
+                ("byte_offset", ctypes.c_uint64)]
+
+
+_DL_DELETER = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+
+class _DLManaged(ctypes.Structure):  # mev_dl_managed, DLPack's DLManagedTensor
+    _fields_ = [("dl_tensor", _DLTensor), ("manager_ctx", ctypes.c_void_p), ("deleter", ctypes.c_void_p)]
+
+
+_DLTENSOR = b"dltensor"
+
+
+@ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+def _capsule_destructor(capsule):
+    """PyCapsule destructor: a capsule still named "dltensor" was never consumed (a consumer renames
+    it "used_dltensor" and takes over the deleter), so call the managed tensor's deleter."""
+    api = ctypes.pythonapi
+    api.PyCapsule_IsValid.restype = ctypes.c_int
+    api.PyCapsule_IsValid.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    if not api.PyCapsule_IsValid(capsule, _DLTENSOR):
+        return
+    api.PyCapsule_GetPointer.restype = ctypes.c_void_p
+    api.PyCapsule_GetPointer.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    ptr = api.PyCapsule_GetPointer(capsule, _DLTENSOR)
+    if ptr:
+        m = _DLManaged.from_address(ptr)
+        if m.deleter:
+            _DL_DELETER(m.deleter)(ptr)
 
 
 def _ptr(a) -> Optional[int]:
@@ -417,13 +452,14 @@ class Handle:
     # -- zero-copy export (DLPack) ----------------------------------------
     def output_dlpack(self, which: str):
         """PyCapsule ("dltensor") viewing the handle's internal output buffer `which` (DLPACK_OUTPUTS);
-        valid while the handle lives; torch.from_dlpack() consumes it."""
+        valid while the handle lives; torch.from_dlpack() consumes it.  A capsule dropped unconsumed
+        frees its descriptor through the capsule destructor (DLPack's producer contract)."""
         m = _vp()
         _check(self._lib.mev_output_dlpack(self._h, DLPACK_OUTPUTS.index(which), ctypes.byref(m)))
         new = ctypes.pythonapi.PyCapsule_New
         new.restype = ctypes.py_object
         new.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]
-        return new(m.value, b"dltensor", None)
+        return new(m.value, _DLTENSOR, ctypes.cast(_capsule_destructor, ctypes.c_void_p))
 
     def output_tensors(self, names=("obs", "reward", "done", "status", "terminated", "truncated",
                                     "agents_alive", "step")):

@@ -845,9 +845,34 @@ int mev_set_state(mev_handle* h, const mev_state* s) {
     return MEV_OK;
 }
 
+// The handle's own output buffers made to hold the last outputs: a step that wrote
+// elsewhere (caller buffers, the pinned host block of a host-mode step, a packed
+// gather row) is copied in, stream-ordered, and h->last points back at them.
+static int sync_internal(mev_handle* h) {
+    const size_t E = size_t(h->cfg.num_envs), EN = E * size_t(h->cfg.num_agents);
+    const mev::Outputs& L = h->last;
+    const mev::Outputs& I = h->internal;
+    auto pull = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+        if (!src || src == dst) return hipSuccess;
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, h->stream);
+    };
+    HIP_TRY(pull(I.obs, L.obs, EN * size_t(h->D) * sizeof(float)));
+    HIP_TRY(pull(I.rew, L.rew, EN * sizeof(float)));
+    HIP_TRY(pull(I.done, L.done, EN));
+    HIP_TRY(pull(I.status, L.status, EN));
+    HIP_TRY(pull(I.term, L.term, E));
+    HIP_TRY(pull(I.trunc, L.trunc, E));
+    HIP_TRY(pull(I.alive_cnt, L.alive_cnt, E * sizeof(int32_t)));
+    HIP_TRY(pull(I.step, L.step, E * sizeof(int32_t)));
+    h->last = h->internal;
+    return MEV_OK;
+}
+
 int mev_device_outputs(mev_handle* h, float** obs, float** rew, uint8_t** done, uint8_t** status, uint8_t** term,
                        uint8_t** trunc) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r = sync_internal(h)) return r;
     if (obs) *obs = h->internal.obs;
     if (rew) *rew = h->internal.rew;
     if (done) *done = h->internal.done;
@@ -1061,24 +1086,8 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
     }
     // the live outputs are restored into the handle's own buffers; envs a masked
     // restore leaves alone keep their current outputs, so bring those in first
-    {
-        const size_t EN = E * size_t(h->cfg.num_agents);
-        auto pull = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-            if (!src || src == dst) return hipSuccess;
-            return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, h->stream);
-        };
-        const mev::Outputs& L = h->last;
-        mev::Outputs& I = h->internal;
-        if (env_mask) {
-            HIP_TRY(pull(I.obs, L.obs, EN * size_t(h->D) * sizeof(float)));
-            HIP_TRY(pull(I.rew, L.rew, EN * sizeof(float)));
-            HIP_TRY(pull(I.done, L.done, EN));
-            HIP_TRY(pull(I.status, L.status, EN));
-            HIP_TRY(pull(I.term, L.term, E));
-            HIP_TRY(pull(I.trunc, L.trunc, E));
-            HIP_TRY(pull(I.alive_cnt, L.alive_cnt, E * sizeof(int32_t)));
-            HIP_TRY(pull(I.step, L.step, E * sizeof(int32_t)));
-        }
+    if (env_mask) {
+        if (int r = sync_internal(h)) return r;
     }
     h->last = h->internal;
     const std::vector<SnapField> f = snap_fields(h);
@@ -1204,6 +1213,16 @@ int mev_gather_result(mev_handle* h, void** stacked, uint64_t* bytes_per_rank, i
     return MEV_OK;
 }
 
+// A failed or stuck gather: abort the communicator (its kernels exit), then
+// release the gather resources as free_comm does, without ncclCommDestroy; the
+// outputs of later queries come from the handle's own buffers again.
+static void abort_comm(mev_handle* h) {
+    (void)ncclCommAbort(h->comm);
+    h->comm = nullptr;
+    if (h->last.obs != h->internal.obs) h->last = h->internal;  // h->last pointed into a packed row
+    h->free_comm();
+}
+
 int mev_gather_wait(mev_handle* h, int32_t timeout_ms) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (!h->comm) return fail(MEV_E_INVALID, "no communicator (mev_comm_init)");
@@ -1217,14 +1236,12 @@ int mev_gather_wait(mev_handle* h, int32_t timeout_ms) {
             if (q != hipErrorNotReady) return fail(MEV_E_HIP, std::string("gather: ") + hipGetErrorString(q));
             ncclResult_t ae = ncclSuccess;
             if (ncclCommGetAsyncError(h->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
-                (void)ncclCommAbort(h->comm);
-                h->comm = nullptr;
+                abort_comm(h);
                 return fail(MEV_E_HIP, std::string("RCCL gather failed: ") + ncclGetErrorString(ae));
             }
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             if (timeout_ms > 0 && ms > double(timeout_ms)) {
-                (void)ncclCommAbort(h->comm);  // a lost peer must not hang the caller
-                h->comm = nullptr;
+                abort_comm(h);  // a lost peer must not hang the caller
                 return fail(MEV_E_HIP, "RCCL gather timed out (communicator aborted)");
             }
             std::this_thread::sleep_for(std::chrono::microseconds(50));
@@ -1250,6 +1267,10 @@ int mev_output_dlpack(mev_handle* h, int32_t which, mev_dl_managed** out) {
     int nd = 1;
     int64_t sh[3] = {E, 0, 0};
     mev_dl_dtype dt{1, 8, 1};  // u8
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (which != MEV_OUT_GATHERED) {
+        if (int r = sync_internal(h)) return r;
+    }
     const mev::Outputs& I = h->internal;
     switch (which) {
         case MEV_OUT_OBS: data = I.obs; nd = 3; sh[1] = N; sh[2] = D; dt = {2, 32, 1}; break;
@@ -1262,7 +1283,12 @@ int mev_output_dlpack(mev_handle* h, int32_t which, mev_dl_managed** out) {
         case MEV_OUT_STEP: data = I.step; dt = {0, 32, 1}; break;
         case MEV_OUT_GATHERED:
             if (!h->comm || h->rank != h->root) return fail(MEV_E_INVALID, "the gather buffer lives on the root rank");
-            data = h->pk_buf[h->gathers > 0 ? int((h->gathers - 1) & 1) : 0];
+            {
+                const int b = h->gathers > 0 ? int((h->gathers - 1) & 1) : 0;
+                // as mev_gather_result: the handle's stream waits for the RCCL receives into it
+                if (h->gather_pending[b]) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gather[b], 0));
+                data = h->pk_buf[b];
+            }
             nd = 2; sh[0] = h->world; sh[1] = int64_t(h->pk_bytes);
             break;
         default: return fail(MEV_E_INVALID, "unknown output");

@@ -25,7 +25,7 @@ def state_from_records(f, i, routes):
 def make_oracle(meta):
     R = int(meta["rays"])
     return O.OracleEnv(num_lanes=int(meta["num_lanes"]), n_agents=int(meta["n_agents"]), rays=R,
-                       obs_dim=127 if R <= 96 else 31 + R, use_team=bool(meta["use_team"]),
+                       obs_dim=int(meta.get("obs_dim", 127 if R <= 96 else 31 + R)), use_team=bool(meta["use_team"]),
                        respawn=bool(meta["respawn"]), max_steps=int(meta["max_steps"]), traffic=bool(meta["traffic"]),
                        density=float(meta["density"]), reward=meta["reward"], max_npcs=64)
 
@@ -68,3 +68,54 @@ def replay(name):
             break
     env.close()
     return errs
+
+
+EGO_FIELDS = {"x": "x", "y": "y", "v": "v", "h": "heading", "acc": "acc", "steer": "steering", "sx": "spawn_x",
+              "sy": "spawn_y", "sv": "spawn_v", "sh": "spawn_heading", "prev_dist": "prev_dist", "pa0": "prev_a0",
+              "pa1": "prev_a1", "path_index": "path_index", "route": "route", "intention": "intention",
+              "alive": "alive"}
+NPC_FIELDS = {"x": "npc_x", "y": "npc_y", "v": "npc_v", "h": "npc_heading", "acc": "npc_acc",
+              "steer": "npc_steering", "path_index": "npc_path_index", "route": "npc_route",
+              "intention": "npc_intention", "alive": "npc_alive"}
+
+
+def oracle_from_device_state(meta, st, e, traffic_routes=None):
+    """An oracle env holding env e of a device handle's state (mev_get_state arrays, every hidden
+    Car field included): the reference's IntersectionEnv with its cars / traffic_cars / step_count
+    set to the same values (cpp/IntersectionEnv.cpp:394-416, set_state)."""
+    o = make_oracle(meta)
+    if traffic_routes is not None:
+        o.set_traffic_routes([int(r) for r in traffic_routes])
+    n = int(meta["n_agents"])
+    cars = np.zeros(n, O.CAR_DTYPE)
+    for a, b in EGO_FIELDS.items():
+        cars[a] = st[b][e]
+    k = int(st["npc_count"][e])
+    npcs = np.zeros(k, O.CAR_DTYPE)
+    for a, b in NPC_FIELDS.items():
+        npcs[a] = st[b][e, :k]
+    o.set_state(cars, npcs, int(st["step_count"][e]))
+    return o
+
+
+def check_step(tag, out, e, r):
+    """Every output of env e of a device step (numpy dict) equals the oracle's step result r, bit for bit."""
+    assert G.bits_equal(out["obs"][e], r["obs"]), tag + ": obs"
+    assert G.bits_equal(out["reward"][e], r["rew"]), tag + ": reward"
+    assert G.bits_equal(out["status"][e], r["status"]) and G.bits_equal(out["done"][e], r["done"]), tag + ": status"
+    got = [int(out["terminated"][e]), int(out["truncated"][e]), int(out["agents_alive"][e]), int(out["step"][e])]
+    assert got == [r["terminated"], r["truncated"], r["agents_alive"], r["step"]], tag + ": flags"
+
+
+def check_state(tag, gst, e, o):
+    """The full ego / NPC state of env e (mev_get_state arrays) equals the oracle's, bit for bit."""
+    egos, npcs, sc = o.get_state()
+    for a, b in EGO_FIELDS.items():
+        if a in egos.dtype.names:
+            assert G.bits_equal(gst[b][e], egos[a]), f"{tag}: ego {a}"
+    assert int(gst["npc_count"][e]) == len(npcs), tag + ": npc count"
+    k = len(npcs)
+    for a, b in NPC_FIELDS.items():
+        if k and a in npcs.dtype.names:
+            assert G.bits_equal(gst[b][e, :k], npcs[a]), f"{tag}: npc {a}"
+    assert int(gst["step_count"][e]) == int(sc), tag + ": step_count"

@@ -126,3 +126,41 @@ def test_gather_two_ranks_on_one_device():
     if "SKIP" in r.stdout:
         pytest.skip(r.stdout.strip().splitlines()[-1])
     assert r.returncode == 0 and "GATHER OK" in r.stdout, out[-3000:]
+
+
+def test_output_views_follow_host_and_gather_steps(mev):
+    """mev_device_outputs / DLPack views hold the LAST outputs whichever buffers the step
+    wrote: a small handle's host-mode step (pinned zero-copy block), a device step into
+    caller buffers, and a packed gather row are each copied into the internal buffers
+    before the views are handed out."""
+    import torch
+    from marl_traffic_intersection_amd import _capi
+
+    E, N, R = 16, 3, 32
+    h = mev.Handle(num_envs=E, num_agents=N, lidar_rays=R, use_team_reward=1, device=0)
+    try:
+        torch.cuda.set_device(0)
+        h.set_stream(torch.cuda.current_stream().cuda_stream)
+        rng = np.random.default_rng(9)
+        for _ in range(4):  # host mode: the pinned block (outputs <= 256 KB)
+            host = h.step(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32), auto_reset=True)
+        t = h.output_tensors()
+        torch.cuda.synchronize()
+        for k, v in host.items():
+            assert np.array_equal(_bits(t[k].cpu().numpy()), _bits(v)), k
+        mine = {k: torch.zeros_like(torch.as_tensor(v), device="cuda:0") for k, v in h.alloc_outputs().items()}
+        h.step(torch.rand((E, N, 2), device="cuda:0") * 2 - 1, out=mine, device=True)  # caller buffers
+        t = h.output_tensors()
+        torch.cuda.synchronize()
+        for k in mine:
+            assert torch.equal(t[k], mine[k]), k
+        h.comm_init(_capi.comm_unique_id(), world=1, rank=0, root=0)
+        h.step(torch.rand((E, N, 2), device="cuda:0") * 2 - 1, device=True, gather=True)  # packed row
+        last = h.get_outputs()
+        t = h.output_tensors(("obs", "reward", "done", "status", "terminated", "truncated"))
+        torch.cuda.synchronize()
+        for k, v in t.items():
+            assert np.array_equal(_bits(v.cpu().numpy()), _bits(last[k])), k
+        h.comm_destroy()
+    finally:
+        h.close()

@@ -159,3 +159,106 @@ def test_vec_env_snapshot_restore_outputs(mev):
     torch.cuda.synchronize()
     assert torch.equal(obs, obs_snap)
     v.close()
+
+
+# ---- restores pinned to the oracle (reference IntersectionEnv::get_state / set_state,
+# cpp/IntersectionEnv.cpp:394-416, EnvState.h:9-15: a snapshot "for fast MCTS rollbacks").
+# At snapshot time an oracle env is built from each env's full device state; after the
+# device restores the snapshot (whole, or masked), its envs are stepped beside those
+# oracles, bit for bit -- so a restore is checked against what the reference computes from
+# the snapshotted state, not only against the handle's own earlier trajectory.
+import oracle_replay as OR  # noqa: E402
+from conftest import STEP_KERNELS, use_step_kernel  # noqa: E402
+
+ROUTES3 = [(1, 4), (2, 8), (3, 12), (4, 7), (5, 11), (6, 3), (7, 10), (8, 2), (9, 6), (10, 1), (11, 5), (12, 9)]
+
+
+def _meta(n, rays, traffic=False, density=0.5, max_steps=2000, team=True):
+    return dict(rays=rays, obs_dim=31 + rays, num_lanes=3, n_agents=n, use_team=team, respawn=True, max_steps=max_steps,
+                traffic=traffic, density=density, reward=[10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2])
+
+
+def _ended(out):
+    return (out["terminated"] != 0) | (out["truncated"] != 0)
+
+
+def _step_beside(h, oracles, ended, rng, steps, n, troutes=None, spawn_p=0.0):
+    """Step h (auto-reset on) and every env's oracle; compare each output and, at the end, the state."""
+    E = h.E
+    st = h.get_state()
+    for t in range(steps):
+        a = rng.uniform(-1, 1, (E, n, 2)).astype(np.float32)
+        spawn = None
+        if troutes is not None:
+            spawn = np.where(rng.uniform(size=E) < spawn_p, rng.integers(0, len(troutes), E), -1).astype(np.int32)
+        out = h.step(a, auto_reset=True, spawn_route=spawn)
+        for e in range(E):
+            o = oracles[e]
+            if ended[e]:  # auto-reset before the step: reset() then step()
+                o.reset([int(r) for r in st["route"][e]])
+            r = o.step(a[e], 1.0 / 60.0, int(spawn[e]) if spawn is not None else -1)
+            OR.check_step(f"env {e} step {t + 1} after restore", out, e, r)
+            ended[e] = bool(r["terminated"] or r["truncated"])
+        st = h.get_state()
+    for e in range(E):
+        OR.check_state(f"env {e} end", st, e, oracles[e])
+
+
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
+@pytest.mark.parametrize("masked", [False, True])
+def test_restore_then_step_matches_oracle_from_snapshot(mev, kernel, masked):
+    En, n, rays = 48, 8, 64
+    meta = _meta(n, rays, max_steps=70)
+    h = mev.Handle(num_envs=En, num_agents=n, lidar_rays=rays, use_team_reward=1, max_steps=70)
+    use_step_kernel(mev, h, kernel)
+    rng = np.random.default_rng(40 + kernel + 2 * masked)
+    for a in _acts(rng, 45, e=En, n=n):
+        last = h.step(a, auto_reset=True)
+    snap = h.snapshot()
+    st_snap = h.get_state()
+    obs_snap = h.observations()
+    ended_snap = _ended(last)
+    snap_oracles = [OR.oracle_from_device_state(meta, st_snap, e) for e in range(En)]
+    for a in _acts(rng, 20, e=En, n=n):  # move on past the snapshot
+        last = h.step(a, auto_reset=True)
+    if masked:
+        mask = (rng.uniform(size=En) < 0.5).astype(np.uint8)
+        st_now = h.get_state()
+        ended_now = _ended(last)
+        h.restore(snap, env_mask=mask)
+        oracles = [snap_oracles[e] if mask[e] else OR.oracle_from_device_state(meta, st_now, e) for e in range(En)]
+        ended = [bool(ended_snap[e] if mask[e] else ended_now[e]) for e in range(En)]
+    else:
+        h.restore(snap)
+        oracles = snap_oracles
+        ended = [bool(x) for x in ended_snap]
+    obs = h.observations()
+    for e in range(En):  # a restored env's observation is the snapshot's
+        if not masked or mask[e]:
+            assert np.array_equal(obs[e].view(np.uint32), obs_snap[e].view(np.uint32)), e
+    _step_beside(h, oracles, ended, rng, 40, n)
+    h.close()
+
+
+@pytest.mark.parametrize("kernel", STEP_KERNELS)
+def test_traffic_restore_with_spawn_replay_matches_oracle(mev, kernel):
+    En, rays = 32, 64
+    meta = _meta(1, rays, traffic=True, density=3.0, team=False)
+    h = mev.Handle(num_envs=En, num_agents=1, lidar_rays=rays, traffic_flow=1, traffic_density=3.0, max_npcs=32)
+    use_step_kernel(mev, h, kernel)
+    troutes = [h.route_id(s - 1, 12 + t - 1) for s, t in ROUTES3]
+    h.set_traffic_routes(troutes)
+    rng = np.random.default_rng(77 + kernel)
+    for a in _acts(rng, 60, e=En, n=1):  # Philox spawns fill the envs with NPCs
+        last = h.step(a, auto_reset=True)
+    snap = h.snapshot()
+    st_snap = h.get_state()
+    assert st_snap["npc_count"].sum() > 0
+    oracles = [OR.oracle_from_device_state(meta, st_snap, e, troutes) for e in range(En)]
+    ended = [bool(x) for x in _ended(last)]
+    for a in _acts(rng, 25, e=En, n=1):
+        h.step(a, auto_reset=True)
+    h.restore(snap)
+    # spawns replayed through mev_step_args.spawn_route (the reference's spawn RNG is unseeded)
+    _step_beside(h, oracles, ended, rng, 40, 1, troutes=troutes, spawn_p=0.2)
+    h.close()
