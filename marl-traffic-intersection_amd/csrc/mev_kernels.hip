@@ -152,6 +152,14 @@ __device__ inline __attribute__((address_space(1))) float* egof(const SimParams&
 __device__ inline __attribute__((address_space(1))) int32_t* egoi(const SimParams& p, int k) {
     return gmem(reinterpret_cast<int32_t*>(p.ego.x + p.ego.stride * k));
 }
+// Element i of a global array addressed as base + 32-bit unsigned byte offset: the
+// global_load saddr form (wave-uniform base in SGPRs, one offset VGPR shared by all
+// the fields of an agent) instead of a 64-bit VGPR address per load.
+template <class T>
+__device__ __forceinline__ T ldu(const __attribute__((address_space(1))) T* base, uint32_t i) {
+    typedef const __attribute__((address_space(1))) char gchar;
+    return *(const __attribute__((address_space(1))) T*)((gchar*)base + i * (uint32_t)sizeof(T));
+}
 __device__ inline __attribute__((address_space(1))) float* npcf(const SimParams& p, int k) {
     return gmem(p.npc.x + p.npc.stride * k);
 }
@@ -184,6 +192,13 @@ __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The same for LDS written by this wave's own ds_write instructions only (not by
+// LDS DMA): one wave's LDS operations are processed in order, so a compiler
+// barrier that keeps the reads after the writes is enough.
+__device__ inline void wave_lds_order() {
+    __builtin_amdgcn_wave_barrier();
 }
 
 // Inclusive add / max scans over the 64 lanes with DPP row shifts and row
@@ -1352,6 +1367,11 @@ __device__ void write_obs_head(const SimParams& p, int i, const EL& el, const NL
 #endif
 
 // Dynamic LDS of k_cars, carved for the handle's N egos and K NPC slots.
+// s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maximum)
+constexpr int kWaitVmcnt0 = 0x0F70;
+// LDS path windows of the car part's first pass (k_step, no traffic): 4 x 1 KB + 1 KB
+constexpr int kWinBytes = 5 * 1024;
+
 struct CarsLDS {
     float *x, *y, *v, *h, *c, *s, *acc, *steer, *prev_dist, *pa0, *pa1;
     float *sx, *sy, *sv, *sh, *rew, *a0, *a1, *tgx, *tgy, *t10x, *t10y;
@@ -1369,6 +1389,9 @@ struct CarsLDS {
     float* head;
     float* rel;
     int32_t* envw;
+    // k_step without traffic (null otherwise): 5 KB for the LDS path windows of the car
+    // part's first pass, inside the LiDAR pool's region (free until the LiDAR runs)
+    float4* win;
 };
 
 __host__ __device__ constexpr size_t lds_al(size_t b) { return (b + 15) & ~size_t(15); }
@@ -1409,11 +1432,15 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
     L.head = nullptr;
     L.rel = nullptr;
     L.envw = nullptr;
+    L.win = nullptr;
     return L;
 }
 
-#ifndef MEV_EARLY_PATH  // measured slower everywhere (VGPRs 101 -> 128 with spills): off
-#define MEV_EARLY_PATH 0
+
+// phase 1's first path windows loaded from group-layout route / index registers
+// right after the state round (1), or after the state went through LDS (0)
+#ifndef MEV_EARLY_WINDOW
+#define MEV_EARLY_WINDOW 1
 #endif
 
 // k_step's output strategy: 0 = each part stores its outputs as it produces
@@ -1462,7 +1489,7 @@ struct CarsCtx {
 // instead of delaying this wave's.  FUSED: the LiDAR runs in the same wave
 // (k_step) and reads the obstacle table and candidate masks from LDS, so they
 // are not published to HBM.
-template <bool TRAFFIC, bool FUSED, class NL, int PK = 1>
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
                                             const CarsLDS& el, NL* nl) {
     static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
@@ -1486,80 +1513,150 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // ---- phase 0: ego state -> LDS (lane = agent).  An env whose previous
     // step ended starts from its spawns (vector auto-reset; reset +
     // add_car_with_route, :66-131).
-    // Every load is issued up front (one round trip); only an env being reset
-    // waits a second round for its spawn poses.
+    // Round A: every load the car part needs before its path window -- the env
+    // flags, the actions, every state field, the LiDAR beam offsets and (first
+    // pass of phase 1) each lane group's route and path index -- is issued back to
+    // back and unconditionally (no load waits behind a branch on another load's
+    // value); only an env being reset waits a second round for its spawn poses.
+    // Then the path windows of phase 1's first pass are issued straight from the
+    // group-layout route / index registers (round B), while the state goes
+    // through LDS.  (Before: the flags, the actions, the state and the path window
+    // were four dependent rounds.)
     const int ee = PK == 1 ? e : e + (tid < N ? tid : 0) / NE;  // the lane's env (lane = agent slot)
-    const bool pending = gmem(p.pending_reset)[ee] != 0;
-    const int step_prev = gmem(p.step_count)[ee];
+    const bool lane_on = tid < N;  // N <= 64: one agent slot per lane
+    const int il = lane_on ? tid : 0;
+    const int gl = e * NE + il;
+    const uint32_t ug = (uint32_t)gl;
+    const uint8_t pending_b = ldu(gmem(p.pending_reset), (uint32_t)ee);
+    const int step_prev = ldu(gmem(p.step_count), (uint32_t)ee);
     const int npcs_prev = TRAFFIC ? gmem(p.npc.count)[e] : 0;
-    const bool do_reset = in.auto_reset && pending;
-    const int prev_step = do_reset ? 0 : step_prev;
-    const int prev_npcs = TRAFFIC ? (do_reset ? 0 : npcs_prev) : 0;
-    if constexpr (FUSED) {
-        for (int b = tid; b < p.R; b += WAVE) el.rel[b] = gmem(p.rel_angles)[b];
+    const float a0 = ldu(gmem(in.actions), 2 * ug), a1 = ldu(gmem(in.actions), 2 * ug + 1);
+    const int route_l = ldu(egoi(p, EF_ROUTE), ug);
+    const float x0 = ldu(egof(p, EF_X), ug), y0 = ldu(egof(p, EF_Y), ug), v0 = ldu(egof(p, EF_V), ug);
+    const float h0 = ldu(egof(p, EF_H), ug), acc0 = ldu(egof(p, EF_ACC), ug), steer0 = ldu(egof(p, EF_STEER), ug);
+    const float pd0 = ldu(egof(p, EF_PREV_DIST), ug), pa00 = ldu(egof(p, EF_PA0), ug), pa10 = ldu(egof(p, EF_PA1), ug);
+    const float sx0 = ldu(egof(p, EF_SX), ug), sy0 = ldu(egof(p, EF_SY), ug), sv0 = ldu(egof(p, EF_SV), ug);
+    const float sh0 = ldu(egof(p, EF_SH), ug);
+    const int pidx_l = ldu(egoi(p, EF_PIDX), ug), intent_l = ldu(egoi(p, EF_INTENT), ug);
+    const uint8_t alive_l = ldu(gmem(p.ego.alive), ug);
+    // phase 1's first pass in group layout (lane (grp, sub): agent grp), without
+    // traffic (there the NPC phase runs in between, and the window registers would
+    // stay live through it): the agent's route, path index and env reset flag
+    // EARLY (k_step's compile-time layouts without traffic: N <= 8 agent slots, the
+    // window LDS in el.win)
+    static_assert(!EARLY || (FUSED && !TRAFFIC), "LDS path windows: k_step without traffic");
+    constexpr bool early = EARLY;
+    const int ga = (tid >> 3) < N ? (tid >> 3) : 0;
+    const int eea = PK == 1 ? e : e + ga / NE;
+    int groute = 0, gpidx = 0;
+    bool gpend = false;
+    // (loads in one basic block, in-bounds by clamped indices rather than behind
+    // branches: the scheduler keeps them together ahead of every use)
+    // and its kinematic state and actions: phase 1's kinematics then read no LDS, so
+    // no LDS read waits for round B's DMA before the window is needed (without alias
+    // information an LDS read waits for every LDS DMA in flight)
+    uint8_t gpend_b = 0, galive_b = 0;
+    Kin gk{};
+    float ga0 = 0.0f, ga1 = 0.0f;
+    if constexpr (early) {
+        const uint32_t ugg = (uint32_t)(e * NE + ga);
+        groute = ldu(egoi(p, EF_ROUTE), ugg);
+        gpidx = ldu(egoi(p, EF_PIDX), ugg);
+        gpend_b = ldu(gmem(p.pending_reset), (uint32_t)eea);
+        gk = Kin{ldu(egof(p, EF_X), ugg), ldu(egof(p, EF_Y), ugg), ldu(egof(p, EF_V), ugg), ldu(egof(p, EF_H), ugg),
+                 ldu(egof(p, EF_ACC), ugg), ldu(egof(p, EF_STEER), ugg)};
+        galive_b = ldu(gmem(p.ego.alive), ugg);
+        ga0 = ldu(gmem(in.actions), 2 * ugg);
+        ga1 = ldu(gmem(in.actions), 2 * ugg + 1);
+    }
+    float rl0 = 0.0f, rl1 = 0.0f;
+    if (FUSED) {
+        const int rmax = p.R - 1;
+        rl0 = ldu(gmem(p.rel_angles), (uint32_t)(tid < rmax ? tid : rmax));
+        rl1 = ldu(gmem(p.rel_angles), (uint32_t)(tid + WAVE < rmax ? tid + WAVE : rmax));
     }
     NpcRegs nreg{};
     if constexpr (TRAFFIC) nreg = npc_load(p, e, tid);  // in flight with the ego loads
-    // MEV_EARLY_PATH (N <= 8: one pass of phase 1): lane (grp, sub) reads agent grp's
-    // route and path index with the state and issues its path window loads right
-    // away, before the state goes through LDS (phase 1 would otherwise read them
-    // back from LDS first, one more round trip in front of the path loads)
-    const bool early = MEV_EARLY_PATH && N <= 8;
-    float2 ept[8], epend = make_float2(0.0f, 0.0f), epprev = epend, ep10 = epend;
+    // every load above is issued before any of their values is used (a use scheduled
+    // between them would put a wait for the first loads in front of the rest)
+    __builtin_amdgcn_sched_barrier(0);
+    const bool pending = pending_b != 0;
+    gpend = gpend_b != 0;
+    const bool do_reset = in.auto_reset && pending;
+    const int prev_step = do_reset ? 0 : step_prev;
+    const int prev_npcs = TRAFFIC ? (do_reset ? 0 : npcs_prev) : 0;
+    if (lane_on) {
+        el.a0[il] = a0;
+        el.a1[il] = a1;
+        el.route[il] = route_l;
+        el.x[il] = x0; el.y[il] = y0; el.v[il] = v0; el.h[il] = h0;
+        el.acc[il] = acc0; el.steer[il] = steer0; el.prev_dist[il] = pd0;
+        el.pa0[il] = pa00; el.pa1[il] = pa10;
+        el.sx[il] = sx0; el.sy[il] = sy0; el.sv[il] = sv0; el.sh[il] = sh0;
+        el.pidx[il] = pidx_l; el.intent[il] = intent_l; el.alive[il] = alive_l;
+    }
+    if constexpr (FUSED) {
+        if (p.R <= 2 * WAVE) {
+            if (tid < p.R) el.rel[tid] = rl0;
+            if (tid + WAVE < p.R) el.rel[tid + WAVE] = rl1;
+        } else {
+            for (int b = tid; b < p.R; b += WAVE) el.rel[b] = gmem(p.rel_angles)[b];
+        }
+    }
+    if (lane_on && do_reset) {  // the lane's env was auto-reset: its agents start from their spawns
+        const int rid = reset_route(p, in.rng_counter, ee, PK == 1 ? il : il - (ee - e) * NE, route_l);
+        const float rx = gmem(p.rt.spawn)[3 * rid], ry = gmem(p.rt.spawn)[3 * rid + 1], rh = gmem(p.rt.spawn)[3 * rid + 2];
+        el.route[il] = rid;
+        el.x[il] = rx; el.y[il] = ry; el.v[il] = 0.0f; el.h[il] = rh;
+        el.acc[il] = 0.0f; el.steer[il] = 0.0f; el.prev_dist[il] = 0.0f; el.pa0[il] = 0.0f; el.pa1[il] = 0.0f;
+        el.sx[il] = rx; el.sy[il] = ry; el.sv[il] = 0.0f; el.sh[il] = rh;
+        el.pidx[il] = 0; el.intent[il] = gmem(p.rt.intent)[rid]; el.alive[il] = 1;
+    }
+    // round B: the first pass's path windows, loaded straight into LDS (gfx950
+    // global_load_lds_dwordx4: no VGPRs held while they are in flight) from the
+    // group-layout route / index registers.  Agent grp's window is the 64 points
+    // from s_e = start_i rounded down to even (16-B aligned: 32 chunks of 2 points,
+    // [start_i, start_i + 50) and the look-ahead target start_i + <= 59 inside it);
+    // lane (grp, sub) loads chunks 4 sub .. 4 sub + 3 (instruction m: chunk 4 sub +
+    // m at win + m KB + grp * 128 + sub * 16) and reads back exactly those, so each
+    // lane's 8 points arrive as 4 aligned 16-B LDS reads.  A fifth instruction brings
+    // the route's last chunk (points 158, 159: lane sub 0) and path[10, 11] (sub 1).
+    // Chunks past the path's end are clamped to its last one: those points lie
+    // beyond every window's range and are never used.
     int eroute = 0, epidx = 0;
     if (early) {
-        const int ga = (tid >> 3) < N ? (tid >> 3) : 0;
-        const int eea = PK == 1 ? e : e + ga / NE;
-        eroute = egoi(p, EF_ROUTE)[e * NE + ga];
-        epidx = egoi(p, EF_PIDX)[e * NE + ga];
-        if (in.auto_reset && gmem(p.pending_reset)[eea] != 0) {
-            eroute = reset_route(p, in.rng_counter, eea, PK == 1 ? ga : ga - (eea - e) * NE, eroute);
-            epidx = 0;
+        const bool greset = in.auto_reset && gpend;
+        eroute = greset ? reset_route(p, in.rng_counter, eea, PK == 1 ? ga : ga - (eea - e) * NE, groute) : groute;
+        epidx = greset ? 0 : gpidx;
+        if (greset) {  // agent ga starts from its spawn (as the lane layout above)
+            gk = Kin{gmem(p.rt.spawn)[3 * eroute], gmem(p.rt.spawn)[3 * eroute + 1], 0.0f,
+                     gmem(p.rt.spawn)[3 * eroute + 2], 0.0f, 0.0f};
+            galive_b = 1;
         }
-        const GF2 P = gf2(p.rt.path + (size_t)eroute * (2 * PATH_LEN));
         const int start_i = epidx < 0 ? 0 : epidx;
+        const int sub = tid & 7;
+        const uint32_t rbase = (uint32_t)eroute * (2 * PATH_LEN * 4);  // bytes
+        typedef const __attribute__((address_space(1))) char gchar;
+        gchar* path_b = (gchar*)gmem(p.rt.path);
+        __attribute__((address_space(3))) char* win = (__attribute__((address_space(3))) char*)el.win;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int q = start_i + (tid & 7) * 8 + j;
-            ept[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+        for (int m = 0; m < 4; ++m) {
+            int c = (start_i >> 1) + sub * 4 + m;
+            c = c < PATH_LEN / 2 ? c : PATH_LEN / 2 - 1;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(path_b + rbase + c * 16),
+                                             (__attribute__((address_space(3))) void*)(win + m * 1024), 16, 0, 0);
         }
-        epend = P[PATH_LEN - 1];
-        epprev = P[PATH_LEN - 2];
-        ep10 = P[10];
-    }
-    for (int i = tid; i < N; i += WAVE) {
-        const int g = e * NE + i;
-        const int route_l = egoi(p, EF_ROUTE)[g];
-        const float a0 = in.actions[2 * g], a1 = in.actions[2 * g + 1];
-        const float x = egof(p, EF_X)[g], y = egof(p, EF_Y)[g], v = egof(p, EF_V)[g], h = egof(p, EF_H)[g];
-        const float acc = egof(p, EF_ACC)[g], steer = egof(p, EF_STEER)[g], pd = egof(p, EF_PREV_DIST)[g];
-        const float pa0 = egof(p, EF_PA0)[g], pa1 = egof(p, EF_PA1)[g];
-        const float sx = egof(p, EF_SX)[g], sy = egof(p, EF_SY)[g], sv = egof(p, EF_SV)[g], sh = egof(p, EF_SH)[g];
-        const int pidx = egoi(p, EF_PIDX)[g], intent = egoi(p, EF_INTENT)[g];
-        const uint8_t alive = gmem(p.ego.alive)[g];
-        el.a0[i] = a0;
-        el.a1[i] = a1;
-        if (do_reset) {
-            const int rid = reset_route(p, in.rng_counter, ee, PK == 1 ? i : i - (ee - e) * NE, route_l);
-            const float rx = gmem(p.rt.spawn)[3 * rid], ry = gmem(p.rt.spawn)[3 * rid + 1], rh = gmem(p.rt.spawn)[3 * rid + 2];
-            el.route[i] = rid;
-            el.x[i] = rx; el.y[i] = ry; el.v[i] = 0.0f; el.h[i] = rh;
-            el.acc[i] = 0.0f; el.steer[i] = 0.0f; el.prev_dist[i] = 0.0f; el.pa0[i] = 0.0f; el.pa1[i] = 0.0f;
-            el.sx[i] = rx; el.sy[i] = ry; el.sv[i] = 0.0f; el.sh[i] = rh;
-            el.pidx[i] = 0; el.intent[i] = gmem(p.rt.intent)[rid]; el.alive[i] = 1;
-        } else {
-            el.route[i] = route_l;
-            el.x[i] = x; el.y[i] = y; el.v[i] = v; el.h[i] = h;
-            el.acc[i] = acc; el.steer[i] = steer; el.prev_dist[i] = pd;
-            el.pa0[i] = pa0; el.pa1[i] = pa1;
-            el.sx[i] = sx; el.sy[i] = sy; el.sv[i] = sv; el.sh[i] = sh;
-            el.pidx[i] = pidx; el.intent[i] = intent; el.alive[i] = alive;
-        }
+        const int cx = sub == 0 ? PATH_LEN / 2 - 1 : 5;  // points 158, 159 / 10, 11
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(path_b + rbase + cx * 16),
+                                         (__attribute__((address_space(3))) void*)(win + 4 * 1024), 16, 0, 0);
     }
     const int step_no = prev_step + 1;  // res.step = ++step_count (:137)
     // gmem(p.step_count)[e] = step_no is stored with the other env flags (a store this
     // early would be drained by the vmcnt waits of every later load)
-    wave_lds_sync();
+    // (no fence: an acquire fence would also wait for round B's LDS DMA, which
+    // phase 1 first needs after the kinematics; one wave's LDS operations complete
+    // in order, so ordering the code is enough)
+    wave_lds_order();
 
     STAMP(0);
     int ncnt = 0;
@@ -1589,14 +1686,13 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         const int pidx0 = early ? epidx : el.pidx[ii];
         const int start_i = pidx0 < 0 ? 0 : pidx0;
         const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
-        // the 50-point window and the look-ahead target lie in [start_i, start_i + 64): 8 points per lane
+        // the window's first point: start_i, or (early: the LDS window of round B)
+        // start_i rounded down to even; the 50-point window and the look-ahead target
+        // lie in [w0, w0 + 64): 8 points per lane
+        const int w0 = early ? (start_i & ~1) : start_i;
         float2 pt[8];
         float2 pend, pprev, p10;
-        if (early) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pt[j] = ept[j];
-            pend = epend; pprev = epprev; p10 = ep10;
-        } else {
+        if (!early) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int q = start_i + sub * 8 + j;
@@ -1604,33 +1700,50 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             }
             pend = P[PATH_LEN - 1]; pprev = P[PATH_LEN - 2]; p10 = P[10];
         }
-        Kin k{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
-        const bool alive = act && el.alive[ii] != 0;
+        Kin k = early ? gk : Kin{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
+        const bool alive = act && (early ? galive_b : el.alive[ii]) != 0;
+        const float a0_i = early ? ga0 : el.a0[ii], a1_i = early ? ga1 : el.a1[ii];
         float cH, sH;
 #if MEV_BF_PHYS
         {
             // every lane runs the update; a dead agent keeps its state (one sincosf)
             Kin ku = k;
-            car_update_heading(ku, el.a0[ii], el.a1[ii], in.dt);
+            car_update_heading(ku, a0_i, a1_i, in.dt);
             sincosf(alive ? ku.h : k.h, &sH, &cH);
             car_update_move(ku, cH, sH);
             if (alive) k = ku;
         }
 #else
-        if (alive) car_update(k, el.a0[ii], el.a1[ii], in.dt, &cH, &sH);
+        if (alive) car_update(k, a0_i, a1_i, in.dt, &cH, &sH);
         else sincosf(k.h, &sH, &cH);
 #endif
         STAMPX(1);
+        if (early) {  // round B's window: wait for the LDS DMA, then 4 aligned 16-B reads per lane
+            __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+            const float4* wl = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + grp * 128 + sub * 16);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const float4 q = wl[m * 64];  // + m KB
+                pt[2 * m] = make_float2(q.x, q.y);
+                pt[2 * m + 1] = make_float2(q.z, q.w);
+            }
+            // lane (grp, 0): points 158, 159; lane (grp, 1): points 10, 11
+            const float4* wx = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + 4096 + grp * 128);
+            const float4 ends = wx[0], ten = wx[1];
+            pprev = make_float2(ends.x, ends.y);
+            pend = make_float2(ends.z, ends.w);
+            p10 = make_float2(ten.x, ten.y);
+        }
         // Car::update_path_index (Car.cpp:47-74): first minimum over the window, in order
         float bd = __builtin_inff();
         int bi = 0x7fffffff;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int off = sub * 8 + j;
-            if (off < cnt) {
+            const int q = w0 + sub * 8 + j;  // the point's path index
+            if (q >= start_i && q < start_i + cnt) {
                 const float dx = pt[j].x - k.x, dy = pt[j].y - k.y;
                 const float d = dx * dx + dy * dy;
-                if (d < bd) { bd = d; bi = start_i + off; }
+                if (d < bd) { bd = d; bi = q; }
             }
         }
         // minimum over the 8 lanes of the group (first index on ties): DPP swaps
@@ -1645,7 +1758,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         // look-ahead point of the observation (:444-452), picked from the window
         {
             const int tidx = pidx + 10 < PATH_LEN - 1 ? pidx + 10 : PATH_LEN - 1;
-            const int toff = tidx - start_i;
+            const int toff = tidx - w0;
             if (act && toff >= 0 && toff < 64 && sub == (toff >> 3)) {
                 float2 t = pt[0];
 #pragma unroll
@@ -3058,6 +3171,10 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
     el.head = reinterpret_cast<float*>(step_lds + sl.head);
     el.rel = reinterpret_cast<float*>(step_lds + sl.rel);
     el.envw = reinterpret_cast<int32_t*>(step_lds + sl.envw);
+    if constexpr (!TRAFFIC && NM > 0) {
+        static_assert(NM == 0 || FixedLayout<(NM ? NM : 1), 0>::lay.bytes >= kWinBytes, "LDS path windows");
+        el.win = reinterpret_cast<float4*>(step_lds + sl.lidar);
+    }
     __shared__ typename std::conditional<TRAFFIC, NpcLDST<KM>, char>::type nl_storage;
     NpcLDST<KM>* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
@@ -3071,7 +3188,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
     if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS - 1);
 #endif
     CarsCtx cx{};
-    if (wv == 0) cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK>(p, in, out, e, el, nl);
+    if (wv == 0) cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK, (MEV_EARLY_WINDOW && !TRAFFIC && NM > 0)>(p, in, out, e, el, nl);
     if (SPLIT) __syncthreads();
     else wave_lds_sync();
 #if !defined(MEV_EXP_STOP) || MEV_EXP_STOP != 0  // timing-only stop0: the car part without cars_post
