@@ -93,6 +93,10 @@ struct mev_handle {
     hipEvent_t ev_step[2] = {nullptr, nullptr}, ev_gather[2] = {nullptr, nullptr};
     bool gather_pending[2] = {false, false};
     int64_t gathers = 0;  // gathered steps so far; the last one used buffer (gathers - 1) & 1
+    // NPC-aware deal of the fused traffic kernel: valid while every step since the
+    // last state change went through it (the rings then hold one entry per env)
+    bool deal_valid = false;
+    int deal_ring = 0;
 
     template <class T>
     hipError_t alloc(T** p, size_t n) {
@@ -305,6 +309,10 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&p.npc.alive, EK); A(&p.npc.count, size_t(E));
     A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 2); A(&p.debug, size_t(E) * 8);
     A(&p.ob_box, size_t(E) * size_t(N + c.max_npcs)); A(&p.ob_cand, EN * 2);
+    if (c.traffic_flow) {  // the fused traffic kernel's NPC-aware deal (mev_kernels.h, kDealLists)
+        A(&p.deal_cnt, size_t(3) * mev::kDealRingInts);
+        A(&p.deal_order, size_t(mev::kDealLists) * mev::kDealClasses * size_t(E));
+    }
     // outputs
     A(&h->internal.obs, EN * size_t(D)); A(&h->internal.rew, EN); A(&h->internal.done, EN); A(&h->internal.status, EN);
     A(&h->internal.term, size_t(E)); A(&h->internal.trunc, size_t(E)); A(&h->internal.alive_cnt, size_t(E));
@@ -468,6 +476,7 @@ int mev_configure_traffic(mev_handle* h, int32_t enabled, float density) {
             return fail(MEV_E_INVALID, "the fused step kernel (mev_set_step_kernel 2) cannot hold this handle's NPC slots");
     }
     h->cfg.traffic_flow = enabled;
+    h->deal_valid = false;
     h->cfg.traffic_density = density < 0.0f ? 0.0f : density;  // configure_traffic clamps (:56-60)
     h->sp.traffic = enabled;
     return MEV_OK;
@@ -622,6 +631,7 @@ int mev_reset(mev_handle* h, const uint8_t* env_mask, float* obs, uint32_t flags
     }
     mev::Outputs o = h->internal;
     if (dev && obs) o.obs = obs;
+    h->deal_valid = false;  // NPC counts changed outside the step: the deal restarts
     HIP_TRY(mev::launch_reset(h->sp, d_mask, o, h->stream, h->rng_counter++));
     h->last.obs = o.obs;
     if (!dev) {
@@ -733,7 +743,20 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         memcpy(&h->sp_dev, &h->sp, sizeof(mev::SimParams));
         h->sp_valid = true;
     }
+    // the NPC-aware deal (fused traffic k_step only; MEV_NO_DEAL=1 turns it off)
+    static const bool no_deal = [] { const char* v = getenv("MEV_NO_DEAL"); return v && v[0] == '1'; }();
+    const bool deal = h->sp.traffic && h->sp.deal_cnt && !no_deal && mev::step_kernel_for(h->sp) == 2;
+    if (deal) {
+        if (!h->deal_valid) {  // fresh rings: this step deals by the identity order and builds the next
+            HIP_TRY(hipMemsetAsync(h->sp.deal_cnt, 0, size_t(3) * mev::kDealRingInts * sizeof(int32_t), h->stream));
+            h->deal_ring = 0;
+        }
+        in.deal = 2 | (h->deal_valid ? 1 : 0);
+        in.deal_ring = h->deal_ring;
+    }
     HIP_TRY(mev::launch_step(h->sp, h->d_sp, in, o, h->stream, ev));
+    h->deal_valid = deal;
+    if (deal) h->deal_ring = h->deal_ring == 2 ? 0 : h->deal_ring + 1;
     h->last = o;
     if (gather && h->world == 1) {
         ++h->gathers;  // a world of one: the root's row is written in place, nothing to move
@@ -839,6 +862,7 @@ int mev_set_state(mev_handle* h, const mev_state* s) {
     STATE_FIELDS(SET)
 #undef SET
     HIP_TRY(hipMemsetAsync(h->sp.pending_reset, 0, E, h->stream));
+    h->deal_valid = false;
     HIP_TRY(mev::launch_observe_reset_lidar(h->sp, h->internal, h->stream));
     h->last.obs = h->internal.obs;
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1090,6 +1114,7 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
         if (int r = sync_internal(h)) return r;
     }
     h->last = h->internal;
+    h->deal_valid = false;
     const std::vector<SnapField> f = snap_fields(h);
     std::vector<size_t> off;
     const size_t total = snap_offsets(f, E, &off);

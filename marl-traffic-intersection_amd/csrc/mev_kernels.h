@@ -99,7 +99,25 @@ struct SimParams {
     int32_t step_pack;
     // two waves per fused workgroup (host side): 0 auto (<= 2048 workgroups), 1 off, 2 on
     int32_t step_split;
+    // NPC-aware env deal of the fused traffic kernel (see kDealLists): per (ring, list,
+    // class) counters, each on its own 128-B line, and per (list, class) env orders
+    int32_t* deal_cnt;    // [3][kDealLists][kDealClasses][kDealPad]
+    int32_t* deal_order;  // [kDealLists][kDealClasses][E]
 };
+
+// The fused traffic k_step deals envs to workgroups by their NPC count: every env
+// stays in logical list x (the workgroups b with b % 8 == x, i.e. one XCD), and
+// within a list the workgroups take its envs heaviest first (the i-th workgroup of
+// list x, b = 8 i + x, the i-th env in descending NPC class), so that the first
+// workgroups the dispatcher places -- one per SIMD -- hold the heaviest envs and
+// every SIMD's four wave slots get one env from each quarter of the NPC-count
+// order.  At the end of its step each env appends itself to the class list of
+// step t+1 (a counter atomic per (list, class)); rings of three counter sets:
+// step t reads ring t % 3, fills ring (t+1) % 3 and clears ring (t+2) % 3.
+constexpr int kDealLists = 8;
+constexpr int kDealClasses = 8;  // NPC counts 0..6, 7 and more
+constexpr int kDealPad = 32;     // ints per counter (128 B)
+constexpr int kDealRingInts = kDealLists * kDealClasses * kDealPad;
 
 struct StepInputs {
     const float* actions;      // [E*N*2]
@@ -108,6 +126,10 @@ struct StepInputs {
     float spawn_prob;          // 1 - expf(-density * dt) computed on host with glibc
     int32_t auto_reset;
     uint64_t rng_counter;      // handle-wide step counter (Philox counter for NPC spawns)
+    // NPC-aware deal (fused traffic k_step): bit 0 take envs from ring deal_ring's
+    // lists (else the XCD-aware identity order), bit 1 build ring deal_ring + 1
+    int32_t deal;
+    int32_t deal_ring;
 };
 
 // The kernels launch_step will use for p: 1 = k_cars + k_lidar, 2 = the fused

@@ -328,6 +328,26 @@ __device__ inline int xcd_env(int b, int E) {
     return b < 8 * q ? (b & 7) * q + (b >> 3) : b;
 }
 
+// The env of workgroup b under the NPC-aware deal (kDealLists in mev_kernels.h):
+// list x = b % 8 (the XCD the dispatcher sends b to), rank i = b / 8 in that list's
+// descending NPC-class order, from the counts and orders step t - 1 built.
+__device__ inline int deal_env(const SimParams& p, int ring, int b) {
+    const int x = b & (kDealLists - 1);
+    int i = b >> 3;
+    const __attribute__((address_space(1))) int32_t* cnt =
+        gmem(p.deal_cnt) + (size_t)ring * kDealRingInts + x * kDealClasses * kDealPad;
+    int n[kDealClasses];
+#pragma unroll
+    for (int c = 0; c < kDealClasses; ++c) n[c] = __builtin_amdgcn_readfirstlane(cnt[c * kDealPad]);
+    int c = kDealClasses - 1;
+#pragma unroll
+    for (int k = kDealClasses - 1; k > 0; --k) {  // heaviest class first
+        if (c == k && i >= n[k]) { i -= n[k]; c = k - 1; }
+    }
+    i = i < p.E - 1 ? i : p.E - 1;  // (the host keeps the rings consistent; never out of bounds)
+    return __builtin_amdgcn_readfirstlane(gmem(p.deal_order)[((size_t)x * kDealClasses + c) * p.E + i]);
+}
+
 // -------------------------------------------------------- shared state ---
 struct EgoLDS {
     float x[MAXN], y[MAXN], v[MAXN], h[MAXN], c[MAXN], s[MAXN];
@@ -1478,6 +1498,7 @@ struct CarsCtx {
     int step_no;    // step counter after this step
     bool do_reset;  // the env was auto-reset at the start of this step
     int ncnt;       // NPCs alive after the traffic phase
+    bool ended;     // (set by cars_post, PK == 1) terminated or truncated this step
 };
 
 // The per-env body of the step before the LiDAR (k_cars, or the first part of
@@ -2002,7 +2023,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     }
 
     STAMP(5);
-    return CarsCtx{step_no, do_reset, ncnt};
+    return CarsCtx{step_no, do_reset, ncnt, false};
 }
 
 // The rest of the car part (after the LiDAR in k_step, right after cars_pre in
@@ -2011,7 +2032,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
 // Reads only the car LDS (the LiDAR never writes it).
 template <bool TRAFFIC, bool FUSED, class NL, int PK = 1>
 __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out, const int e, const CarsLDS& el,
-                                          const NL* nl, const CarsCtx& cx) {
+                                          const NL* nl, CarsCtx& cx) {
     const int tid = threadIdx.x & (WAVE - 1);
     const int NE = p.N;  // agents per env (PK > 1: see cars_pre)
     const int npk = PK == 1 ? 1 : (p.E - e < PK ? p.E - e : PK);
@@ -2066,6 +2087,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
         const int alive_cnt = __builtin_popcountll(alive_m & emask), succ_cnt = __builtin_popcountll(succ_m & emask);
         const bool terminated = p.respawn ? (succ_cnt > 0 && succ_cnt == alive_cnt) : ((done_m & emask) != 0ull);
         const bool truncated = p.max_steps > 0 && step_e >= p.max_steps;
+        if (PK == 1) cx.ended = terminated || truncated;
         if (in_env) {
             if (STAGE) el.rew[i] = rew_i;
             else {
@@ -2213,7 +2235,7 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
     __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
     NpcLDS* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
-    const CarsCtx cx = cars_pre<TRAFFIC, false>(p, in, out, e, el, nl);
+    CarsCtx cx = cars_pre<TRAFFIC, false>(p, in, out, e, el, nl);
     wave_lds_sync();
     cars_post<TRAFFIC, false>(p, out, e, el, nl, cx);
 }
@@ -3161,7 +3183,8 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
     extern __shared__ __align__(16) unsigned char step_lds[];
     const int wv = SPLIT ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
     // PK envs per wave (few agents per env): envs e .. e + PK - 1, see cars_pre
-    const int e = xcd_env((int)blockIdx.x, (int)gridDim.x) * PK;
+    const int e = (TRAFFIC && (in.deal & 1)) ? deal_env(p, in.deal_ring, (int)blockIdx.x)
+                                             : xcd_env((int)blockIdx.x, (int)gridDim.x) * PK;
 #if defined(MEV_STAMPS_R)
     STAMP_RAW(0);
 #endif
@@ -3195,6 +3218,22 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
     if (!MEV_POST_AFTER_LIDAR && wv == 0) {
         cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
         wave_lds_sync();
+    }
+    if (TRAFFIC && (in.deal & 2)) {
+        // the NPC-aware deal of the next step: this env joins its list's class for
+        // step t + 1 (an env that ended restarts without NPCs after its auto-reset)
+        const int lane0 = threadIdx.x & (WAVE - 1);
+        const int x = (int)blockIdx.x & (kDealLists - 1);
+        const int nxt = in.deal_ring == 2 ? 0 : in.deal_ring + 1;
+        if (lane0 == 0) {
+            const int c = (in.auto_reset && cx.ended) ? 0 : (cx.ncnt < kDealClasses - 1 ? cx.ncnt : kDealClasses - 1);
+            const int slot = atomicAdd(p.deal_cnt + (size_t)nxt * kDealRingInts + (x * kDealClasses + c) * kDealPad, 1);
+            gmem(p.deal_order)[((size_t)x * kDealClasses + c) * p.E + slot] = e;
+        }
+        if (blockIdx.x == 0 && lane0 < kDealLists * kDealClasses) {  // clear ring t + 2
+            const int clr = nxt == 2 ? 0 : nxt + 1;
+            gmem(p.deal_cnt)[(size_t)clr * kDealRingInts + lane0 * kDealPad] = 0;
+        }
     }
     if (SPLIT && wv == 0) return;  // wave 1 runs the LiDAR
 #else
