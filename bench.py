@@ -224,6 +224,37 @@ def dry_run(args):
         dist.destroy_process_group()
 
 
+def verify_gather(env, _capi, E, N, D, world, gfmt, ls, dev):
+    """Root: decode the last gathered step's [world][bytes] buffer (sharding.PackedOutputs) and
+    check it: every rank's rows finite with valid status codes, and the root's own row equal,
+    bit for bit, to the library's decode of the same step (mev_get_outputs)."""
+    import torch
+    import torch.utils.dlpack as tdl
+    from marl_traffic_intersection_amd import sharding
+
+    ptr, per_rank, w = env.gather_result()
+    if not ptr or w != world:
+        return "missing"
+    lay = sharding.PackedOutputs(E, N, D, fmt=gfmt, lidar_slots=ls,
+                                 table=env.lidar_decode_table() if gfmt else None)
+    stacked = tdl.from_dlpack(env.output_dlpack("gathered"))
+    got = lay.unpack_gathered(stacked, world * E, world)
+    torch.cuda.synchronize(dev)
+    if not (torch.isfinite(got["obs"]).all().item() and torch.isfinite(got["reward"]).all().item()
+            and int(got["status"].max().item()) <= 5):
+        return "FAILED: non-finite or invalid rows"
+    mine = env.get_outputs()
+    for k in sharding.PackedOutputs.FIELDS:
+        a = got[k][:E].cpu().numpy()
+        b = mine[k]
+        if a.dtype.kind == "f":
+            a, b = a.view("u4"), b.view("u4")
+        if not (a == b).all():
+            return f"FAILED: root row {k} differs from the library's decode"
+    return (f"decoded {world} rank rows ({'u8 LiDAR codes' if gfmt else 'f32 rows'}): finite, valid status codes; "
+            f"the root's row bit-equal to mev_get_outputs of the same step")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,6 +264,8 @@ def main():
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the second timed phase (every step's outputs gathered to rank 0 over RCCL)")
     ap.add_argument("--gather-timeout", type=float, default=120.0, help="seconds before a stuck gather is aborted")
+    ap.add_argument("--gather-format", choices=("u8", "f32"), default="u8",
+                    help="packed gather rows: u8 = 31-float heads + one LiDAR code per beam (lossless), f32 = plain rows")
     ap.add_argument("--no-kernel-events", action="store_true", help="do not record per-kernel HIP events")
     ap.add_argument("--event-every", type=int, default=50, help="record the per-kernel events on every n-th step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -354,6 +387,9 @@ def main():
             import threading
             init_err = []
 
+            gfmt = _capi.MEV_GATHER_LIDAR_U8 if args.gather_format == "u8" else _capi.MEV_GATHER_F32
+            env.set_gather_format(gfmt)
+
             def _init():
                 try:
                     with stdout_to_stderr():
@@ -398,18 +434,23 @@ def main():
                 dist.barrier()
             g_elapsed, bad = max_over_ranks([g_elapsed, 1.0 - ok])
             if bad == 0.0:
-                per = _capi.packed_layout(E, N, D)[1]  # bytes per rank per step
+                ls = env.lidar_slots()
+                per = _capi.packed_layout(E, N, D, gfmt, ls)[1]  # bytes per rank per step
+                per_f32 = _capi.packed_layout(E, N, D)[1]
                 gather.update({
                     "value": round(world * E * N * K / g_elapsed, 1), "unit": "agent-steps/s",
-                    "ms_per_step": round(g_elapsed / K * 1e3, 5), "bytes_per_rank_per_step": per,
+                    "ms_per_step": round(g_elapsed / K * 1e3, 5), "format": args.gather_format,
+                    "bytes_per_rank_per_step": per, "bytes_per_rank_per_step_f32_rows": per_f32,
                     "root_ingress_GBs": round(per * (world - 1) / (g_elapsed / K) / 1e9, 2),
                     "what": "phase 1's steps with every step's packed outputs (obs|reward|done|status|"
-                            "terminated|truncated) gathered to rank 0: one grouped ncclSend/ncclRecv per step "
-                            "from the C ABI (MEV_GATHER_TO_ROOT), on a communication stream overlapping the next step"})
+                            "terminated|truncated; u8: 31-float obs heads + one LiDAR code per beam, decoded "
+                            "bit-exactly on the root) gathered to rank 0: one grouped ncclSend/ncclRecv per step "
+                            "from the C ABI (MEV_GATHER_TO_ROOT), on a communication stream overlapping the next step",
+                    "bound": "at N > 1 the root receives (N - 1) x bytes_per_rank_per_step every step over its xGMI "
+                             "links, so this phase is bound by the root's ingress, not by the step kernel; at N = 1 "
+                             "the root's row is written in place and nothing moves"})
                 if rank == 0:
-                    ptr, per_rank, w = env.gather_result()
-                    torch.cuda.synchronize(dev)
-                    gather["verified"] = "gather buffer present" if ptr else "missing"
+                    gather["verified"] = verify_gather(env, _capi, E, N, D, world, gfmt, ls, dev)
             elif "error" not in gather:
                 gather["error"] = "another rank failed in the gather phase"
         elif "error" not in gather:

@@ -22,8 +22,10 @@ MEV_DEVICE_PTRS = 0x1
 MEV_AUTO_RESET = 0x2
 MEV_GATHER_TO_ROOT = 0x4
 MEV_COMM_ID_BYTES = 128
-# packed-output fields (mev_packed_layout) and DLPack outputs (mev_output_dlpack), include/marlenv.h order
-PACKED_FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated")
+MEV_GATHER_F32 = 0
+MEV_GATHER_LIDAR_U8 = 1
+# packed-output fields (mev_packed_layout2) and DLPack outputs (mev_output_dlpack), include/marlenv.h order
+PACKED_FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated", "lidar")
 DLPACK_OUTPUTS = ("obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step", "gathered")
 
 STATUS_NAMES = ("ALIVE", "DEAD", "SUCCESS", "CRASH_WALL", "CRASH_LINE", "CRASH_CAR")
@@ -41,7 +43,7 @@ EXPORTED = (
     "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel", "mev_set_step_pack", "mev_get_step_pack",
     "mev_set_step_split", "mev_get_step_split",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
-    "mev_gather_wait", "mev_output_dlpack",
+    "mev_gather_wait", "mev_output_dlpack", "mev_packed_layout2", "mev_set_gather_format", "mev_lidar_decode_table",
 )
 
 
@@ -156,6 +158,9 @@ def load_library(variant: str = None):
     L.mev_car_check_collision.argtypes = [f32p, f32p, i32p]
     u64p = ctypes.POINTER(ctypes.c_uint64)
     L.mev_packed_layout.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, u64p, u64p]
+    L.mev_packed_layout2.argtypes = [ctypes.c_int32] * 5 + [u64p, u64p]
+    L.mev_set_gather_format.argtypes = [_vp, ctypes.c_int32]
+    L.mev_lidar_decode_table.argtypes = [_vp, f32p]
     L.mev_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.mev_comm_init.argtypes = [_vp, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.mev_comm_destroy.argtypes = [_vp]
@@ -434,6 +439,21 @@ class Handle:
         _check(self._lib.mev_comm_init(self._h, bytes(unique_id), int(world), int(rank), int(root), int(slots)))
         self.comm = dict(world=int(world), rank=int(rank), root=int(root), slots=int(slots) or self.E)
 
+    def set_gather_format(self, fmt: int):
+        """MEV_GATHER_F32 (plain obs rows) or MEV_GATHER_LIDAR_U8 (31-float heads + one LiDAR code per
+        beam, lossless); before comm_init."""
+        _check(self._lib.mev_set_gather_format(self._h, int(fmt)))
+        self.gather_format = int(fmt)
+
+    def lidar_decode_table(self) -> np.ndarray:
+        """The compact gather format's 256-entry code -> LiDAR float table (mev_lidar_decode_table)."""
+        t = np.zeros(256, np.float32)
+        _check(self._lib.mev_lidar_decode_table(self._h, t.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+        return t
+
+    def lidar_slots(self) -> int:
+        return min(self.R, self.D - 31)
+
     def comm_destroy(self):
         _check(self._lib.mev_comm_destroy(self._h))
         self.comm = None
@@ -614,11 +634,13 @@ def car_check_collision(box_a, box_b) -> bool:
     return bool(r.value)
 
 
-def packed_layout(slots: int, agents: int, obs_dim: int):
-    """(offsets by field, total bytes) of one rank's packed outputs (mev_packed_layout; host-only, no GPU)."""
+def packed_layout(slots: int, agents: int, obs_dim: int, fmt: int = MEV_GATHER_F32, lidar_slots: int = 0):
+    """(offsets by field, total bytes) of one rank's packed outputs (mev_packed_layout2; host-only, no GPU).
+    fmt MEV_GATHER_LIDAR_U8: "obs" holds [slots][N][31] heads and "lidar" [slots][N][lidar_slots] codes."""
     off = (ctypes.c_uint64 * len(PACKED_FIELDS))()
     n = ctypes.c_uint64()
-    _check(load_library().mev_packed_layout(int(slots), int(agents), int(obs_dim), off, ctypes.byref(n)))
+    _check(load_library().mev_packed_layout2(int(slots), int(agents), int(obs_dim), int(lidar_slots), int(fmt), off,
+                                             ctypes.byref(n)))
     return dict(zip(PACKED_FIELDS, (int(x) for x in off))), int(n.value)
 
 

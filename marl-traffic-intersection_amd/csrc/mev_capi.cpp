@@ -86,7 +86,10 @@ struct mev_handle {
     // multi-GPU gather (mev_comm_init): packed outputs, double buffered by step parity
     ncclComm_t comm = nullptr;
     int world = 1, rank = 0, root = 0, slots = 0;
-    uint64_t pk_off[MEV_PK_COUNT] = {};
+    uint64_t pk_off[MEV_PK_FIELDS] = {};
+    int gather_fmt = MEV_GATHER_F32;  // mev_set_gather_format
+    std::vector<float> h_lidar_table;  // [256] decode table of the compact format (mev_lidar_decode_table)
+    float* d_lidar_table = nullptr;
     uint64_t pk_bytes = 0;
     uint8_t* pk_buf[2] = {nullptr, nullptr};  // root: [world][pk_bytes]; other ranks: [pk_bytes]
     hipStream_t comm_stream = nullptr;
@@ -230,6 +233,14 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     if (h->cfg.traffic_density < 0.0f) h->cfg.traffic_density = 0.0f;  // configure_traffic (:56-60)
     h->D = D;
     h->lidar_slots = std::min(c.lidar_rays, D - mev::OBS_HEAD);
+    {  // the compact gather format's LiDAR codes -> floats (Lidar::normalized, Lidar.cpp:92-98)
+        const float inv = (c.lidar_max_dist > 0.0f) ? (1.0f / c.lidar_max_dist) : 0.0f;
+        h->h_lidar_table.assign(256, 0.0f);
+        h->h_lidar_table[0] = c.lidar_max_dist * inv;  // no hit: max_dist
+        for (size_t k = 0; k < dists.size() && k + 1 < size_t(mev::kLidarCodeDead); ++k)
+            h->h_lidar_table[k + 1] = dists[k] * inv;  // hit at probe k
+        h->h_lidar_table[mev::kLidarCodeDead] = 0.0f;  // dead agent
+    }
     h->P = 8 * c.num_lanes;
     h->nroutes = h->P * h->P;
     h->pts = mev::build_lane_points(c.num_lanes);
@@ -322,6 +333,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&h->d_paths, h->h_paths.size()); A(&h->d_pbox, h->h_pbox.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
     A(&h->d_rel, rel.size()); A(&h->d_traffic, size_t(h->P) * size_t(h->P));
     A(&h->d_reset_routes, size_t(h->P) * size_t(h->P));
+    A(&h->d_lidar_table, size_t(256));
     A(reinterpret_cast<uint8_t**>(&h->d_sp), sizeof(mev::SimParams));
     float* d_dist = nullptr;
     if (!dist_mul_exact) A(&d_dist, dists.size());
@@ -330,6 +342,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
         delete h;
         return fail(MEV_E_NOMEM, "device allocation failed: " + m);
     }
+    h->internal.obs_ld = D;
     h->last = h->internal;
     // upload tables
     err = hipMemcpyAsync(h->d_paths, h->h_paths.data(), h->h_paths.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
@@ -338,6 +351,8 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_intent, h->h_intent.data(), h->h_intent.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_rel, rel.data(), rel.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess && d_dist) err = hipMemcpyAsync(d_dist, dists.data(), dists.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess)
+        err = hipMemcpyAsync(h->d_lidar_table, h->h_lidar_table.data(), 256 * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_traffic, h->h_traffic.data(), h->h_traffic.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
     // default ego routes: reference env.py:138-145 (mapping routes, cyclic)
     std::vector<int32_t> ego(EN);
@@ -672,6 +687,7 @@ static bool pin_ready(mev_handle* h) {
     h->pin_out.trunc = d + h->pin_off[7];
     h->pin_out.alive_cnt = reinterpret_cast<int32_t*>(d + h->pin_off[8]);
     h->pin_out.step = reinterpret_cast<int32_t*>(d + h->pin_off[9]);
+    h->pin_out.obs_ld = h->D;
     return true;
 }
 
@@ -728,6 +744,10 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         o.status = base + h->pk_off[MEV_PK_STATUS];
         o.term = base + h->pk_off[MEV_PK_TERMINATED];
         o.trunc = base + h->pk_off[MEV_PK_TRUNCATED];
+        if (h->gather_fmt == MEV_GATHER_LIDAR_U8) {  // heads [slots][N][31] + one LiDAR code per beam
+            o.obs_ld = mev::OBS_HEAD;
+            o.lidar_u8 = base + h->pk_off[MEV_PK_LIDAR];
+        }
     }
     const hipEvent_t* ev = nullptr;
     if (!h->tev.empty() && (h->t_phase++ % h->t_every) == 0) {
@@ -805,11 +825,16 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     return MEV_OK;
 }
 
+static int sync_internal(mev_handle* h);  // below, with mev_device_outputs
+
 int mev_get_outputs(mev_handle* h, float* obs, float* rew, uint8_t* done, uint8_t* status, uint8_t* term,
                     uint8_t* trunc, int32_t* alive, int32_t* step, uint32_t flags) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->cfg.device));
     const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
+    if (h->last.lidar_u8) {  // compact gather row: decoded into the handle's buffers first
+        if (int r0 = sync_internal(h)) return r0;
+    }
     int r = copy_out(h, h->last, obs, rew, done, status, term, trunc, alive, step,
                      dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost);
     if (r) return r;
@@ -880,7 +905,11 @@ static int sync_internal(mev_handle* h) {
         if (!src || src == dst) return hipSuccess;
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, h->stream);
     };
-    HIP_TRY(pull(I.obs, L.obs, EN * size_t(h->D) * sizeof(float)));
+    if (L.lidar_u8)  // a compact-format gather row: decode heads + LiDAR codes into the obs rows
+        HIP_TRY(mev::launch_unpack_lidar_u8(L.obs, L.lidar_u8, h->d_lidar_table, I.obs, int(EN), h->D, h->lidar_slots,
+                                            h->stream));
+    else
+        HIP_TRY(pull(I.obs, L.obs, EN * size_t(h->D) * sizeof(float)));
     HIP_TRY(pull(I.rew, L.rew, EN * sizeof(float)));
     HIP_TRY(pull(I.done, L.done, EN));
     HIP_TRY(pull(I.status, L.status, EN));
@@ -1068,6 +1097,9 @@ int mev_snapshot(mev_handle* h, void* dst, uint32_t flags) {
     HIP_TRY(hipSetDevice(h->cfg.device));
     const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
     const size_t E = size_t(h->cfg.num_envs);
+    if (h->last.lidar_u8) {  // compact gather row: the snapshot stores plain obs rows
+        if (int r0 = sync_internal(h)) return r0;
+    }
     const std::vector<SnapField> f = snap_fields(h);
     std::vector<size_t> off;
     const size_t total = snap_offsets(f, E, &off);
@@ -1171,6 +1203,43 @@ int mev_packed_layout(int32_t slots, int32_t num_agents, int32_t obs_dim, uint64
     return MEV_OK;
 }
 
+int mev_packed_layout2(int32_t slots, int32_t num_agents, int32_t obs_dim, int32_t lidar_slots, int32_t format,
+                       uint64_t* offsets, uint64_t* bytes) {
+    if (!offsets || !bytes) return fail(MEV_E_INVALID, "null argument");
+    if (slots < 1 || num_agents < 1 || obs_dim < mev::OBS_HEAD || lidar_slots < 0 || lidar_slots > obs_dim - mev::OBS_HEAD)
+        return fail(MEV_E_INVALID, "slots and agents must be >= 1, obs_dim >= 31, 0 <= lidar_slots <= obs_dim - 31");
+    if (format != MEV_GATHER_F32 && format != MEV_GATHER_LIDAR_U8) return fail(MEV_E_INVALID, "unknown gather format");
+    const uint64_t C = uint64_t(slots), N = uint64_t(num_agents);
+    const bool u8 = format == MEV_GATHER_LIDAR_U8;
+    const uint64_t row = u8 ? uint64_t(mev::OBS_HEAD) : uint64_t(obs_dim);
+    const uint64_t sizes[MEV_PK_FIELDS] = {C * N * row * 4, C * N * 4, C * N, C * N, C, C,
+                                           u8 ? C * N * uint64_t(lidar_slots) : 0};
+    uint64_t off = 0;
+    for (int f = 0; f < MEV_PK_FIELDS; ++f) {
+        off = (off + 255) & ~uint64_t(255);
+        offsets[f] = off;
+        off += sizes[f];
+    }
+    *bytes = (off + 255) & ~uint64_t(255);
+    return MEV_OK;
+}
+
+int mev_set_gather_format(mev_handle* h, int32_t format) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (format != MEV_GATHER_F32 && format != MEV_GATHER_LIDAR_U8) return fail(MEV_E_INVALID, "unknown gather format");
+    if (h->comm) return fail(MEV_E_INVALID, "set the gather format before mev_comm_init");
+    if (format == MEV_GATHER_LIDAR_U8 && h->sp.lidar_steps + 1 >= mev::kLidarCodeDead)
+        return fail(MEV_E_INVALID, "the compact gather format needs at most 253 LiDAR march probes");
+    h->gather_fmt = format;
+    return MEV_OK;
+}
+
+int mev_lidar_decode_table(const mev_handle* h, float* table) {
+    if (!h || !table) return fail(MEV_E_INVALID, "null argument");
+    memcpy(table, h->h_lidar_table.data(), 256 * sizeof(float));
+    return MEV_OK;
+}
+
 int mev_comm_unique_id(uint8_t* id) {
     if (!id) return fail(MEV_E_INVALID, "null argument");
     static_assert(sizeof(ncclUniqueId) == MEV_COMM_ID_BYTES, "unique id size");
@@ -1190,7 +1259,7 @@ int mev_comm_init(mev_handle* h, const uint8_t* id, int32_t world, int32_t rank,
     if (slots < h->cfg.num_envs) return fail(MEV_E_INVALID, "slots must be >= num_envs");
     HIP_TRY(hipSetDevice(h->cfg.device));
     HIP_TRY(hipStreamSynchronize(h->stream));
-    int rc = mev_packed_layout(slots, h->cfg.num_agents, h->D, h->pk_off, &h->pk_bytes);
+    int rc = mev_packed_layout2(slots, h->cfg.num_agents, h->D, h->lidar_slots, h->gather_fmt, h->pk_off, &h->pk_bytes);
     if (rc) return rc;
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));

@@ -60,7 +60,19 @@ struct Outputs {
     uint8_t* trunc;
     int32_t* alive_cnt;
     int32_t* step;
+    // floats per observation row in `obs`: D, or OBS_HEAD when lidar_u8 is set (the
+    // compact gather format: the LiDAR block goes to lidar_u8 as one code per beam,
+    // [E*N][lidar_slots]: 0 = no hit (max_dist), k + 1 = hit at march probe k, 255 =
+    // dead agent (0.0); decoded through mev_lidar_decode_table; padding columns
+    // beyond 31 + lidar_slots are not written)
+    int32_t obs_ld;
+    uint8_t* lidar_u8;
 };
+// the LiDAR code of a dead agent's beam in the compact gather format
+constexpr int kLidarCodeDead = 255;
+// decode the compact format's rows: obs [n][D] from heads [n][31] and codes [n][slots]
+hipError_t launch_unpack_lidar_u8(const float* head, const uint8_t* codes, const float* table, float* obs, int n,
+                                  int D, int slots, hipStream_t s);
 
 struct SimParams {
     int32_t E, N, R, K, D;   // envs, agents, beams, npc slots, obs_dim

@@ -2188,7 +2188,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             const float f3 = (self ? h : wrap_angle(oh - h)) / PI_F;
             if (act) {
                 // k_step stages the head in LDS (written with the LiDAR block by fused_store)
-                float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)(e * NE + i) * p.D;
+                float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)(e * NE + i) * out.obs_ld;
                 if (!alv) {
                     for (int cc = sub; cc < OBS_HEAD; cc += 8) row[cc] = 0.0f;
                 } else {
@@ -2205,20 +2205,20 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
                     }
                 }
                 if (!STAGE)
-                    for (int cc = OBS_HEAD + p.lidar_slots + sub; cc < p.D; cc += 8) row[cc] = 0.0f;
+                    for (int cc = OBS_HEAD + p.lidar_slots + sub; cc < out.obs_ld; cc += 8) row[cc] = 0.0f;
             }
         }
     } else {
         for (int i = tid; i < N; i += WAVE) {
             const int g = e * NE + i;
-            float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)g * p.D;
+            float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)g * out.obs_ld;
             if (!el.alive[i]) {
                 for (int c = 0; c < OBS_HEAD; ++c) row[c] = 0.0f;
                 if (!STAGE)
-                    for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
+                    for (int c = OBS_HEAD + p.lidar_slots; c < out.obs_ld; ++c) row[c] = 0.0f;
                 continue;
             }
-            write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row, !STAGE);
+            write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row, !STAGE && out.obs_ld == p.D);
         }
     }
     STAMP(6);
@@ -2506,7 +2506,12 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (!Src::kStaged && __popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
         for (int j = 0; j < na; ++j) {
             if ((am >> j) & 1ull) continue;
-            float* row = out.obs + (size_t)(a0 + j) * p.D + OBS_HEAD;
+            if (out.lidar_u8) {  // compact gather format: the dead-agent code
+                uint8_t* crow = out.lidar_u8 + (size_t)(a0 + j) * p.lidar_slots;
+                for (int b = lane; b < p.lidar_slots; b += WAVE) crow[b] = (uint8_t)kLidarCodeDead;
+                continue;
+            }
+            float* row = out.obs + (size_t)(a0 + j) * out.obs_ld + OBS_HEAD;
             for (int b = lane; b < p.lidar_slots; b += WAVE) row[b] = 0.0f;
         }
     }
@@ -2992,6 +2997,17 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     auto lidar_value = [&](int r) {
         return ((r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max) * p.lidar_inv;
     };
+    if (out.lidar_u8) {  // compact gather format: one code per beam (0 no hit, k + 1 hit at probe k)
+        for (int j = 0; j < nal; ++j) {
+            const int g = __float_as_int(ag[j].w);
+            uint8_t* crow = out.lidar_u8 + (size_t)g * p.lidar_slots;
+            for (int b = lane; b < p.lidar_slots; b += WAVE) {
+                const int r = res[j * R + b];
+                crow[b] = (uint8_t)((r & 1) ? (r >> 1) + 1 : 0);
+            }
+        }
+        return;
+    }
     if (p.lidar_slots <= WAVE) {
         // lane = beam: the agents' global indices come from one LDS read (readlane per
         // row) and 8 rows' results are read before any is stored (one LDS wait per 8 rows)
@@ -3005,14 +3021,14 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             for (int u = 0; u < 8; ++u) {
                 if (j0 + u < nal && beam) {
                     const int g = __builtin_amdgcn_readlane(gl, j0 + u);
-                    out.obs[(size_t)g * p.D + OBS_HEAD + lane] = lidar_value(rr[u]);
+                    out.obs[(size_t)g * out.obs_ld + OBS_HEAD + lane] = lidar_value(rr[u]);
                 }
             }
         }
     } else {
         for (int j = 0; j < nal; ++j) {
             const int g = __float_as_int(ag[j].w);
-            float* row = out.obs + (size_t)g * p.D + OBS_HEAD;
+            float* row = out.obs + (size_t)g * out.obs_ld + OBS_HEAD;
             for (int b = lane; b < p.lidar_slots; b += WAVE) row[b] = lidar_value(res[j * R + b]);
         }
     }
@@ -3491,6 +3507,31 @@ hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outpu
 hipError_t launch_observe_reset_lidar(const SimParams& p, const Outputs& out, hipStream_t s) {
     if (p.traffic) hipLaunchKernelGGL(k_reset<true>, dim3(p.E), dim3(WAVE), 0, s, p, nullptr, out, 0, 0ull);
     else hipLaunchKernelGGL(k_reset<false>, dim3(p.E), dim3(WAVE), 0, s, p, nullptr, out, 0, 0ull);
+    return hipGetLastError();
+}
+
+// ------------------------------------------- compact gather format unpack ---
+// obs rows [n][D] from the compact format's heads [n][31] and LiDAR codes
+// [n][slots] through the decode table (mev_lidar_decode_table): the same floats the
+// plain step writes; padding columns are zero.  Thread = (row, column).
+__global__ void k_unpack_lidar_u8(const float* head, const uint8_t* codes, const float* table, float* obs, int n,
+                                  int D, int slots) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)n * D) return;
+    const size_t row = t / D;
+    const int c = (int)(t - row * D);
+    float v = 0.0f;
+    if (c < OBS_HEAD) v = head[row * OBS_HEAD + c];
+    else if (c < OBS_HEAD + slots) v = table[codes[row * slots + (c - OBS_HEAD)]];
+    obs[t] = v;
+}
+
+hipError_t launch_unpack_lidar_u8(const float* head, const uint8_t* codes, const float* table, float* obs, int n,
+                                  int D, int slots, hipStream_t s) {
+    const size_t total = (size_t)n * D;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unpack_lidar_u8, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, head, codes, table,
+                       obs, n, D, slots);
     return hipGetLastError();
 }
 

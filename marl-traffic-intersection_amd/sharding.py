@@ -39,18 +39,27 @@ def env_owner(env: int, total_envs: int, world: int) -> int:
 
 
 class PackedOutputs:
-    """Byte layout of one rank's step outputs: the library's mev_packed_layout
-    (host-only, no device), so these views match what MEV_GATHER_TO_ROOT writes."""
+    """Byte layout of one rank's step outputs: the library's mev_packed_layout2
+    (host-only, no device), so these views match what MEV_GATHER_TO_ROOT writes.
+
+    fmt = MEV_GATHER_LIDAR_U8 (the compact format): the message holds each row's
+    31-float head and one u8 code per LiDAR beam; unpack() rebuilds the float
+    rows through the library's decode table (`table`, Handle.lidar_decode_table()),
+    bit-identical to the plain step's."""
 
     FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated")
 
-    def __init__(self, slots: int, agents: int, obs_dim: int):
+    def __init__(self, slots: int, agents: int, obs_dim: int, fmt: int = 0, lidar_slots: int = 0, table=None):
         from . import _capi
 
         self.C, self.N, self.D = int(slots), int(agents), int(obs_dim)
-        self.offsets, self.nbytes = _capi.packed_layout(self.C, self.N, self.D)
+        self.fmt, self.L = int(fmt), int(lidar_slots)
+        if self.fmt == _capi.MEV_GATHER_LIDAR_U8 and table is None:
+            raise ValueError("the compact gather format needs the decode table (Handle.lidar_decode_table())")
+        self.table = table
+        self.offsets, self.nbytes = _capi.packed_layout(self.C, self.N, self.D, self.fmt, self.L)
         self.offsets: Dict[str, int]
-        self.used = self.offsets["truncated"] + self.C
+        self.used = self.offsets["lidar"] + (self.C * self.N * self.L if self.fmt else 0)
 
     def pointers(self, base: int) -> Dict[str, int]:
         """Field pointers (for mev_step's output arguments) inside a buffer at `base`."""
@@ -58,11 +67,15 @@ class PackedOutputs:
 
     def _shapes(self):
         C, N, D = self.C, self.N, self.D
-        return {"obs": ((C, N, D), 4), "reward": ((C, N), 4), "done": ((C, N), 1), "status": ((C, N), 1),
-                "terminated": ((C,), 1), "truncated": ((C,), 1)}
+        sh = {"obs": ((C, N, 31 if self.fmt else D), 4), "reward": ((C, N), 4), "done": ((C, N), 1),
+              "status": ((C, N), 1), "terminated": ((C,), 1), "truncated": ((C,), 1)}
+        if self.fmt:
+            sh["lidar"] = ((C, N, self.L), 1)
+        return sh
 
     def unpack(self, buf) -> Dict[str, object]:
-        """Typed views of one packed buffer (torch uint8 tensor or numpy uint8 array)."""
+        """Outputs of one packed buffer (torch uint8 tensor or numpy uint8 array): views in the
+        plain format; in the compact format "obs" is rebuilt [C, N, D] from heads + decoded codes."""
         out = {}
         is_torch = hasattr(buf, "view") and hasattr(buf, "data_ptr")
         for name, (shape, isz) in self._shapes().items():
@@ -79,6 +92,21 @@ class PackedOutputs:
                 import numpy as np
                 a = raw.view(np.float32) if isz == 4 else raw
                 out[name] = a.reshape(shape)
+        if self.fmt:
+            head, codes = out["obs"], out.pop("lidar")
+            C, N, D, L = self.C, self.N, self.D, self.L
+            if is_torch:
+                import torch
+                tab = torch.as_tensor(self.table, dtype=torch.float32, device=codes.device)
+                obs = torch.zeros((C, N, D), dtype=torch.float32, device=codes.device)
+                obs[..., :31] = head
+                obs[..., 31:31 + L] = tab[codes.long()]
+            else:
+                import numpy as np
+                obs = np.zeros((C, N, D), np.float32)
+                obs[..., :31] = head
+                obs[..., 31:31 + L] = np.asarray(self.table, np.float32)[codes]
+            out["obs"] = obs
         return out
 
     def unpack_gathered(self, stacked, total_envs: int, world: int) -> Dict[str, object]:

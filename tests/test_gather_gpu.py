@@ -29,18 +29,27 @@ def _bits(a):
     return a.view(np.uint32) if a.dtype == np.float32 else a
 
 
-def test_gather_world1_row_equals_plain_step(mev):
+@pytest.mark.parametrize("fmt", [0, 1], ids=["f32", "lidar_u8"])
+def test_gather_world1_row_equals_plain_step(mev, fmt):
+    """fmt 1: the compact format (heads + one u8 code per beam), decoded through the
+    library's table -- bit-identical to the plain rows, dead agents included."""
     import torch
     import torch.utils.dlpack as tdl
     from marl_traffic_intersection_amd import _capi, sharding
 
     E, N, R, T = 48, 8, 64, 40
-    cfg = dict(num_envs=E, num_agents=N, lidar_rays=R, use_team_reward=1, max_steps=25, device=0)
+    cfg = dict(num_envs=E, num_agents=N, lidar_rays=R, use_team_reward=1, max_steps=25, device=0,
+               respawn_enabled=0 if fmt else 1)  # no respawn: crashed agents stay dead (code 255 rows)
     plain = mev.Handle(**cfg)
     gat = mev.Handle(**cfg)
     try:
+        if fmt:
+            gat.set_gather_format(_capi.MEV_GATHER_LIDAR_U8)
         gat.comm_init(_capi.comm_unique_id(), world=1, rank=0, root=0, slots=E + 3)
-        lay = sharding.PackedOutputs(E + 3, N, plain.D)
+        lay = sharding.PackedOutputs(E + 3, N, plain.D, fmt=fmt, lidar_slots=gat.lidar_slots(),
+                                     table=gat.lidar_decode_table() if fmt else None)
+        if fmt:
+            assert lay.nbytes < 0.6 * sharding.PackedOutputs(E + 3, N, plain.D).nbytes
         rng = np.random.default_rng(5)
         for t in range(T):
             act = rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)
@@ -55,7 +64,8 @@ def test_gather_world1_row_equals_plain_step(mev):
             got = lay.unpack(buf[0])
             for k in FIELDS:
                 assert np.array_equal(_bits(got[k][:E]), _bits(ref[k])), (t, k)
-                assert not np.any(got[k][E:]), (t, k)  # unused slots stay zero
+                tail = got[k][E:, :, :31] if (fmt and k == "obs") else got[k][E:]
+                assert not np.any(tail), (t, k)  # unused slots stay zero
             assert np.array_equal(extra["agents_alive"], ref["agents_alive"])
             assert np.array_equal(extra["step"], ref["step"])
             last = gat.get_outputs()  # mev_get_outputs reads where the step wrote: the packed row
