@@ -78,6 +78,36 @@ def make_handle(mod, meta, num_envs: int, device: int = 0):
                       reward=meta["reward"], max_npcs=32, device=device)
 
 
+def single_env_handle(mod, d):
+    """A one-env handle at golden scenario d's initial state (as replay() sets it up);
+    returns (handle, spawn_route(t) for its steps)."""
+    meta = d["meta"]
+    L = int(meta["num_lanes"])
+    h = make_handle(mod, meta, 1)
+    troutes = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["traffic_routes"]]
+    h.set_traffic_routes(troutes)
+    ego_routes = np.array([[h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["ego_routes"]]],
+                          np.int32)
+    h.set_ego_routes(ego_routes)
+    st = h.get_state()
+    f, i = d["init_ego_f"], d["init_ego_i"]
+    for j, key in enumerate(EGO_F):
+        st[key][0] = f[:, j]
+    st["alive"][0], st["intention"][0], st["path_index"][0], st["route"][0] = i[:, 0], i[:, 1], i[:, 2], ego_routes[0]
+    k = len(d["init_npc_f"])
+    st["npc_count"][0] = k
+    if k:
+        nf, ni = d["init_npc_f"], d["init_npc_i"]
+        for j, key in enumerate(NPC_F):
+            st[key][0, :k] = nf[:, j]
+        st["npc_alive"][0, :k], st["npc_intention"][0, :k], st["npc_path_index"][0, :k] = ni[:, 0], ni[:, 1], ni[:, 2]
+        st["npc_route"][0, :k] = [troutes[r] for r in ni[:, 3]]
+    st["step_count"][0] = int(meta.get("init_step", 0))
+    h.set_state(st)
+    spawn_of = (lambda t: np.array([d["spawned"][t]], np.int32)) if meta["traffic"] else (lambda t: None)
+    return h, spawn_of
+
+
 def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: int = 0,
            pack: int = 0, split: int = 0) -> List[Report]:
     """Run the scenarios `names` (identical configs) as envs 0..B-1 of one handle

@@ -206,7 +206,9 @@ def test_rgb_array_render():
         e.step(np.zeros((4, 2), np.float32))
     frame = e.render()
     assert frame.shape == (750, 750, 3) and frame.dtype == np.uint8
-    assert (frame == np.array(render.EGO, np.uint8)).all(-1).sum() > 4 * 400  # four 54x24 cars
+    for i in range(4):  # four 54x24 cars, coloured by agent index (Renderer.cpp:597-599)
+        col = np.array(render._rgba8(render.AGENT_COLORS[i])[:3], np.uint8)
+        assert (frame == col).all(-1).sum() > 600, i
     assert (frame == np.array(render.HIT, np.uint8)).all(-1).any()
     e.close()
 
