@@ -406,30 +406,6 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     p.n_traffic_routes = int(h->h_traffic.size());
     p.reset_routes = h->d_reset_routes;
     p.n_reset_routes = 0;
-    if (N == 1) {
-        // the LiDAR a respawned lone ego observes, per route (its spawn pose with no other car):
-        // k_step's split kernel starts the LiDAR before it knows which egos respawn
-        const size_t nr = size_t(h->nroutes), slots = size_t(h->lidar_slots);
-        float* scratch_ego = nullptr;
-        uint8_t* scratch_alive = nullptr;
-        unsigned long long* scratch_cand = nullptr;
-        float* table = nullptr;
-        uint8_t* codes = nullptr;
-        hipError_t e2 = h->alloc(&scratch_ego, nr * mev::EF_COUNT);
-        if (e2 == hipSuccess) e2 = h->alloc(&scratch_alive, nr);
-        if (e2 == hipSuccess) e2 = h->alloc(&scratch_cand, nr * 2);
-        if (e2 == hipSuccess) e2 = h->alloc(&table, nr * (size_t(mev::OBS_HEAD) + slots));
-        if (e2 == hipSuccess) e2 = h->alloc(&codes, nr * (slots ? slots : 1));
-        if (e2 == hipSuccess) e2 = mev::launch_spawn_lidar(p, scratch_ego, scratch_alive, scratch_cand, table, codes, h->stream);
-        if (e2 != hipSuccess) {
-            const std::string m = hipGetErrorString(e2);
-            delete h;
-            *out = nullptr;
-            return fail(MEV_E_HIP, "spawn LiDAR table: " + m);
-        }
-        p.spawn_lidar = table;
-        p.spawn_lidar_u8 = codes;
-    }
     // initial state = a reset (the reference env.py constructor ends with reset(), env.py:136)
     const int rc = mev_reset(h, nullptr, nullptr, 0);
     if (rc != MEV_OK) {

@@ -115,12 +115,6 @@ struct SimParams {
     // class) counters, each on its own 128-B line, and per (list, class) env orders
     int32_t* deal_cnt;    // [3][kDealLists][kDealClasses][kDealPad]
     int32_t* deal_order;  // [kDealLists][kDealClasses][E]
-    // LiDAR of a lone car at each route's spawn pose (handles with one ego per env;
-    // null otherwise): the LiDAR block a respawned lone ego observes, per route, as
-    // floats [nroutes][OBS_HEAD + lidar_slots] (columns OBS_HEAD..) and as the compact
-    // format's codes [nroutes][lidar_slots] (launch_spawn_lidar)
-    const float* spawn_lidar;
-    const uint8_t* spawn_lidar_u8;
 };
 
 // The fused traffic k_step deals envs to workgroups by their NPC count: every env
@@ -167,12 +161,6 @@ hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outpu
                         uint64_t rng_counter);
 // recompute the observation rows from the current state with LiDAR = max (after set_state)
 hipError_t launch_observe_reset_lidar(const SimParams& p, const Outputs& out, hipStream_t s);
-
-// spawn_lidar tables of p (one ego per env): the LiDAR of a car alone at each route's
-// spawn pose, computed by k_lidar on scratch state (ego SoA [EF_COUNT][nroutes] f32,
-// alive [nroutes], candidate masks [nroutes][2]); float rows [nroutes][OBS_HEAD + slots]
-hipError_t launch_spawn_lidar(const SimParams& p, float* scratch_ego, uint8_t* scratch_alive,
-                              unsigned long long* scratch_cand, float* table, uint8_t* codes, hipStream_t s);
 
 // masked per-env copy of snapshot fields (mev_restore)
 constexpr int kMaxRestoreFields = 48;

@@ -1512,7 +1512,7 @@ struct CarsCtx {
 // are not published to HBM.
 template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
-                                            const CarsLDS& el, NL* nl, const bool split_lone = false) {
+                                            const CarsLDS& el, NL* nl) {
     static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
     // status, collisions, respawn, observation head); the LiDAR block of the
@@ -1623,13 +1623,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         } else {
             for (int b = tid; b < p.R; b += WAVE) el.rel[b] = gmem(p.rel_angles)[b];
         }
-    }
-    if (split_lone) {
-        // k_step SPLIT, one ego per env: the LiDAR wave starts at barrier A (after the
-        // kinematics), so the candidate masks it reads must already be empty, and the
-        // respawn word it waits on cleared
-        if (lane_on) { el.cand[2 * il] = 0ull; el.cand[2 * il + 1] = 0ull; }
-        if (tid == 0) el.envw[6] = 0;
     }
     if (lane_on && do_reset) {  // the lane's env was auto-reset: its agents start from their spawns
         const int rid = reset_route(p, in.rng_counter, ee, PK == 1 ? il : il - (ee - e) * NE, route_l);
@@ -1896,11 +1889,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         STAMPX(5);
     }
     wave_lds_sync();
-    // barrier A (k_step SPLIT, one ego per env): every pose after the kinematics is in
-    // LDS; the LiDAR wave starts from it while this wave finishes the car part.  A
-    // lone ego's pose changes after this only by a respawn, and then to its route's
-    // spawn pose, whose LiDAR is the route's spawn_lidar row (published below)
-    if (split_lone) __syncthreads();
 
     STAMP(2);
     // one ego per env and no NPCs: no car can touch another, and no LiDAR beam can
@@ -1987,14 +1975,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         }
     }
     wave_lds_sync();
-    if (split_lone) {
-        // the respawned slots for the LiDAR wave (bit 8: published)
-        const uint8_t st = el.status[tid < N ? tid : 0];
-        const bool rs = tid < N && p.respawn && el.alive[tid] && el.done[tid] &&
-                        (st == ST_CRASH_CAR || st == ST_CRASH_WALL || st == ST_CRASH_LINE);
-        const unsigned long long m = ballot(rs);
-        if (tid == 0) __hip_atomic_store(&el.envw[6], (int)(m & 0xffull) | 0x100, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
     STAMPY(3);
 
     STAMP(4);
@@ -3247,16 +3227,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
     if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS - 1);
 #endif
     CarsCtx cx{};
-    // SPLIT with one ego per env: the LiDAR wave starts at barrier A inside cars_pre
-    // (after the kinematics) instead of after the whole of cars_pre
-    const bool split_lone = SPLIT && p.N == 1 && p.spawn_lidar != nullptr;
-    if (wv == 0) cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK, (MEV_EARLY_WINDOW && !TRAFFIC && NM > 0)>(p, in, out, e, el, nl, split_lone);
-    else if (split_lone) __syncthreads();  // barrier A
-    if (SPLIT) {
-        if (!split_lone) __syncthreads();
-    } else {
-        wave_lds_sync();
-    }
+    if (wv == 0) cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK, (MEV_EARLY_WINDOW && !TRAFFIC && NM > 0)>(p, in, out, e, el, nl);
+    if (SPLIT) __syncthreads();
+    else wave_lds_sync();
 #if !defined(MEV_EXP_STOP) || MEV_EXP_STOP != 0  // timing-only stop0: the car part without cars_post
     if (!MEV_POST_AFTER_LIDAR && wv == 0) {
         cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
@@ -3301,30 +3274,6 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
         lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, TRAFFIC ? LIDAR_NPR : MEV_LIDAR_NPR_TAIL,
                    !TRAFFIC || MEV_HELP_TRAFFIC>(
             p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
-    }
-    if (split_lone) {
-        // respawned lone egos observe their route's spawn-pose LiDAR: wait for the car
-        // wave's respawn word (published well before the LiDAR ends; bounded spin), then
-        // overwrite those rows (each lane rewrites the beams it wrote itself)
-        int v = 0;
-        for (int it = 0; it < (1 << 22); ++it) {
-            v = __hip_atomic_load(&el.envw[6], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (v & 0x100) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        const int slots = p.lidar_slots;
-        for (unsigned m = (unsigned)v & 0xffu; m; m &= m - 1u) {
-            const int i = __builtin_ctz(m);
-            const int r = el.route[i];
-            const size_t g = (size_t)g0 + i;
-            if (out.lidar_u8) {
-                for (int b = lane; b < slots; b += WAVE)
-                    out.lidar_u8[g * slots + b] = gmem(p.spawn_lidar_u8)[(size_t)r * slots + b];
-            } else {
-                for (int b = lane; b < slots; b += WAVE)
-                    out.obs[g * out.obs_ld + OBS_HEAD + b] = gmem(p.spawn_lidar)[(size_t)r * (OBS_HEAD + slots) + OBS_HEAD + b];
-            }
-        }
     }
     if (MEV_POST_AFTER_LIDAR) {  // experiment (variant postlate): measured slower, 41.6 -> 44.1 us
         if (MEV_PRIO_POST >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_POST);
@@ -3405,8 +3354,6 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
     }
 }
 
-static hipError_t launch_lidar(const SimParams& p, const Outputs& out, int a_begin, int a_end, hipStream_t s);
-
 static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Outputs& out, int e0, int e1,
                               hipStream_t s, const hipEvent_t* ev) {
     // k_cars then k_lidar over the envs [e0, e1)
@@ -3418,14 +3365,7 @@ static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Ou
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[1], s);
-    e = launch_lidar(p, out, e0 * p.N, e1 * p.N, s);
-    if (ev && e == hipSuccess) (void)hipEventRecord(ev[2], s);
-    return e;
-}
-
-// k_lidar over the agents [a_begin, a_end) (poses, alive flags and candidate masks in HBM)
-static hipError_t launch_lidar(const SimParams& p, const Outputs& out, int a_begin, int a_end, hipStream_t s) {
-    const int na = a_end - a_begin;
+    const int a_begin = e0 * p.N, a_end = e1 * p.N, na = a_end - a_begin;
     int G = lidar_group(p.R);
     // small batches: trade pool size for waves (~4 per SIMD on 256 CUs) so latency is hidden
     while (G > 1 && na / G < 4096) G = (G + 1) / 2;
@@ -3442,41 +3382,9 @@ static hipError_t launch_lidar(const SimParams& p, const Outputs& out, int a_beg
         hipLaunchKernelGGL(k_lidar<true>, dim3(blocks), dim3(wpb * WAVE), wpb * wave_lds, s, p, out, G, a_begin, a_end);
     else
         hipLaunchKernelGGL(k_lidar<false>, dim3(blocks), dim3(wpb * WAVE), wpb * wave_lds, s, p, out, G, a_begin, a_end);
-    return hipGetLastError();
-}
-
-// scratch state of launch_spawn_lidar: car r alone at route r's spawn pose
-__global__ void k_spawn_setup(SimParams q) {
-    const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (r >= q.E) return;
-    egof(q, EF_X)[r] = gmem(q.rt.spawn)[3 * r];
-    egof(q, EF_Y)[r] = gmem(q.rt.spawn)[3 * r + 1];
-    egof(q, EF_H)[r] = gmem(q.rt.spawn)[3 * r + 2];
-    gmem(q.ego.alive)[r] = 1;
-    gmem(q.ob_cand)[2 * r] = 0ull;
-    gmem(q.ob_cand)[2 * r + 1] = 0ull;
-}
-
-hipError_t launch_spawn_lidar(const SimParams& p, float* scratch_ego, uint8_t* scratch_alive,
-                              unsigned long long* scratch_cand, float* table, uint8_t* codes, hipStream_t s) {
-    SimParams q = p;  // one env per route, one lone ego each, no NPCs
-    q.E = p.rt.nroutes;
-    q.N = 1;
-    q.traffic = 0;
-    q.ego.x = scratch_ego;
-    q.ego.stride = q.E;
-    q.ego.alive = scratch_alive;
-    q.ob_cand = scratch_cand;
-    q.ob_stride = 1;
-    hipLaunchKernelGGL(k_spawn_setup, dim3((q.E + 63) / 64), dim3(64), 0, s, q);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    Outputs o{};
-    o.obs = table;  // row r: OBS_HEAD unused floats, then the LiDAR block
-    o.obs_ld = OBS_HEAD + p.lidar_slots;
-    if ((e = launch_lidar(q, o, 0, q.E, s)) != hipSuccess) return e;
-    o.lidar_u8 = codes;  // the same beams as the compact format's codes
-    return launch_lidar(q, o, 0, q.E, s);
+    e = hipGetLastError();
+    if (ev && e == hipSuccess) (void)hipEventRecord(ev[2], s);
+    return e;
 }
 
 // NPC slots of the fused kernel's LDS arrays (NpcLDST<KM>): the smallest
