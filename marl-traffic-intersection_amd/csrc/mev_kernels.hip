@@ -38,7 +38,10 @@ constexpr int WAVE = 64;
         __builtin_amdgcn_wave_barrier();                                 \
         if (threadIdx.x == 0) p.debug[e * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
-#define STAMP(k) do { if ((k) == 0) STAMP_RAW(1); if ((k) == 5) STAMP_RAW(2); } while (0)  // 5: end of cars_pre
+#ifndef MEV_STAMPS_POSTEND  // slot 2: end of cars_pre (0) or of cars_post (1: the split kernel's car wave end)
+#define MEV_STAMPS_POSTEND 0
+#endif
+#define STAMP(k) do { if ((k) == 0) STAMP_RAW(1); if ((k) == (MEV_STAMPS_POSTEND ? 6 : 5)) STAMP_RAW(2); } while (0)
 #define STAMPX(k) do {} while (0)
 #define STAMPY(k) do {} while (0)
 #elif defined(MEV_STAMPS_X)

@@ -19,17 +19,22 @@ def main():
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--step-kernel", type=int, default=0)
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--rays", type=int, default=64)
     a = ap.parse_args()
     mev = pkgload.load()
-    h = mev.Handle(num_envs=a.envs, num_agents=8, lidar_rays=64, use_team_reward=1)
+    h = mev.Handle(num_envs=a.envs, num_agents=a.agents, lidar_rays=a.rays, use_team_reward=int(a.agents > 1))
     h.set_step_kernel(a.step_kernel)
     fused = h.step_kernel() == 2
     rng = np.random.default_rng(0)
     rows = []
     for t in range(a.steps):
-        h.step(rng.uniform(-1, 1, (a.envs, 8, 2)).astype(np.float32), auto_reset=True)
+        h.step(rng.uniform(-1, 1, (a.envs, a.agents, 2)).astype(np.float32), auto_reset=True)
         if t >= a.steps // 2:
-            rows.append(h.debug_stamps().astype(np.int64).reshape(a.envs, 8))
+            st = h.debug_stamps().astype(np.int64).reshape(a.envs, 8)
+            st[:, 7] &= (1 << 40) - 1  # slot 7 carries HW_ID above bit 40
+            pk = h.step_pack()
+            rows.append(st[::pk] if pk > 1 else st)  # several envs per wave: the wave's first env holds its stamps
     names = ["cars entry", "cars loaded", "cars end", "lidar entry pool0", "lidar entry pool1", "lidar cars-phase end pool0",
              "lidar cars-phase end pool1"]
     if fused:  # one pool per env: slots 4 / 6 are its phase-1 / phase-2 ends

@@ -18,6 +18,8 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "exp_none": ["-DMEV_EXP_NOROAD", "-DMEV_EXP_NOCARS"], "exp_iters": ["-DMEV_ITERS"],
                "stampsx": ["-DMEV_STAMPS", "-DMEV_STAMPS_X"], "stampsy": ["-DMEV_STAMPS", "-DMEV_STAMPS_Y"],
                "stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
+               # stampsr with slot 2 = end of cars_post (the split kernel's car wave)
+               "stampsrp": ["-DMEV_STAMPS", "-DMEV_STAMPS_R", "-DMEV_STAMPS_POSTEND=1"],
                "stampsn": ["-DMEV_STAMPS_N"],  # NPC phase parts (tools/npc_profile.py --parts)
                # exact variants: probes per road-march step (product: 2)
                "npr1": ["-DMEV_LIDAR_NPR=1"], "npr3": ["-DMEV_LIDAR_NPR=3"],
