@@ -276,7 +276,7 @@ int mev_packed_layout(int32_t slots, int32_t num_agents, int32_t obs_dim, uint64
  *     (max_dist), k + 1 a hit at march probe k, 255 a dead agent.  Lossless: the floats
  *     are table[code] (mev_lidar_decode_table, 256 entries), bit-identical to the plain
  *     step's; padding columns beyond 31 + lidar_slots are zero.  At R = 64, N = 8 a row
- *     shrinks from 380 B to 194 B (the message from 12.66 MB to 6.46 MB at 4096 envs).
+ *     shrinks from 380 B to 194 B (the message from 12.66 MB to 6.37 MB at 4096 envs).
  * mev_packed_layout2: offsets of all MEV_PK_FIELDS fields for either format (the LiDAR
  * field is empty in MEV_GATHER_F32).  Host-only. */
 #define MEV_GATHER_F32 0
