@@ -3238,6 +3238,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
         cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
         wave_lds_sync();
     }
+#endif
     if (TRAFFIC && (in.deal & 2)) {
         // the NPC-aware deal of the next step: this env joins its list's class for
         // step t + 1 (an env that ended restarts without NPCs after its auto-reset)
@@ -3254,10 +3255,10 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimPa
             gmem(p.deal_cnt)[(size_t)clr * kDealRingInts + lane0 * kDealPad] = 0;
         }
     }
-    if (SPLIT && wv == 0) return;  // wave 1 runs the LiDAR
-#else
+#if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 0  // (stop0 keeps the deal: the env order stays the product's)
     return;
 #endif
+    if (SPLIT && wv == 0) return;  // wave 1 runs the LiDAR
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 1  // timing-only: the car part alone
     return;
 #endif
