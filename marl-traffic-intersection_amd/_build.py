@@ -63,9 +63,13 @@ def build(force: bool = False, verbose: bool = False, variant: str = "", flags=N
             raise KeyError(f"unknown library variant {variant!r} (experiment builds: tools/variants.py)")
         flags = VARIANTS[variant]
     tmp = path + ".tmp"
-    # LLVM's default machine scheduler (max-ilp was +0.7 % in round 1, 0.5 % slower on the round-2 kernel)
-    cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC] + list(flags)
+    # LLVM's default machine scheduler (max-ilp was +0.7 % in round 1, 0.5 % slower on the round-2 kernel).
+    # No SLP vectorization: packed v_pk_mul/add_f32 cost gfx950 more issue cycles than the scalar pairs
+    # they replace, plus the v_mov shuffles and hazard s_nops around them (config 3 35.0 -> 33.9 us,
+    # config 5 55.5 -> 53.0 us per step; config 2 -1.4 %: profiles/r3_ab_noslp.txt).  Exact: the same
+    # IEEE operations, unfused.
+    cmd = [_hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fno-slp-vectorize",
+           "-fPIC", "-shared", "-Wall", "-Wno-unused-function", "-I", INCLUDE, "-I", CSRC] + list(flags)
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     # RCCL for the multi-GPU gather (mev_comm_*); when torch is imported first its
     # bundled librccl.so (same SONAME librccl.so.1) satisfies this dependency,

@@ -208,7 +208,7 @@ def test_rgb_array_render():
     assert frame.shape == (750, 750, 3) and frame.dtype == np.uint8
     for i in range(4):  # four 54x24 cars, coloured by agent index (Renderer.cpp:597-599)
         col = np.array(render._rgba8(render.AGENT_COLORS[i])[:3], np.uint8)
-        assert (frame == col).all(-1).sum() > 600, i
+        assert (frame == col).all(-1).sum() > 300, i  # (semi-transparent hit rays are drawn over the cars)
     assert (frame == np.array(render.HIT, np.uint8)).all(-1).any()
     e.close()
 

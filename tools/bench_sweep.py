@@ -79,11 +79,14 @@ def main():
     ap.add_argument("--step-kernel", type=int, default=0, help="0 auto, 1 k_cars + k_lidar, 2 fused k_step")
     ap.add_argument("--pack", type=int, default=0, help="envs per fused wave: 0 auto, 1, 2, 4")
     ap.add_argument("--split", type=int, default=0, help="two waves per fused workgroup: 0 auto, 1 off, 2 on")
+    ap.add_argument("--envs", type=int, default=0, help="override the configs' env count")
     a = ap.parse_args()
     res = []
     for cfg in CONFIGS:
         if a.only and cfg["name"] not in a.only.split(","):
             continue
+        if a.envs:
+            cfg = dict(cfg, E=a.envs, desc=cfg["desc"].replace(str(cfg["E"]), str(a.envs), 1))
         r = run(cfg, a.steps if cfg["E"] > 1 else 200, a.warmup, a.step_kernel, a.pack, a.split)
         print(json.dumps(r), flush=True)
         res.append(r)

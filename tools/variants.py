@@ -47,6 +47,8 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # timing-only (wrong results): NPC controller without ghost scans / without round B
                "x_noscan": ["-DMEV_X_NOSCAN"], "x_nob": ["-DMEV_X_NOB"], "x_noplan": ["-DMEV_X_NOPLAN"],
                "x_noseq": ["-DMEV_X_NOSEQ"],
+               # (-fno-slp-vectorize is the product's since round 3; "slp" re-enables it)
+               "slp": ["-fslp-vectorize"], "novec": ["-fno-vectorize"],
                # timing-only: k_step stopped after the car part / LiDAR phase 1 / 2 / 3 (instruction budgets)
                "stop1": ["-DMEV_EXP_STOP=1"], "stop2": ["-DMEV_EXP_STOP=2"], "stop3": ["-DMEV_EXP_STOP=3"],
                "stop4": ["-DMEV_EXP_STOP=4"], "stop0": ["-DMEV_EXP_STOP=0"],
