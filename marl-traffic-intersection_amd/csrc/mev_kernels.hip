@@ -3193,8 +3193,11 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // workgroup share its LDS; wave 0 runs cars_pre, then both pass a barrier and
 // wave 1 runs the LiDAR while wave 0 runs cars_post -- the two latency chains
 // after the car part overlap instead of following each other.
+#ifndef MEV_SPLIT_WPE
+#define MEV_SPLIT_WPE 4
+#endif
 template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false>
-__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, 4) void k_step(const SimParams* __restrict__ pp, StepInputs in,
+__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? MEV_SPLIT_WPE : 4) void k_step(const SimParams* __restrict__ pp, StepInputs in,
                                                                      Outputs out) {
     static_assert(!SPLIT || (!TRAFFIC && !MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE),
                   "split waves: the plain fused step");

@@ -89,6 +89,9 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "trk": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
                "nounclust": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule=1"],
                "bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
+               # the split kernel (car wave + LiDAR wave per workgroup) with 8 / 6 waves per SIMD
+               "split8": ["-DMEV_SPLIT_WPE=8"], "split8i1": ["-DMEV_SPLIT_WPE=8", "-DMEV_PHASE1_ILP=1"],
+               "split6": ["-DMEV_SPLIT_WPE=6"], "split5": ["-DMEV_SPLIT_WPE=5"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
                "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 
