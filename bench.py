@@ -266,6 +266,8 @@ def main():
     ap.add_argument("--gather-timeout", type=float, default=120.0, help="seconds before a stuck gather is aborted")
     ap.add_argument("--gather-format", choices=("u8", "f32"), default="u8",
                     help="packed gather rows: u8 = 31-float heads + one LiDAR code per beam (lossless), f32 = plain rows")
+    ap.add_argument("--settle-ms", type=float, default=200.0,
+                    help="untimed steps for this long before the warm-up (SIMD clock ramp from idle); 0 = none")
     ap.add_argument("--no-kernel-events", action="store_true", help="do not record per-kernel HIP events")
     ap.add_argument("--event-every", type=int, default=50, help="record the per-kernel events on every n-th step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -340,6 +342,21 @@ def main():
     def step(t):
         env.step(actions[t].data_ptr(), 1.0 / 60.0, out=outs[t & 1], auto_reset=True, device=True)
 
+    # Clock settle (untimed, before the W warm-up steps): an idle MI355X needs ~0.1 s of load before
+    # its SIMD clock reaches the level it then holds for the rest of a rollout; without it a short run
+    # (the driver's 5 warm-up + 20 timed steps) times the ramp -- k_step averaged 36.9 us over such
+    # 20 steps against 34.4 us over 1000.  The steps are the metric's own (same handle,
+    # actions and outputs); the envs are reset afterwards, so the warm-up and timed steps start from
+    # the same state as without it.
+    settle_steps = 0
+    if args.settle_ms > 0:
+        t_end = time.perf_counter() + args.settle_ms * 1e-3
+        while time.perf_counter() < t_end:
+            for _ in range(64):
+                step(settle_steps % (W + K))
+                settle_steps += 1
+            torch.cuda.synchronize(dev)
+        env.reset(device=True)
     for t in range(W):
         step(t)
     torch.cuda.synchronize(dev)
@@ -514,6 +531,9 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": W,
+            "clock_settle": {"steps": settle_steps, "ms": args.settle_ms,
+                             "what": "untimed steps of the same workload before the warm-up (the SIMD clock's "
+                                     "ramp from idle), then the envs reset; --settle-ms 0 turns it off"},
             "ms_per_step": round(elapsed / K * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
