@@ -245,8 +245,11 @@ int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave);
  * workgroup -- the car part, then the LiDAR in one wave beside the rest of the
  * car part (rewards, flags, observation head) in the other.  0 = automatic (on
  * when the batch needs <= 2048 workgroups, i.e. <= 4 waves per SIMD, no traffic),
- * 1 = off, 2 = on (no traffic).  mev_get_step_split returns 1 when the next step
- * uses it.  Replaces nothing in the reference. */
+ * 1 = off, 2 = on (no traffic), 3 = early split (no traffic, one env per
+ * workgroup, N * R <= 512: the LiDAR wave marches the road from the poses after
+ * the kinematics while the car wave resolves collisions).  mev_get_step_split
+ * returns 1 (split) or 2 (early split) when the next step uses it.  Replaces
+ * nothing in the reference. */
 int mev_set_step_split(mev_handle* h, int32_t mode);
 int mev_get_step_split(const mev_handle* h, int32_t* split);
 

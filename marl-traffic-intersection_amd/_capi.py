@@ -571,14 +571,15 @@ class Handle:
         return v.value
 
     def set_step_split(self, mode: int = 0):
-        """Two waves per fused workgroup: 0 automatic, 1 off, 2 on (scheduling only; results identical)."""
+        """Two waves per fused workgroup: 0 automatic, 1 off, 2 on, 3 early split (scheduling only;
+        results identical)."""
         _check(self._lib.mev_set_step_split(self._h, int(mode)))
 
-    def step_split(self) -> bool:
-        """Whether the next step runs two waves per fused workgroup."""
+    def step_split(self) -> int:
+        """Two waves per fused workgroup in the next step: 0 no, 1 split, 2 early split."""
         v = ctypes.c_int32()
         _check(self._lib.mev_get_step_split(self._h, ctypes.byref(v)))
-        return bool(v.value)
+        return int(v.value)
 
     def set_reset_routes(self, routes):
         """Draw every agent's route from `routes` at each reset (empty: fixed routes)."""

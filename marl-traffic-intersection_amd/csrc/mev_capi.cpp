@@ -1007,7 +1007,8 @@ int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave) {
 
 int mev_set_step_split(mev_handle* h, int32_t mode) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
-    if (mode < 0 || mode > 2) return fail(MEV_E_INVALID, "split mode must be 0 (auto), 1 (off) or 2 (on)");
+    if (mode < 0 || mode > 3)
+        return fail(MEV_E_INVALID, "split mode must be 0 (auto), 1 (off), 2 (on) or 3 (early split)");
     HIP_TRY(hipSetDevice(h->cfg.device));
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->sp.step_split = mode;
@@ -1016,7 +1017,8 @@ int mev_set_step_split(mev_handle* h, int32_t mode) {
 
 int mev_get_step_split(const mev_handle* h, int32_t* split) {
     if (!h || !split) return fail(MEV_E_INVALID, "null argument");
-    *split = mev::step_kernel_for(h->sp) == 2 && mev::step_split(h->sp) ? 1 : 0;
+    const bool fused = mev::step_kernel_for(h->sp) == 2;
+    *split = fused && mev::step_esplit(h->sp) ? 2 : (fused && mev::step_split(h->sp) ? 1 : 0);
     return MEV_OK;
 }
 

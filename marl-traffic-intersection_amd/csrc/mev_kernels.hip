@@ -25,6 +25,18 @@ constexpr int WAVE = 64;
 // Diagnostic build only (-DMEV_STAMPS): per-env phase timestamps (s_memtime)
 // into SimParams::debug[e*8 + k]; never compiled into the product library.
 // -DMEV_STAMPS_X moves stamps 1-5 into k_cars' physics phase (STAMPX).
+// -DMEV_STAMPS_ES: the early split's per-env timeline (tools/es_timeline.py): wall clock
+// (s_memrealtime) of car-wave entry / barrier A / barrier B / end (slots 0-3) and
+// LiDAR-wave A passed / road end / B passed / end (4-7), lane 0 of the wave that gets there
+#ifdef MEV_STAMPS_ES
+#define ES_STAMP(k)                                                                              \
+    do {                                                                                         \
+        __builtin_amdgcn_wave_barrier();                                                         \
+        if ((threadIdx.x & 63) == 0) p.debug[e * 8 + (k)] = __builtin_amdgcn_s_memrealtime();   \
+    } while (0)
+#else
+#define ES_STAMP(k) do {} while (0)
+#endif
 #ifdef MEV_STAMPS
 #define STAMP_RAW(k)                                                     \
     do {                                                                 \
@@ -170,6 +182,10 @@ __device__ inline __attribute__((address_space(1))) int32_t* npci(const SimParam
     return gmem(reinterpret_cast<int32_t*>(p.npc.x + p.npc.stride * k));
 }
 __device__ inline unsigned long long ballot(bool p) { return __ballot(p); }
+// lanes below this one with their bit set in mask
+__device__ inline int lane_rank(unsigned long long mask) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
 
 // atan2f for wave code: the branch-free atan2f_bf unless a lane of the wave has a
 // zero / infinite / NaN operand (then fdlibm's atan2f for the wave); bit-identical
@@ -1513,9 +1529,14 @@ struct CarsCtx {
 // instead of delaying this wave's.  FUSED: the LiDAR runs in the same wave
 // (k_step) and reads the obstacle table and candidate masks from LDS, so they
 // are not published to HBM.
-template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false>
+// ESPLIT (k_step's early split, one env per two-wave workgroup): the LiDAR wave
+// computes the poses after the kinematics itself and marches the road while this
+// wave runs the car part; this wave leaves the beam offsets (el.rel) to it, records
+// the respawned egos (el.envw[6]) at the end and passes workgroup barrier B.
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
                                             const CarsLDS& el, NL* nl) {
+    static_assert(!ESPLIT || (FUSED && !TRAFFIC), "early split: k_step without traffic");
     static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
     // status, collisions, respawn, observation head); the LiDAR block of the
@@ -1594,7 +1615,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         ga1 = ldu(gmem(in.actions), 2 * ugg + 1);
     }
     float rl0 = 0.0f, rl1 = 0.0f;
-    if (FUSED) {
+    if (FUSED && !ESPLIT) {
         const int rmax = p.R - 1;
         rl0 = ldu(gmem(p.rel_angles), (uint32_t)(tid < rmax ? tid : rmax));
         rl1 = ldu(gmem(p.rel_angles), (uint32_t)(tid + WAVE < rmax ? tid + WAVE : rmax));
@@ -1619,7 +1640,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         el.sx[il] = sx0; el.sy[il] = sy0; el.sv[il] = sv0; el.sh[il] = sh0;
         el.pidx[il] = pidx_l; el.intent[il] = intent_l; el.alive[il] = alive_l;
     }
-    if constexpr (FUSED) {
+    if constexpr (FUSED && !ESPLIT) {
         if (p.R <= 2 * WAVE) {
             if (tid < p.R) el.rel[tid] = rl0;
             if (tid + WAVE < p.R) el.rel[tid + WAVE] = rl1;
@@ -1892,6 +1913,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         STAMPX(5);
     }
     wave_lds_sync();
+    ES_STAMP(1);
 
     STAMP(2);
     // one ego per env and no NPCs: no car can touch another, and no LiDAR beam can
@@ -1977,6 +1999,13 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             el.tgx[i] = el.t10x[i]; el.tgy[i] = el.t10y[i];  // path[min(0 + 10, 159)]
         }
     }
+    if constexpr (ESPLIT) {  // the respawned egos (agent slots), for the LiDAR wave after barrier B
+        const uint8_t st = el.status[tid < N ? tid : 0];
+        const bool rs = tid < N && p.respawn && el.alive[tid < N ? tid : 0] && el.done[tid < N ? tid : 0] &&
+                        (st == ST_CRASH_CAR || st == ST_CRASH_WALL || st == ST_CRASH_LINE);
+        const unsigned long long m = ballot(rs);
+        if (tid == 0) el.envw[6] = (int)(unsigned)m;
+    }
     wave_lds_sync();
     STAMPY(3);
 
@@ -2026,6 +2055,10 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     }
 
     STAMP(5);
+    if constexpr (ESPLIT) {
+        __syncthreads();  // barrier B: obstacle table, candidate masks, respawns
+        ES_STAMP(2);
+    }
     return CarsCtx{step_no, do_reset, ncnt, false};
 }
 
@@ -2361,9 +2394,6 @@ __device__ inline void slab_clip(float c0, float dc, float idc, float a, float b
     hi = fminf(hi, fmaxf(t1, t2));
 }
 
-__device__ inline int lane_rank(unsigned long long mask) {
-    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-}
 
 
 // Per-wave LDS of k_lidar: ag float4[G] (x, y, heading, agent id) of the
@@ -2484,10 +2514,17 @@ struct LidarSrcLds {
 // longest beam of its agent is done (lockstep cost = max over the agent's
 // beams, pooled cost ~ their mean); phase 3 resolves the cars as packed
 // (agent, box, beam) pairs and writes the observation's LiDAR block.
-template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR, bool HELP = false>
+//
+// PART (k_step's early split, the LiDAR wave of a two-wave workgroup): 1 = phases 1-2
+// (the road march) only, from the poses the car wave staged in ag[] after the
+// kinematics; 2 = phases 1-2 again for the compacted agents in `redo` (egos the car
+// part respawned since; the caller has put their new poses in ag[]), then phase 3
+// and the block writes.  0 = everything.
+template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR, bool HELP = false, int PART = 0>
 __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& out, const Src& src, const int G,
                                            const int a0, const int na, const int lane, unsigned char* base,
-                                           const LidarLayout& lay) {
+                                           const LidarLayout& lay, const unsigned long long redo = 0ull,
+                                           const unsigned long long alive_in = 0ull) {
     const int R = p.R;
     float4* ag = reinterpret_cast<float4*>(base + lay.ag);
     float2* dir = reinterpret_cast<float2*>(base + lay.dir);
@@ -2498,15 +2535,18 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
 #endif
 
     // ---- phase 1: alive agents of the group (compacted), beam directions
+    // (PART 1/2: the alive agents as the caller computed them -- in the early split
+    // the LiDAR wave starts before the car wave has staged the state)
     bool alv = false;
-    if (lane < na) alv = src.alive(a0 + lane);
-    const unsigned long long am = ballot(alv);
+    if (PART != 0) alv = (alive_in >> lane) & 1ull;
+    else if (lane < na) alv = src.alive(a0 + lane);
+    const unsigned long long am = PART != 0 ? alive_in : ballot(alv);
     const int nal = __popcll(am);
-    if (alv) {
+    if (PART == 0 && alv) {  // (PART 1/2: staged by the car wave / the caller)
         const int g = a0 + lane;
         ag[lane_rank(am)] = src.pose(g);
     }
-    if (!Src::kStaged && __popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
+    if (PART != 2 && !Src::kStaged && __popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
         for (int j = 0; j < na; ++j) {
             if ((am >> j) & 1ull) continue;
             if (out.lidar_u8) {  // compact gather format: the dead-agent code
@@ -2618,12 +2658,34 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         return r >= 0 ? r : -(k1 + MEV_LIDAR_NPR1) - 1;
 #endif
     };
+    // one pass of the early split's re-march: compacted agent j (PART 2)
+    auto pass1_one = [&](auto small, const int j) {
+        const float4 a = ag[j];
+        for (int b0 = 0; b0 < R; b0 += WAVE) {
+            const int b = b0 + lane;
+            const bool vb = b < R;
+            const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : (vb ? src.rel(b) : 0.0f));
+            float2 d;
+            const int r = setup(a, rel_b, small, d);
+            if (vb) {
+                dir[j * R + b] = d;
+                res[j * R + b] = r >= 0 ? r : -r - 1;
+            }
+            const bool pend = vb && r < 0;
+            const unsigned long long m = ballot(pend);
+            if (pend) queue[qn + lane_rank(m)] = (unsigned short)(j * R + b);
+            qn += __popcll(m);
+        }
+    };
     // ILP = 2: two agents per pass, two independent dependency chains (sincosf's
     // double polynomial, the safe distance, the probes) the compiler interleaves
     // (k_step, 128 VGPRs); ILP = 1 in k_lidar, whose 64-VGPR budget would spill
     auto phase1 = [&](auto small) {
+        if constexpr (PART == 2) {  // the respawned agents only
+            for (unsigned long long tm = redo; tm; tm &= tm - 1ull) pass1_one(small, __builtin_ctzll(tm));
+        } else {
         for (int j = 0; j < nal; j += ILP) {
-            if ((Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P1B >= 0 && 4 * j >= MEV_PRIO_P1B_AT * nal)
+            if (PART == 0 && (Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P1B >= 0 && 4 * j >= MEV_PRIO_P1B_AT * nal)
                 __builtin_amdgcn_s_setprio(MEV_PRIO_P1B < 0 ? 0 : MEV_PRIO_P1B);
             float4 a[ILP];
 #pragma unroll
@@ -2650,6 +2712,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 }
             }
         }
+        }
     };
     // |heading| < 100 for every agent (always, unless set_state() planted a
     // wild heading): |h + rel| < 120, the range of the branch-free sincosf
@@ -2664,7 +2727,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 4] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    if ((Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P2 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P2 < 0 ? 0 : MEV_PRIO_P2);
+    if (PART == 0 && (Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P2 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P2 < 0 ? 0 : MEV_PRIO_P2);
     // ---- phase 2: pooled road + screen march of the queued beams
     // (Lidar.cpp:31-48, first stop wins): LIDAR_NPR exact probes, then a jump
     // over the provably safe stretch after the last one
@@ -2797,6 +2860,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     }
 #endif
     wave_lds_sync();
+    if constexpr (PART == 1) return;  // the early split's road march: phase 3 after the car part
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 3  // timing-only: stop after phase 2
     if (Src::kBoxLds) return;
 #endif
@@ -3193,12 +3257,35 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // workgroup share its LDS; wave 0 runs cars_pre, then both pass a barrier and
 // wave 1 runs the LiDAR while wave 0 runs cars_post -- the two latency chains
 // after the car part overlap instead of following each other.
+//
+// ESPLIT (early split, large batches, one env per two-wave workgroup, 8 waves per
+// SIMD at <= 64 VGPRs): the LiDAR wave computes the agents' poses after Car::update
+// itself and marches the road (LiDAR phases 1-2) while the car wave runs the car
+// part; after barrier B (obstacle table, candidate masks, respawns) it re-marches
+// the respawned egos' beams and resolves the cars (phase 3) while the car wave runs
+// cars_post.  The car waves' latency-bound chains and the LiDAR waves'
+// VALU-bound phases then share each SIMD instead of following each other.
 #ifndef MEV_SPLIT_WPE
 #define MEV_SPLIT_WPE 4
 #endif
-template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false>
-__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? MEV_SPLIT_WPE : 4) void k_step(const SimParams* __restrict__ pp, StepInputs in,
-                                                                     Outputs out) {
+#ifndef MEV_ESPLIT_WPE
+#define MEV_ESPLIT_WPE 8
+#endif
+#ifndef MEV_PRIO_ESPLIT_ROAD  // the early split's LiDAR wave: kinematics and road march (its critical path)
+#define MEV_PRIO_ESPLIT_ROAD 3
+#endif
+#ifndef MEV_PRIO_ESPLIT_CARS  // the early split's car wave (slack until barrier B)
+#define MEV_PRIO_ESPLIT_CARS 2
+#endif
+#ifndef MEV_PRIO_ESPLIT_CARPHASE  // the LiDAR wave after barrier B (re-march, car pairs, block writes)
+#define MEV_PRIO_ESPLIT_CARPHASE 1
+#endif
+#ifndef MEV_ESPLIT_ILP
+#define MEV_ESPLIT_ILP 1
+#endif
+template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
+__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_ESPLIT_WPE : (SPLIT ? MEV_SPLIT_WPE : 4)) void k_step(
+    const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
     static_assert(!SPLIT || (!TRAFFIC && !MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE),
                   "split waves: the plain fused step");
     const SimParams& p = *pp;
@@ -3224,6 +3311,89 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? MEV_SPLIT_WPE : 4)
     NpcLDST<KM>* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
     if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
+    if constexpr (ESPLIT) {
+        static_assert(SPLIT && !TRAFFIC && NM > 0, "early split: two waves, no traffic");
+        const int lane = threadIdx.x & (WAVE - 1);
+        const int g0 = e * p.N;
+        // the wave's agent slots: PK envs of N agents (consecutive in the SoA), one LiDAR pool
+        const int NE = p.N;
+        const int NS = PK == 1 ? NE : (p.E - e < PK ? p.E - e : PK) * NE;
+        unsigned char* lbase = step_lds + sl.lidar;
+        const LidarLayout lay = FixedLayout<(NM ? NM : 1), 0>::lay;
+        if (wv == 0) {
+            // the car part (its path windows through VGPRs: the LiDAR wave owns the LiDAR
+            // area from the start), barrier B at the end of cars_pre
+            ES_STAMP(0);
+            __builtin_amdgcn_s_setprio(MEV_PRIO_ESPLIT_CARS);
+            CarsCtx cx = cars_pre<false, true, NpcLDST<KM>, PK, false, true>(p, in, out, e, el, nl);
+            cars_post<false, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
+            ES_STAMP(3);
+        } else {
+#ifdef MEV_X_ES_NOLIDAR  // timing-only: the LiDAR wave only passes the barrier
+            __syncthreads();
+            return;
+#endif
+            __builtin_amdgcn_s_setprio(MEV_PRIO_ESPLIT_ROAD);
+            // the beam offsets (this wave stages them in the early split) and, lane i < N,
+            // agent i's pose after Car::update exactly as cars_pre computes it (an env
+            // whose previous step ended starts from its spawns; a dead agent keeps its
+            // pose): the road march needs nothing else from the car part
+            for (int b = lane; b < p.R; b += WAVE) el.rel[b] = gmem(p.rel_angles)[b];
+            const bool on = lane < NS;
+            const int il = on ? lane : 0;
+            const int ee = PK == 1 ? e : e + il / NE;  // the slot's env
+            const uint32_t ug = (uint32_t)(g0 + il);
+            const bool pend = ldu(gmem(p.pending_reset), (uint32_t)ee) != 0;
+            const int route_l = ldu(egoi(p, EF_ROUTE), ug);
+            Kin k{ldu(egof(p, EF_X), ug), ldu(egof(p, EF_Y), ug), ldu(egof(p, EF_V), ug), ldu(egof(p, EF_H), ug),
+                  ldu(egof(p, EF_ACC), ug), ldu(egof(p, EF_STEER), ug)};
+            bool alive = ldu(gmem(p.ego.alive), ug) != 0;
+            const float a0 = ldu(gmem(in.actions), 2 * ug), a1 = ldu(gmem(in.actions), 2 * ug + 1);
+            if (in.auto_reset && pend) {
+                const int rid = reset_route(p, in.rng_counter, ee, PK == 1 ? il : il - (ee - e) * NE, route_l);
+                k = Kin{gmem(p.rt.spawn)[3 * rid], gmem(p.rt.spawn)[3 * rid + 1], 0.0f, gmem(p.rt.spawn)[3 * rid + 2],
+                        0.0f, 0.0f};
+                alive = true;
+            }
+            {
+                Kin ku = k;
+                float sH, cH;
+                car_update_heading(ku, a0, a1, in.dt);
+                sincosf(alive ? ku.h : k.h, &sH, &cH);
+                car_update_move(ku, cH, sH);
+                if (alive) k = ku;
+            }
+            alive = on && alive;
+            const unsigned long long am = ballot(alive);
+            float4* ag = reinterpret_cast<float4*>(lbase + lay.ag);
+            if (alive) ag[lane_rank(am)] = make_float4(k.x, k.y, k.h, __int_as_float(g0 + il));
+            wave_lds_sync();
+            ES_STAMP(4);
+            lidar_body<TAB, MEV_ESPLIT_ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true, 1>(
+                p, out, LidarSrcLds{el, g0}, NS, g0, NS, lane, lbase, lay, 0ull, am);
+            ES_STAMP(5);
+            __syncthreads();  // barrier B: the car part's obstacle table, candidate masks and respawns
+            ES_STAMP(6);
+            // respawned egos: their spawn poses into ag[] and their beams marched again
+            const unsigned rmask = (unsigned)el.envw[6];
+            const bool rs = alive && lane < 32 && ((rmask >> (lane & 31)) & 1u);
+            const unsigned long long rl = ballot(rs);
+            unsigned long long redo = 0ull;
+            if (rl != 0ull) {
+                if (rs) ag[lane_rank(am)] = make_float4(el.x[lane], el.y[lane], el.h[lane], __int_as_float(g0 + lane));
+                for (unsigned long long m = rl; m; m &= m - 1ull) {
+                    const int i = __builtin_ctzll(m);
+                    redo |= 1ull << __popcll(am & ((1ull << i) - 1ull));
+                }
+                wave_lds_sync();
+            }
+            __builtin_amdgcn_s_setprio(MEV_PRIO_ESPLIT_CARPHASE);
+            lidar_body<TAB, MEV_ESPLIT_ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true, 2>(
+                p, out, LidarSrcLds{el, g0}, NS, g0, NS, lane, lbase, lay, redo, am);
+            ES_STAMP(7);
+        }
+        return;
+    }
 #ifdef MEV_EXP_SKEW  // experiment: odd workgroups start MEV_EXP_SKEW x 64 x 127 cycles late
     if (blockIdx.x & 1) {
         for (int t = 0; t < MEV_EXP_SKEW; ++t) __builtin_amdgcn_s_sleep(127);
@@ -3448,8 +3618,14 @@ int step_pack(const SimParams& p) {
 #ifndef MEV_SPLIT_MAX_WG
 #define MEV_SPLIT_MAX_WG 2048
 #endif
+// the early split (k_step ESPLIT): mev_set_step_split(3); a workgroup's PK envs
+// (step_pack) with their beams in one LiDAR pool
+bool step_esplit(const SimParams& p) {
+    if (p.traffic || !fixed_fits<8, 0>(p) || p.step_split != 3) return false;
+    return step_pack(p) * p.N * p.R <= kPoolBeams && p.N <= 8;
+}
 bool step_split(const SimParams& p) {
-    if (p.traffic || !fixed_fits<8, 0>(p) || p.step_split == 1) return false;
+    if (p.traffic || !fixed_fits<8, 0>(p) || p.step_split == 1 || step_esplit(p)) return false;
     if (p.step_split == 2) return true;
     const int pk = step_pack(p);
     return (p.E + pk - 1) / pk <= MEV_SPLIT_MAX_WG;
@@ -3472,6 +3648,14 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         const int pk = step_pack(p);
         const int wg = (p.E + pk - 1) / pk;
         if constexpr (!MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE)  // (experiment builds: no split)
+        if (step_esplit(p)) {  // early split: a car wave and a LiDAR wave per workgroup
+            if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            return;
+        }
+        if constexpr (!MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE)
         if (step_split(p)) {  // two waves per workgroup (<= 4 waves per SIMD)
             if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);

@@ -21,12 +21,18 @@ META = dict(rays=RAYS, obs_dim=31 + RAYS, num_lanes=3, n_agents=N, use_team=True
             density=0.5, reward=[10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2])
 
 
-def test_bench_workload_sampled_envs_match_oracle(mev):
+@pytest.mark.parametrize("split", [0, 3])
+def test_bench_workload_sampled_envs_match_oracle(mev, split):
+    """split 0: the bench's automatic choice (one wave per env); 3: the early split
+    (a car wave and a LiDAR wave per env, the LiDAR's road march started after the
+    kinematics, respawned egos re-marched)."""
     import torch
 
     h = mev.Handle(num_envs=E, num_agents=N, lidar_rays=RAYS, use_team_reward=1, respawn_enabled=1,
                    max_steps=MAXS, seed=0, device=0)
+    h.set_step_split(split)
     assert h.step_kernel() == 2, "the bench size runs the fused k_step"
+    assert h.step_split() == (2 if split == 3 else 0)
     torch.cuda.set_device(0)
     stream = torch.cuda.current_stream(0)
     h.set_stream(stream.cuda_stream)

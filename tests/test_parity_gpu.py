@@ -70,12 +70,14 @@ def test_golden_scenario_packed_waves(mev, name, pack):
     assert not bad, bad
 
 
-@pytest.mark.parametrize("split", [1, 2])
+@pytest.mark.parametrize("split", [1, 2, 3])
 @pytest.mark.parametrize("name", [n for n in SINGLE if not G.load(n)["meta"]["traffic"]])
 def test_golden_scenario_split_waves(mev, name, split):
     """Each non-traffic golden on the fused kernel with one wave per workgroup
-    (split 1) and with the car part and the LiDAR in two waves (split 2) -- the
-    small-batch default, forced off and on here; both bit-exact."""
+    (split 1), with the car part and the LiDAR in two waves (split 2) -- the
+    small-batch default, forced off and on here -- and with the early split
+    (3: the LiDAR wave marches the road from the poses after the kinematics; envs
+    whose beams exceed one 512-beam pool take the automatic choice); all bit-exact."""
     (rep,) = G.replay(mev, name, kernel=2, split=split)
     assert rep.ok, f"{name}: {rep.mismatches[:5]} (steps checked {rep.steps})"
 

@@ -21,7 +21,7 @@ def _warm_state(mev, steps=60, seed=0, **kw):
     h = _handle(mev, **kw)
     rng = np.random.default_rng(seed)
     for _ in range(steps):
-        h.step(rng.uniform(-1, 1, (E, N, 2)).astype(np.float32))
+        h.step(rng.uniform(-1, 1, (E, h.N, 2)).astype(np.float32))
     st = h.get_state()
     h.close()
     return st
@@ -68,6 +68,42 @@ def test_fused_and_two_kernel_paths_agree_full_size(mev, rays):
     s1, s2 = hs[0].get_state(), hs[1].get_state()
     for k in s1:
         assert np.array_equal(s1[k], s2[k]), k
+    for h in hs:
+        h.close()
+
+
+@pytest.mark.parametrize("n,rays,pack", [(8, 64, 1), (4, 128, 1), (2, 64, 1), (1, 64, 2), (2, 64, 4), (1, 64, 8)])
+def test_early_split_agrees_full_size(mev, n, rays, pack):
+    """The early split (mev_set_step_split(3): a car wave and a LiDAR wave per env,
+    the LiDAR's road march started right after the kinematics, respawned egos'
+    beams marched again after the car part) == one wave per env == k_cars +
+    k_lidar, bit for bit, step after step, with auto-reset and respawns in the
+    window (4096 envs; 8 x 64 is the bench's config 3; with `pack` envs per workgroup
+    the LiDAR wave serves all their agents, e.g. config 2 at 2 envs)."""
+    st = _warm_state(mev, seed=8, num_agents=n, lidar_rays=rays)
+    rng = np.random.default_rng(9)
+    hs = []
+    for kernel, split, pk in ((1, 0, 1), (2, 1, 1), (2, 3, pack)):
+        h = _handle(mev, num_agents=n, lidar_rays=rays, max_steps=70)
+        h.set_step_kernel(kernel)
+        h.set_step_pack(pk)
+        h.set_step_split(split)
+        h.set_state(st)
+        hs.append(h)
+    assert hs[2].step_split() == 2 and hs[1].step_split() == 0
+    assert hs[2].step_pack() == pack
+    respawns = 0
+    for t in range(120):
+        a = rng.uniform(-1, 1, (E, n, 2)).astype(np.float32)
+        o = [h.step(a, auto_reset=True) for h in hs]
+        for k in o[0]:
+            assert np.array_equal(o[0][k], o[1][k]), (t, k)
+            assert np.array_equal(o[0][k], o[2][k]), (t, k)
+        respawns += int(np.isin(o[2]["status"], (3, 4, 5)).sum())
+    s = [h.get_state() for h in hs]
+    for k in s[0]:
+        assert np.array_equal(s[0][k], s[2][k]), k
+    assert respawns > 100, respawns  # crashed egos respawn: the LiDAR wave's re-march ran
     for h in hs:
         h.close()
 

@@ -92,6 +92,11 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                # the split kernel (car wave + LiDAR wave per workgroup) with 8 / 6 waves per SIMD
                "split8": ["-DMEV_SPLIT_WPE=8"], "split8i1": ["-DMEV_SPLIT_WPE=8", "-DMEV_PHASE1_ILP=1"],
                "split6": ["-DMEV_SPLIT_WPE=6"], "split5": ["-DMEV_SPLIT_WPE=5"],
+               # the early split (mev_set_step_split(3)) without the car part's round-A group loads
+               "eswpe6": ["-DMEV_ESPLIT_WPE=6"],
+               "esilp2": ["-DMEV_ESPLIT_ILP=2"], "esroad2": ["-DMEV_PRIO_ESPLIT_ROAD=2"], "escars3": ["-DMEV_PRIO_ESPLIT_CARS=3"],
+               "escars1": ["-DMEV_PRIO_ESPLIT_CARS=1"], "escp0": ["-DMEV_PRIO_ESPLIT_CARPHASE=0"], "x_es_nolidar": ["-DMEV_X_ES_NOLIDAR"],
+               "stampses": ["-DMEV_STAMPS_ES"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
                "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 
