@@ -153,6 +153,7 @@ int step_pack(const SimParams& p);
 // whether the fused path runs two waves per workgroup (car part / LiDAR overlap)
 bool step_split(const SimParams& p);
 bool step_esplit(const SimParams& p);
+int esplit_pack(const SimParams& p);
 // ev (nullable): three events recorded before k_cars, between k_cars and k_lidar, after k_lidar
 // (with k_step: before it, and twice after it)
 // dp: a device copy of p (k_step reads its parameters through it)

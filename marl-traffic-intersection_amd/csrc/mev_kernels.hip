@@ -3604,6 +3604,7 @@ int step_kernel_for(const SimParams& p) {
 // envs per wave (1024 waves, one per SIMD) 194 M (profiles/r2_pack_sweep.txt).
 int step_pack(const SimParams& p) {
     if (p.traffic || !fixed_fits<8, 0>(p)) return 1;
+    if (step_esplit(p)) return esplit_pack(p);
     int pk = p.step_pack;
     if (pk != 1 && pk != 2 && pk != 4 && pk != 8) {
         pk = 4;
@@ -3618,11 +3619,33 @@ int step_pack(const SimParams& p) {
 #ifndef MEV_SPLIT_MAX_WG
 #define MEV_SPLIT_MAX_WG 2048
 #endif
-// the early split (k_step ESPLIT): mev_set_step_split(3); a workgroup's PK envs
-// (step_pack) with their beams in one LiDAR pool
+// Envs per workgroup of the early split (k_step ESPLIT; 0: it does not apply).  An
+// explicit mev_set_step_pack is kept (reduced to <= 8 agent slots) when the slots'
+// beams fit one 512-beam LiDAR pool.  Automatic: 4 envs while their beams stay
+// <= 256 and >= 1024 workgroups remain, else 2 envs within one pool and >= 1024
+// workgroups, else 0 (the automatic choice then keeps one wave per env / the plain
+// split; mev_set_step_split(3) forces one env per workgroup at 8 waves per SIMD).
+// Measured against the plain split's best, one MI355X (profiles/r3_esplit_shapes.txt):
+// 4096 x 1 x 64 beams (config 2) 13.3 -> 11.6 us per step at 4 envs, 4096 x 4 x 64
+// 24.1 -> 22.0 at 2, 2048 x 1 x 64 12.4 -> 10.0 at 2, 4096 x 1 x 128 15.5 -> 14.4 at 2.
+int esplit_pack(const SimParams& p) {
+    if (p.traffic || !fixed_fits<8, 0>(p) || p.N > 8) return 0;
+    const int nr = p.N * p.R;
+    int pk = p.step_pack;
+    if (pk == 1 || pk == 2 || pk == 4 || pk == 8) {
+        while (pk > 1 && pk * p.N > 8) pk /= 2;
+        return pk * nr <= kPoolBeams ? pk : 0;
+    }
+    if (4 * p.N <= 8 && 4 * nr <= kPoolBeams / 2 && p.E / 4 >= 1024) return 4;
+    if (2 * p.N <= 8 && 2 * nr <= kPoolBeams && p.E / 2 >= 1024) return 2;
+    return p.step_split == 3 && nr <= kPoolBeams ? 1 : 0;
+}
+// the early split: automatic (mode 0) where esplit_pack finds >= 2 envs per
+// workgroup, or forced (mode 3)
 bool step_esplit(const SimParams& p) {
-    if (p.traffic || !fixed_fits<8, 0>(p) || p.step_split != 3) return false;
-    return step_pack(p) * p.N * p.R <= kPoolBeams && p.N <= 8;
+    if (p.step_split == 1 || p.step_split == 2) return false;
+    const int pk = esplit_pack(p);
+    return p.step_split == 3 ? pk > 0 : pk >= 2;
 }
 bool step_split(const SimParams& p) {
     if (p.traffic || !fixed_fits<8, 0>(p) || p.step_split == 1 || step_esplit(p)) return false;

@@ -146,7 +146,20 @@ def test_random_states_match_oracle_packed_waves(mev, cfg, pack):
     _random_states_vs_oracle(mev, cfg, 2, pack)
 
 
-def _random_states_vs_oracle(mev, cfg, kernel, pack=0):
+@pytest.mark.parametrize("pack", [1, 2, 4])
+@pytest.mark.parametrize("cfg", [c for c in CONFIGS if not c.get("traffic")],
+                         ids=[c["name"] for c in CONFIGS if not c.get("traffic")])
+def test_random_states_match_oracle_early_split(mev, cfg, pack):
+    """The early split (mev_set_step_split(3): the LiDAR wave computes the poses
+    after Car::update itself and marches the road beside the car part), `pack`
+    envs per workgroup, each env from its own random state: every output and the
+    state after every step bit-exact against the oracle."""
+    if pack > 1 and pack * cfg["n"] > 8:
+        pytest.skip("fewer agent slots than the pack: the same run as a smaller pack")
+    _random_states_vs_oracle(mev, cfg, 2, pack, split=3)
+
+
+def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0):
     rng = np.random.default_rng(zlib.crc32(cfg["name"].encode()))
     E, T = 24, 50
     n, lanes = cfg["n"], cfg.get("lanes", 3)
@@ -161,6 +174,11 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0):
     if pack:
         h.set_step_pack(pack)
         assert h.step_pack() == (pack if pack * n <= 8 else max(1, 8 // n)), h.step_pack()
+    if split:
+        h.set_step_split(split)
+        if h.step_split() != 2:  # the early split needs the slots' beams in one 512-beam pool
+            assert h.step_pack() * n * R_ > 512, (h.step_pack(), n, R_)
+            pytest.skip("beams of the workgroup's slots exceed one LiDAR pool")
     table = ROUTES2 if lanes == 2 else ROUTES3
     st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0))
     h.set_traffic_routes(troutes)
