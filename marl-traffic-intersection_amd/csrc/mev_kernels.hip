@@ -1330,7 +1330,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
 // ego features, path look-ahead, 5 nearest alive neighbours (egos first, then
 // NPCs; stable by distance == libstdc++ insertion sort for <= 16 candidates).
 template <bool TRAFFIC, class EL, class NL>
-__device__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt, float tx,
+__device__ __forceinline__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt, float tx,
                                   float ty, float* row, bool pad = true) {
     const float x = el.x[i], y = el.y[i], v = el.v[i], h = el.h[i];
     row[0] = x / float(WIDTH);
@@ -1391,7 +1391,7 @@ __device__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const
 }
 
 template <bool TRAFFIC, class EL, class NL>
-__device__ void write_obs_head(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt,
+__device__ __forceinline__ void write_obs_head(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt,
                                const float* path, int pidx, float* row) {
     int tidx = pidx + 10;
     if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
@@ -1533,9 +1533,16 @@ struct CarsCtx {
 // computes the poses after the kinematics itself and marches the road while this
 // wave runs the car part; this wave leaves the beam offsets (el.rel) to it, records
 // the respawned egos (el.envw[6]) at the end and passes workgroup barrier B.
-template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false>
+// Hook: called right after the kinematics (the poses after Car::update in LDS); k_step's
+// mixed order runs the LiDAR road march there (RoadHook).  Hook::kMarks: record the
+// respawned egos in el.envw[6] as the early split does.
+struct NoHook {
+    static constexpr bool kMarks = false;
+    __device__ __forceinline__ void operator()() const {}
+};
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false, class Hook = NoHook>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
-                                            const CarsLDS& el, NL* nl) {
+                                            const CarsLDS& el, NL* nl, const Hook& hook = Hook{}) {
     static_assert(!ESPLIT || (FUSED && !TRAFFIC), "early split: k_step without traffic");
     static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
@@ -1914,6 +1921,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     }
     wave_lds_sync();
     ES_STAMP(1);
+    hook();
 
     STAMP(2);
     // one ego per env and no NPCs: no car can touch another, and no LiDAR beam can
@@ -1999,7 +2007,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             el.tgx[i] = el.t10x[i]; el.tgy[i] = el.t10y[i];  // path[min(0 + 10, 159)]
         }
     }
-    if constexpr (ESPLIT) {  // the respawned egos (agent slots), for the LiDAR wave after barrier B
+    if constexpr (ESPLIT || Hook::kMarks) {  // the respawned egos (agent slots), for the LiDAR after barrier B
         const uint8_t st = el.status[tid < N ? tid : 0];
         const bool rs = tid < N && p.respawn && el.alive[tid < N ? tid : 0] && el.done[tid < N ? tid : 0] &&
                         (st == ST_CRASH_CAR || st == ST_CRASH_WALL || st == ST_CRASH_LINE);
@@ -3258,6 +3266,48 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // wave 1 runs the LiDAR while wave 0 runs cars_post -- the two latency chains
 // after the car part overlap instead of following each other.
 //
+// Mixed order (k_step with one wave per env, MEV_MIX): the four waves of a SIMD start
+// together and would all run their latency-bound car parts at once, then all their
+// VALU-bound LiDAR phases.  Every second residency slot (blockIdx >> 10 odd: the
+// dispatcher deals the first 1024 workgroups one per SIMD) runs the road march
+// (LiDAR phases 1-2) right after the kinematics instead, inside cars_pre (RoadHook),
+// then the rest of the car part, the respawned egos' re-march and the car pairs --
+// so each SIMD mixes two waves' car parts with two waves' LiDAR work.
+#ifndef MEV_MIX
+#define MEV_MIX 0
+#endif
+#ifndef MEV_MIX_SHIFT
+#define MEV_MIX_SHIFT 10
+#endif
+#ifndef MEV_PRIO_MIX_ROAD
+#define MEV_PRIO_MIX_ROAD 1
+#endif
+template <bool TAB, int ILP>
+struct RoadHook {
+    static constexpr bool kMarks = true;
+    const SimParams& p;
+    Outputs out;  // (by value: a reference to the kernel's local structs kept them in scratch memory)
+    CarsLDS el;
+    unsigned char* lbase;
+    LidarLayout lay;
+    int g0;
+    bool on;
+    __device__ __forceinline__ void operator()() const {
+        if (!on) return;
+        const int lane = threadIdx.x & (WAVE - 1);
+        const int N = p.N;
+        const bool alv = lane < N && el.alive[lane < N ? lane : 0] != 0;
+        const unsigned long long am = ballot(alv);
+        float4* ag = reinterpret_cast<float4*>(lbase + lay.ag);
+        if (alv) ag[lane_rank(am)] = make_float4(el.x[lane], el.y[lane], el.h[lane], __int_as_float(g0 + lane));
+        wave_lds_sync();
+        __builtin_amdgcn_s_setprio(MEV_PRIO_MIX_ROAD);
+        lidar_body<TAB, ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true, 1>(p, out, LidarSrcLds{el, g0}, N, g0, N, lane, lbase,
+                                                                       lay, 0ull, am);
+        __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
+    }
+};
+
 // ESPLIT (early split, large batches, one env per two-wave workgroup, 8 waves per
 // SIMD at <= 64 VGPRs): the LiDAR wave computes the agents' poses after Car::update
 // itself and marches the road (LiDAR phases 1-2) while the car wave runs the car
@@ -3402,6 +3452,46 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_
 #ifdef MEV_EXP_SKEWPRIO  // experiment: odd workgroups run the car part one priority level lower
     if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS - 1);
 #endif
+    constexpr bool MIXABLE = MEV_MIX && !TRAFFIC && !SPLIT && PK == 1 && NM > 0 && !MEV_FUSED_STAGED &&
+                             !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE;
+    if constexpr (MIXABLE) if (p.N * p.R <= kPoolBeams) {  // one LiDAR pool per env
+        const bool border = (blockIdx.x >> MEV_MIX_SHIFT) & 1;
+        const int lane = threadIdx.x & (WAVE - 1);
+        const int g0 = e * p.N;
+        unsigned char* lbase = step_lds + sl.lidar;
+        const LidarLayout lay = FixedLayout<(NM ? NM : 1), 0>::lay;
+        const RoadHook<TAB, MEV_PHASE1_ILP> hook{p, out, el, lbase, lay, g0, border};
+        CarsCtx cx = cars_pre<false, true, NpcLDST<KM>, 1, (MEV_EARLY_WINDOW && NM > 0), false, RoadHook<TAB, MEV_PHASE1_ILP>>(
+            p, in, out, e, el, nl, hook);
+        wave_lds_sync();
+        cars_post<false, true, NpcLDST<KM>, 1>(p, out, e, el, nl, cx);
+        wave_lds_sync();
+        if (border) {
+            // the respawned egos' spawn poses into ag[] and their beams marched again, then the car pairs
+            const unsigned rmask = (unsigned)el.envw[6];
+            const bool alive = lane < p.N && el.alive[lane < p.N ? lane : 0] != 0;
+            const unsigned long long am = ballot(alive);
+            const bool rs = alive && lane < 32 && ((rmask >> (lane & 31)) & 1u);
+            const unsigned long long rl = ballot(rs);
+            unsigned long long redo = 0ull;
+            if (rl != 0ull) {
+                float4* ag = reinterpret_cast<float4*>(lbase + lay.ag);
+                if (rs) ag[lane_rank(am)] = make_float4(el.x[lane], el.y[lane], el.h[lane], __int_as_float(g0 + lane));
+                for (unsigned long long m = rl; m; m &= m - 1ull) {
+                    const int i = __builtin_ctzll(m);
+                    redo |= 1ull << __popcll(am & ((1ull << i) - 1ull));
+                }
+                wave_lds_sync();
+            }
+            lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true, 2>(
+                p, out, LidarSrcLds{el, g0}, p.N, g0, p.N, lane, lbase, lay, redo, am);
+        } else {
+            __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
+            lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true>(
+                p, out, LidarSrcLds{el, g0}, p.N, g0, p.N, lane, lbase, lay);
+        }
+        return;
+    }
     CarsCtx cx{};
     if (wv == 0) cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK, (MEV_EARLY_WINDOW && !TRAFFIC && NM > 0)>(p, in, out, e, el, nl);
     if (SPLIT) __syncthreads();

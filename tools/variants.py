@@ -97,6 +97,10 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "esilp2": ["-DMEV_ESPLIT_ILP=2"], "esroad2": ["-DMEV_PRIO_ESPLIT_ROAD=2"], "escars3": ["-DMEV_PRIO_ESPLIT_CARS=3"],
                "escars1": ["-DMEV_PRIO_ESPLIT_CARS=1"], "escp0": ["-DMEV_PRIO_ESPLIT_CARPHASE=0"], "x_es_nolidar": ["-DMEV_X_ES_NOLIDAR"],
                "stampses": ["-DMEV_STAMPS_ES"],
+               # mixed order: odd residency slots march the road right after the kinematics
+               "mix": ["-DMEV_MIX=1"], "mixp0": ["-DMEV_MIX=1", "-DMEV_PRIO_MIX_ROAD=0"],
+               "mixp2": ["-DMEV_MIX=1", "-DMEV_PRIO_MIX_ROAD=2"], "mixs11": ["-DMEV_MIX=1", "-DMEV_MIX_SHIFT=11"],
+               "mixs0": ["-DMEV_MIX=1", "-DMEV_MIX_SHIFT=0"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
                "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 
