@@ -626,9 +626,40 @@ __device__ __forceinline__ float npc_throttle(float acc_thr, float min_conflict)
 #ifndef MEV_NPC_KEEPSKIP  // no compaction pass when no NPC is erased
 #define MEV_NPC_KEEPSKIP 1
 #endif
+// The NPC state write-back at the end of k_step (1) or of the NPC phase (0), and the
+// NPC-aware deal's append at the end of k_step (1) or after the car part (0).
+// (the timing-only stop builds return early: they keep both where the car part ends)
+#if defined(MEV_EXP_STOP)
+#define MEV_NPC_DEFER_WB 0
+#define MEV_DEAL_LATE 0
+#endif
+// Measured (profiles/r3_ab_deferwb.txt): config 4 33.1 us with both where the car part
+// ends, 33.4 with both at the end -- not a drain on the critical path; off.
+#ifndef MEV_NPC_DEFER_WB
+#define MEV_NPC_DEFER_WB 0
+#endif
+#ifndef MEV_DEAL_LATE
+#define MEV_DEAL_LATE 0
+#endif
+// the surviving NPCs' state back to HBM (npc_phase's result, in nl)
+template <class NL>
+__device__ __forceinline__ void npc_writeback(const SimParams& p, int e, const NL& nl, int newcnt, int lane) {
+    const int K = p.K;
+    if (lane < newcnt) {
+        const int g = e * K + lane;
+        npcf(p, NF_X)[g] = nl.x[lane]; npcf(p, NF_Y)[g] = nl.y[lane]; npcf(p, NF_V)[g] = nl.v[lane]; npcf(p, NF_H)[g] = nl.h[lane];
+        npcf(p, NF_ACC)[g] = nl.acc[lane]; npcf(p, NF_STEER)[g] = nl.steer[lane]; npci(p, NF_PIDX)[g] = nl.pidx[lane];
+        npci(p, NF_ROUTE)[g] = nl.route[lane]; npci(p, NF_INTENT)[g] = nl.intent[lane]; gmem(p.npc.alive)[g] = 1;
+    }
+    if (lane == 0) gmem(p.npc.count)[e] = newcnt;
+}
+
+// store: write the NPC state back here (k_cars); k_step defers it to its end
+// (npc_writeback), because on gfx950 vmcnt counts stores too: the first wait for
+// a later load (the egos' path windows) would also wait for these stores to land.
 template <class NL>
 __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NL& nl, int lane,
-                          const float* ego_x, const float* ego_y, const NpcRegs& nr) {
+                          const float* ego_x, const float* ego_y, const NpcRegs& nr, const bool store = true) {
     const int K = p.K;
 #ifdef MEV_STAMPS_N
     unsigned long long nt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1308,14 +1339,8 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         wave_lds_sync();
     }
     // store back + corners of the survivors (for ego-NPC SAT)
-    if (lane < newcnt) {
-        const int g = e * K + lane;
-        npcf(p, NF_X)[g] = nl.x[lane]; npcf(p, NF_Y)[g] = nl.y[lane]; npcf(p, NF_V)[g] = nl.v[lane]; npcf(p, NF_H)[g] = nl.h[lane];
-        npcf(p, NF_ACC)[g] = nl.acc[lane]; npcf(p, NF_STEER)[g] = nl.steer[lane]; npci(p, NF_PIDX)[g] = nl.pidx[lane];
-        npci(p, NF_ROUTE)[g] = nl.route[lane]; npci(p, NF_INTENT)[g] = nl.intent[lane]; gmem(p.npc.alive)[g] = 1;
-        car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
-    }
-    if (lane == 0) gmem(p.npc.count)[e] = newcnt;
+    if (MEV_NPC_DEFER_WB == 0 || store) npc_writeback(p, e, nl, newcnt, lane);
+    if (lane < newcnt) car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
     wave_lds_sync();
 #ifdef MEV_STAMPS_N
     NT(7);  // collisions, erase, store
@@ -1712,7 +1737,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
 
     STAMP(0);
     int ncnt = 0;
-    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg);
+    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg, !FUSED);
 #ifndef MEV_TRAFFIC_PRIO  // fused traffic: the rest of the step at a level by the env's NPC count (0: MEV_PRIO_CARS; 3: +1.4 % at config 4)
 #define MEV_TRAFFIC_PRIO 3
 #endif
@@ -3266,6 +3291,30 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // wave 1 runs the LiDAR while wave 0 runs cars_post -- the two latency chains
 // after the car part overlap instead of following each other.
 //
+// The NPC-aware deal of the next step (traffic, §3.1c): this env joins its list's
+// class for step t + 1 (an env that ended restarts without NPCs after its
+// auto-reset).  At the end of k_step (MEV_DEAL_LATE): waiting for the atomic's
+// returned value is a vmcnt wait, which on gfx950 also waits for every store
+// issued before it (the car part's outputs and state write-back).
+template <bool TRAFFIC>
+__device__ __forceinline__ void deal_append(const SimParams& p, const StepInputs& in, const CarsCtx& cx, const int e) {
+    if constexpr (TRAFFIC) {
+        if (!(in.deal & 2)) return;
+        const int lane0 = threadIdx.x & (WAVE - 1);
+        const int x = (int)blockIdx.x & (kDealLists - 1);
+        const int nxt = in.deal_ring == 2 ? 0 : in.deal_ring + 1;
+        if (lane0 == 0) {
+            const int c = (in.auto_reset && cx.ended) ? 0 : (cx.ncnt < kDealClasses - 1 ? cx.ncnt : kDealClasses - 1);
+            const int slot = atomicAdd(p.deal_cnt + (size_t)nxt * kDealRingInts + (x * kDealClasses + c) * kDealPad, 1);
+            gmem(p.deal_order)[((size_t)x * kDealClasses + c) * p.E + slot] = e;
+        }
+        if (blockIdx.x == 0 && lane0 < kDealLists * kDealClasses) {  // clear ring t + 2
+            const int clr = nxt == 2 ? 0 : nxt + 1;
+            gmem(p.deal_cnt)[(size_t)clr * kDealRingInts + lane0 * kDealPad] = 0;
+        }
+    }
+}
+
 // Mixed order (k_step with one wave per env, MEV_MIX): the four waves of a SIMD start
 // together and would all run their latency-bound car parts at once, then all their
 // VALU-bound LiDAR phases.  Every second residency slot (blockIdx >> 10 odd: the
@@ -3502,22 +3551,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_
         wave_lds_sync();
     }
 #endif
-    if (TRAFFIC && (in.deal & 2)) {
-        // the NPC-aware deal of the next step: this env joins its list's class for
-        // step t + 1 (an env that ended restarts without NPCs after its auto-reset)
-        const int lane0 = threadIdx.x & (WAVE - 1);
-        const int x = (int)blockIdx.x & (kDealLists - 1);
-        const int nxt = in.deal_ring == 2 ? 0 : in.deal_ring + 1;
-        if (lane0 == 0) {
-            const int c = (in.auto_reset && cx.ended) ? 0 : (cx.ncnt < kDealClasses - 1 ? cx.ncnt : kDealClasses - 1);
-            const int slot = atomicAdd(p.deal_cnt + (size_t)nxt * kDealRingInts + (x * kDealClasses + c) * kDealPad, 1);
-            gmem(p.deal_order)[((size_t)x * kDealClasses + c) * p.E + slot] = e;
-        }
-        if (blockIdx.x == 0 && lane0 < kDealLists * kDealClasses) {  // clear ring t + 2
-            const int clr = nxt == 2 ? 0 : nxt + 1;
-            gmem(p.deal_cnt)[(size_t)clr * kDealRingInts + lane0 * kDealPad] = 0;
-        }
-    }
+    if (MEV_DEAL_LATE == 0) deal_append<TRAFFIC>(p, in, cx, e);
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 0  // (stop0 keeps the deal: the env order stays the product's)
     return;
 #endif
@@ -3547,6 +3581,10 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_
         cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
     }
     if (MEV_WB_LATE && !MEV_FUSED_STAGED) ego_writeback(p, e, p.N, NS, el, cx.do_reset, lane);
+    if constexpr (TRAFFIC) {
+        if (MEV_NPC_DEFER_WB) npc_writeback(p, e, *nl, cx.ncnt, lane);  // (deferred: see npc_phase)
+        if (MEV_DEAL_LATE) deal_append<TRAFFIC>(p, in, cx, e);
+    }
     if (MEV_FUSED_STAGED) {
         wave_lds_sync();
         fused_store<TAB>(p, out, e, el, reinterpret_cast<const int*>(lbase + lay.res), lane);

@@ -101,6 +101,10 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "mix": ["-DMEV_MIX=1"], "mixp0": ["-DMEV_MIX=1", "-DMEV_PRIO_MIX_ROAD=0"],
                "mixp2": ["-DMEV_MIX=1", "-DMEV_PRIO_MIX_ROAD=2"], "mixs11": ["-DMEV_MIX=1", "-DMEV_MIX_SHIFT=11"],
                "mixs0": ["-DMEV_MIX=1", "-DMEV_MIX_SHIFT=0"],
+               # traffic: the NPC write-back and the deal's append at the end of k_step (product: where the
+               # NPC phase / the car part ends)
+               "npcwblate": ["-DMEV_NPC_DEFER_WB=1"], "deallate": ["-DMEV_DEAL_LATE=1"],
+               "bothlate": ["-DMEV_NPC_DEFER_WB=1", "-DMEV_DEAL_LATE=1"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
                "exp_badrange": ["-DMEV_EXP_BADRANGE"]}
 
