@@ -252,6 +252,21 @@ int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave);
  * nothing in the reference. */
 int mev_set_step_split(mev_handle* h, int32_t mode);
 int mev_get_step_split(const mev_handle* h, int32_t* split);
+/* Host-mode steps as a persistent step server (results are identical either
+ * way).  A step with host buffers (no MEV_DEVICE_PTRS) of a small handle (<= 64
+ * envs, outputs <= 256 KB, the fused kernel, no traffic above one ego / 32 NPC
+ * slots) is answered by a kernel that stays resident between steps (k_serve):
+ * the host posts the step in a mailbox of pinned memory and the kernel answers
+ * once its outputs are there -- a PCIe round trip instead of a kernel launch and
+ * a stream synchronisation.  The kernel leaves after `idle` ms without a step
+ * (MEV_SERVE_IDLE_MS, default 50) and is launched again by the next one; every
+ * other call on the handle stops it first.  mode: 0 = off, 1 = automatic
+ * (default; MEV_NO_SERVE=1 in the environment turns it off).  mev_serve_stats:
+ * steps served, server launches, whether one is running.  Replaces nothing in the
+ * reference (its env.py steps one IntersectionEnv per call on the CPU,
+ * cpp/bindings.cpp:53-55). */
+int mev_set_serve(mev_handle* h, int32_t mode);
+int mev_serve_stats(const mev_handle* h, uint64_t* steps, uint64_t* launches, int32_t* running);
 
 /* ---- Multi-GPU: the per-step RCCL gather of the stacked outputs ----------
  * envs are sharded over the GPUs of a node, one process and

@@ -41,7 +41,7 @@ EXPORTED = (
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
     "mev_kernel_timing", "mev_kernel_times", "mev_set_reset_routes", "mev_snapshot_size", "mev_snapshot",
     "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel", "mev_set_step_pack", "mev_get_step_pack",
-    "mev_set_step_split", "mev_get_step_split",
+    "mev_set_step_split", "mev_get_step_split", "mev_set_serve", "mev_serve_stats",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
     "mev_gather_wait", "mev_output_dlpack", "mev_packed_layout2", "mev_set_gather_format", "mev_lidar_decode_table",
 )
@@ -151,6 +151,8 @@ def load_library(variant: str = None):
     L.mev_get_step_pack.argtypes = [_vp, i32p]
     L.mev_set_step_split.argtypes = [_vp, ctypes.c_int32]
     L.mev_get_step_split.argtypes = [_vp, i32p]
+    L.mev_set_serve.argtypes = [_vp, ctypes.c_int32]
+    L.mev_serve_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), i32p]
     L.mev_configure.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     L.mev_configure_traffic.argtypes = [_vp, ctypes.c_int32, ctypes.c_float]
     L.mev_set_reward.argtypes = [_vp, f32p]
@@ -580,6 +582,16 @@ class Handle:
         v = ctypes.c_int32()
         _check(self._lib.mev_get_step_split(self._h, ctypes.byref(v)))
         return int(v.value)
+
+    def set_serve(self, mode: int = 1):
+        """Host-mode steps through the persistent step server: 0 off, 1 automatic (results identical)."""
+        _check(self._lib.mev_set_serve(self._h, int(mode)))
+
+    def serve_stats(self) -> dict:
+        """Steps the persistent server answered, its launches, and whether one is running."""
+        st, la, ru = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int32()
+        _check(self._lib.mev_serve_stats(self._h, ctypes.byref(st), ctypes.byref(la), ctypes.byref(ru)))
+        return {"steps": int(st.value), "launches": int(la.value), "running": bool(ru.value)}
 
     def set_reset_routes(self, routes):
         """Draw every agent's route from `routes` at each reset (empty: fixed routes)."""

@@ -171,6 +171,7 @@ class IntersectionEnv:
         self.num_lanes = int(num_lanes)
         self._device = int(device)
         self._max_npcs = int(max_npcs)
+        self._paths = {}  # route id -> its 160 path points as (x, y) tuples (Car.path)
         self._use_team, self._respawn, self._max_steps = False, True, 2000
         self._traffic, self._density = False, 0.5
         self._reward = RewardConfig()
@@ -357,7 +358,10 @@ class IntersectionEnv:
             c.intention = int(get("intention", i))
             c.path_index = int(get("path_index", i))
             c._route = int(get("route", i))
-            c.path = [tuple(map(float, p)) for p in h.route_info(c._route)[0]]
+            path = self._paths.get(c._route)
+            if path is None:  # route tables are constant for the env's lane count: built once per route
+                path = self._paths[c._route] = [tuple(map(float, p)) for p in h.route_info(c._route)[0]]
+            c.path = list(path)
             if ego:
                 c.spawn_state = State(st["spawn_x"][0, i], st["spawn_y"][0, i], st["spawn_v"][0, i],
                                       st["spawn_heading"][0, i])

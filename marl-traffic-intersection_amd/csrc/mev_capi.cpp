@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <string>
@@ -154,11 +155,24 @@ struct mev_handle {
     uint8_t* pin_dev = nullptr; // its device address
     size_t pin_off[10] = {};    // actions, spawn, obs, reward, done, status, term, trunc, alive, step
     mev::Outputs pin_out{};     // device addresses of the pinned outputs
+    // Persistent step server (k_serve, mev_set_serve): host-mode steps of a small
+    // handle posted to a resident kernel through a mailbox in pinned memory
+    int serve_mode = 1;                 // 0 off, 1 automatic
+    mev::ServeBox* sbox = nullptr;      // host address of the mailbox (mapped, coherent)
+    mev::ServeBox* sbox_dev = nullptr;  // its device address
+    bool serve_running = false;         // an instance may be resident on `stream`
+    int serve_wg = 0;                   // its workgroups
+    uint32_t serve_seq = 0, serve_sid = 0, serve_epoch = 0;
+    uint64_t serve_steps = 0, serve_launches = 0;
+    uint8_t* gs_pin = nullptr;  // pinned staging of mev_get_state
+    size_t gs_cap = 0;
     ~mev_handle() {
         if (comm_stream) (void)hipStreamSynchronize(comm_stream);
         free_comm();
         free_timing();
         if (pin) (void)hipHostFree(pin);
+        if (sbox) (void)hipHostFree(sbox);
+        if (gs_pin) (void)hipHostFree(gs_pin);
         if (d_snap_stage) (void)hipFree(d_snap_stage);
         for (void* p : allocs) (void)hipFree(p);
         if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -166,6 +180,8 @@ struct mev_handle {
 };
 
 extern "C" {
+
+static int serve_stop(mev_handle* h);  // with mev_step: the resident step server leaves the stream
 
 const char* mev_last_error(void) { return g_err.c_str(); }
 int mev_abi_version(void) { return MEV_ABI_VERSION; }
@@ -421,6 +437,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
 int mev_destroy(mev_handle* h) {
     if (!h) return MEV_OK;
     (void)hipSetDevice(h->cfg.device);
+    (void)serve_stop(h);
     (void)hipStreamSynchronize(h->stream);
     delete h;
     return MEV_OK;
@@ -442,6 +459,7 @@ int mev_obs_dim(const mev_handle* h, int32_t* d) {
 int mev_set_stream(mev_handle* h, void* stream) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));  // order the switch after outstanding work
     h->stream = static_cast<hipStream_t>(stream);  // NULL = the legacy default stream
     return MEV_OK;
@@ -450,6 +468,7 @@ int mev_set_stream(mev_handle* h, void* stream) {
 int mev_use_own_stream(mev_handle* h) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->stream = h->own_stream;
     return MEV_OK;
@@ -458,6 +477,7 @@ int mev_use_own_stream(mev_handle* h) {
 int mev_debug_stamps(mev_handle* h, uint64_t* out) {
     if (!h || !out) return fail(MEV_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipMemcpyAsync(out, h->sp.debug, size_t(h->cfg.num_envs) * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return MEV_OK;
@@ -466,6 +486,7 @@ int mev_debug_stamps(mev_handle* h, uint64_t* out) {
 int mev_sync(mev_handle* h) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     return MEV_OK;
 }
@@ -571,6 +592,7 @@ int mev_set_ego_routes(mev_handle* h, const int32_t* routes) {
     for (size_t i = 0; i < EN; ++i)
         if (routes[i] < 0 || routes[i] >= h->nroutes) return fail(MEV_E_RANGE, "ego route id out of range");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipMemcpyAsync(h->sp.ego.route, routes, EN * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     return MEV_OK;
@@ -582,6 +604,7 @@ int mev_set_traffic_routes(mev_handle* h, const int32_t* routes, int32_t count) 
     for (int i = 0; i < count; ++i)
         if (routes[i] < 0 || routes[i] >= h->nroutes) return fail(MEV_E_RANGE, "traffic route id out of range");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     h->h_traffic.assign(routes, routes + count);
     if (count > 0)
         HIP_TRY(hipMemcpyAsync(h->d_traffic, routes, size_t(count) * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
@@ -635,6 +658,7 @@ static int copy_out(mev_handle* h, const mev::Outputs& src, float* obs, float* r
 int mev_reset(mev_handle* h, const uint8_t* env_mask, float* obs, uint32_t flags) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
     const uint8_t* d_mask = nullptr;
     if (env_mask) {
@@ -691,6 +715,146 @@ static bool pin_ready(mev_handle* h) {
     return true;
 }
 
+// ---- the persistent step server (k_serve; protocol in mev_kernels.h ServeBox) ----
+namespace {
+constexpr double kServeTimeoutMs = 10000.0;  // no answer within this: the call fails
+
+inline void cpu_relax() {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+}
+
+uint32_t serve_idle_ticks() {
+    static const uint32_t ms = [] {
+        const char* v = getenv("MEV_SERVE_IDLE_MS");
+        const int m = v ? atoi(v) : 50;
+        return (uint32_t)(m < 1 ? 1 : (m > 1000 ? 1000 : m));
+    }();
+    return ms * 100000u;  // s_memrealtime: 100 MHz
+}
+
+// post a command: the line's fields are written by the caller, then cmd, then seq (release)
+void serve_post(mev_handle* h, uint32_t cmd) {
+    volatile mev::ServeBox* b = h->sbox;
+    b->cmd = cmd;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    b->seq = ++h->serve_seq;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+}
+
+int serve_launch(mev_handle* h) {
+    mev::ServeArgs sa{};
+    sa.box = h->sbox_dev;
+    sa.actions = reinterpret_cast<const float*>(h->pin_dev + h->pin_off[0]);
+    sa.spawn_route = reinterpret_cast<const int32_t*>(h->pin_dev + h->pin_off[1]);
+    sa.epoch = ++h->serve_epoch;
+    sa.idle_ticks = serve_idle_ticks();
+    HIP_TRY(mev::launch_serve(h->sp, h->d_sp, sa, h->pin_out, h->stream));
+    h->serve_running = true;
+    h->serve_wg = h->sp.E;
+    ++h->serve_launches;
+    return MEV_OK;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
+
+// Stop a resident server (every other call on the handle does this first): post
+// STOP, wait until every workgroup has left, then the stream is free.
+static int serve_stop(mev_handle* h) {
+    if (!h->serve_running) return MEV_OK;
+    serve_post(h, mev::kServeStop);
+    volatile mev::ServeBox* b = h->sbox;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int w = 0; w < h->serve_wg; ++w)
+        while (b->exited[w] != h->serve_epoch) {
+            if (ms_since(t0) > kServeTimeoutMs) return fail(MEV_E_HIP, "step server: no stop within 10 s");
+            cpu_relax();
+        }
+    h->serve_running = false;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+// whether a host-mode step of h (pinned block ready) goes to the server
+static bool serve_wanted(mev_handle* h) {
+    static const bool off = [] { const char* v = getenv("MEV_NO_SERVE"); return v && v[0] == '1'; }();
+    if (off || h->serve_mode == 0 || !h->tev.empty() || !mev::serve_fits(h->sp)) return false;
+    if (h->sbox) return true;
+    void* hp = nullptr;
+    if (hipHostMalloc(&hp, sizeof(mev::ServeBox), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return false;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+        (void)hipHostFree(hp);
+        return false;
+    }
+    memset(hp, 0, sizeof(mev::ServeBox));
+    h->sbox = static_cast<mev::ServeBox*>(hp);
+    h->sbox_dev = static_cast<mev::ServeBox*>(dp);
+    return true;
+}
+
+// one step through the server: post it (launching an instance if none is
+// resident) and wait until every workgroup has answered.  A workgroup that left
+// (idle) without answering: the instance is stopped, the same step (same sid) is
+// posted again and a new instance launched; workgroups that had answered skip it.
+static int serve_step(mev_handle* h, const mev::StepInputs& in) {
+    volatile mev::ServeBox* b = h->sbox;
+    const uint32_t sid = ++h->serve_sid;
+    uint32_t u;
+    b->sid = sid;
+    memcpy(&u, &in.dt, 4);
+    b->dt = u;
+    memcpy(&u, &in.spawn_prob, 4);
+    b->spawn_prob = u;
+    b->auto_reset = (uint32_t)in.auto_reset;
+    b->spawn = in.spawn_route ? 1u : 0u;
+    b->rng_lo = (uint32_t)in.rng_counter;
+    b->rng_hi = (uint32_t)(in.rng_counter >> 32);
+    serve_post(h, mev::kServeStep);
+    if (!h->serve_running)
+        if (int r = serve_launch(h)) return r;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int w = 0; w < h->serve_wg; ++w) {
+        while (b->done[w] != sid) {
+            if (b->exited[w] == h->serve_epoch) {
+                std::atomic_thread_fence(std::memory_order_seq_cst);
+                if (b->done[w] == sid) break;  // answered, then left
+                if (int r = serve_stop(h)) return r;
+                serve_post(h, mev::kServeStep);  // the same step again
+                if (int r = serve_launch(h)) return r;
+                w = 0;
+                continue;
+            }
+            if (ms_since(t0) > kServeTimeoutMs) return fail(MEV_E_HIP, "step server: no answer within 10 s");
+            cpu_relax();
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    ++h->serve_steps;
+    return MEV_OK;
+}
+
+int mev_set_serve(mev_handle* h, int32_t mode) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (mode != 0 && mode != 1) return fail(MEV_E_INVALID, "serve mode must be 0 (off) or 1 (automatic)");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r = serve_stop(h)) return r;
+    h->serve_mode = mode;
+    return MEV_OK;
+}
+
+int mev_serve_stats(const mev_handle* h, uint64_t* steps, uint64_t* launches, int32_t* running) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (steps) *steps = h->serve_steps;
+    if (launches) *launches = h->serve_launches;
+    if (running) *running = h->serve_running ? 1 : 0;
+    return MEV_OK;
+}
+
 int mev_step(mev_handle* h, const mev_step_args* a) {
     if (!h || !a) return fail(MEV_E_INVALID, "null argument");
     if (!a->actions) return fail(MEV_E_INVALID, "actions required");
@@ -708,6 +872,9 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     in.auto_reset = (a->flags & MEV_AUTO_RESET) ? 1 : 0;
     in.rng_counter = h->rng_counter++;
     const bool pinned = !dev && !gather && pin_ready(h);  // zero-copy host mode (small handles)
+    const bool serve = pinned && serve_wanted(h);         // ... answered by the resident step server
+    if (!serve)
+        if (int r = serve_stop(h)) return r;
     if (dev) {
         in.actions = a->actions;
         in.spawn_route = a->spawn_route;
@@ -758,6 +925,7 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     if (!h->sp_valid || memcmp(&h->sp, &h->sp_dev, sizeof(mev::SimParams)) != 0) {
         // parameters changed (configuration calls only): stream-ordered after the
         // launches that read the previous copy; waited for, so the host copy is free
+        if (int r = serve_stop(h)) return r;
         HIP_TRY(hipMemcpyAsync(h->d_sp, &h->sp, sizeof(mev::SimParams), hipMemcpyHostToDevice, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
         memcpy(&h->sp_dev, &h->sp, sizeof(mev::SimParams));
@@ -765,7 +933,7 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     }
     // the NPC-aware deal (fused traffic k_step only; MEV_NO_DEAL=1 turns it off)
     static const bool no_deal = [] { const char* v = getenv("MEV_NO_DEAL"); return v && v[0] == '1'; }();
-    const bool deal = h->sp.traffic && h->sp.deal_cnt && !no_deal && mev::step_kernel_for(h->sp) == 2;
+    const bool deal = !serve && h->sp.traffic && h->sp.deal_cnt && !no_deal && mev::step_kernel_for(h->sp) == 2;
     if (deal) {
         if (!h->deal_valid) {  // fresh rings: this step deals by the identity order and builds the next
             HIP_TRY(hipMemsetAsync(h->sp.deal_cnt, 0, size_t(3) * mev::kDealRingInts * sizeof(int32_t), h->stream));
@@ -774,7 +942,11 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         in.deal = 2 | (h->deal_valid ? 1 : 0);
         in.deal_ring = h->deal_ring;
     }
-    HIP_TRY(mev::launch_step(h->sp, h->d_sp, in, o, h->stream, ev));
+    if (serve) {
+        if (int r = serve_step(h, in)) return r;
+    } else {
+        HIP_TRY(mev::launch_step(h->sp, h->d_sp, in, o, h->stream, ev));
+    }
     h->deal_valid = deal;
     if (deal) h->deal_ring = h->deal_ring == 2 ? 0 : h->deal_ring + 1;
     h->last = o;
@@ -803,7 +975,7 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         ++h->gathers;
     }
     if (pinned) {
-        HIP_TRY(hipStreamSynchronize(h->stream));
+        if (!serve) HIP_TRY(hipStreamSynchronize(h->stream));
         const size_t EN_ = EN, E_ = E;
         auto cp = [&](void* dst, int k, size_t bytes) {
             if (dst) memcpy(dst, h->pin + h->pin_off[k], bytes);
@@ -831,6 +1003,7 @@ int mev_get_outputs(mev_handle* h, float* obs, float* rew, uint8_t* done, uint8_
                     uint8_t* trunc, int32_t* alive, int32_t* step, uint32_t flags) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
     if (h->last.lidar_u8) {  // compact gather row: decoded into the handle's buffers first
         if (int r0 = sync_internal(h)) return r0;
@@ -858,19 +1031,58 @@ int mev_get_outputs(mev_handle* h, float* obs, float* rew, uint8_t* done, uint8_
 int mev_get_state(mev_handle* h, const mev_state* s) {
     if (!h || !s) return fail(MEV_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const size_t E = size_t(h->cfg.num_envs), EN = E * size_t(h->cfg.num_agents);
     const size_t EK = E * size_t(h->cfg.max_npcs);
-#define GET(f, dev, n, T) \
-    if (s->f) HIP_TRY(hipMemcpyAsync(s->f, h->sp.dev, (n) * sizeof(T), hipMemcpyDeviceToHost, h->stream));
-    STATE_FIELDS(GET)
-#undef GET
+    // Staged through pinned memory in at most six DMA copies: the 4-byte fields of the
+    // ego and of the NPC SoA are one block each (field k at k * stride), then the alive
+    // flags and the per-env counters; one pageable copy per field cost ~15 us each
+    // (29 of them: env.py's traffic_cars read-back per step).
+    void* const ego4[mev::EF_COUNT] = {s->x, s->y, s->v, s->heading, s->acc, s->steering, s->prev_dist,
+                                      s->prev_a0, s->prev_a1, s->spawn_x, s->spawn_y, s->spawn_v,
+                                      s->spawn_heading, s->path_index, s->route, s->intention};
+    void* const npc4[mev::NF_COUNT] = {s->npc_x, s->npc_y, s->npc_v, s->npc_heading, s->npc_acc,
+                                      s->npc_steering, s->npc_path_index, s->npc_route, s->npc_intention};
+    bool want_e = false, want_n = false;
+    for (void* q : ego4) want_e |= q != nullptr;
+    for (void* q : npc4) want_n |= q != nullptr;
+    const size_t es = size_t(h->sp.ego.stride) * 4, ns = size_t(h->sp.npc.stride) * 4;
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t o_e = 0, o_n = o_e + al(es * mev::EF_COUNT), o_ea = o_n + al(ns * mev::NF_COUNT);
+    const size_t o_na = o_ea + al(EN), o_nc = o_na + al(EK), o_sc = o_nc + al(E * 4), total = o_sc + al(E * 4);
+    if (h->gs_cap < total) {
+        if (h->gs_pin) (void)hipHostFree(h->gs_pin);
+        h->gs_pin = nullptr;
+        h->gs_cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h->gs_pin), total, hipHostMallocDefault));
+        h->gs_cap = total;
+    }
+    uint8_t* st = h->gs_pin;
+    auto d2h = [&](size_t off, const void* src, size_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(st + off, src, bytes, hipMemcpyDeviceToHost, h->stream) : hipSuccess;
+    };
+    if (want_e) HIP_TRY(d2h(o_e, h->sp.ego.x, es * mev::EF_COUNT));
+    if (want_n && EK) HIP_TRY(d2h(o_n, h->sp.npc.x, ns * mev::NF_COUNT));
+    if (s->alive) HIP_TRY(d2h(o_ea, h->sp.ego.alive, EN));
+    if (s->npc_alive) HIP_TRY(d2h(o_na, h->sp.npc.alive, EK));
+    if (s->npc_count) HIP_TRY(d2h(o_nc, h->sp.npc.count, E * 4));
+    if (s->step_count) HIP_TRY(d2h(o_sc, h->sp.step_count, E * 4));
     HIP_TRY(hipStreamSynchronize(h->stream));
+    for (int k = 0; k < mev::EF_COUNT; ++k)
+        if (ego4[k]) memcpy(ego4[k], st + o_e + size_t(k) * es, EN * 4);
+    for (int k = 0; k < mev::NF_COUNT; ++k)
+        if (npc4[k] && EK) memcpy(npc4[k], st + o_n + size_t(k) * ns, EK * 4);
+    if (s->alive) memcpy(s->alive, st + o_ea, EN);
+    if (s->npc_alive && EK) memcpy(s->npc_alive, st + o_na, EK);
+    if (s->npc_count) memcpy(s->npc_count, st + o_nc, E * 4);
+    if (s->step_count) memcpy(s->step_count, st + o_sc, E * 4);
     return MEV_OK;
 }
 
 int mev_set_state(mev_handle* h, const mev_state* s) {
     if (!h || !s) return fail(MEV_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const size_t E = size_t(h->cfg.num_envs), EN = E * size_t(h->cfg.num_agents);
     const size_t EK = E * size_t(h->cfg.max_npcs);
     if (s->route)
@@ -925,6 +1137,7 @@ int mev_device_outputs(mev_handle* h, float** obs, float** rew, uint8_t** done, 
                        uint8_t** trunc) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     if (int r = sync_internal(h)) return r;
     if (obs) *obs = h->internal.obs;
     if (rew) *rew = h->internal.rew;
@@ -939,6 +1152,7 @@ int mev_kernel_timing(mev_handle* h, int32_t enable) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (enable < 0) return fail(MEV_E_INVALID, "enable must be >= 0");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     if (!enable) {
         HIP_TRY(hipStreamSynchronize(h->stream));
         h->free_timing();
@@ -961,6 +1175,7 @@ int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* 
     if (!h || !cars_ms || !lidar_ms || !steps) return fail(MEV_E_INVALID, "null argument");
     if (h->tev.empty()) return fail(MEV_E_INVALID, "kernel timing is not enabled");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(h->fold_timing());
     *cars_ms = h->t_cars_ms;
     *lidar_ms = h->t_lidar_ms;
@@ -978,6 +1193,7 @@ int mev_set_step_kernel(mev_handle* h, int32_t kernel) {
     if (mev::step_kernel_for(q) == 0)
         return fail(MEV_E_INVALID, "the fused step kernel does not support this configuration (traffic mode or too much LDS)");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->sp.step_kernel = kernel;
     return MEV_OK;
@@ -994,6 +1210,7 @@ int mev_set_step_pack(mev_handle* h, int32_t envs_per_wave) {
     if (envs_per_wave != 0 && envs_per_wave != 1 && envs_per_wave != 2 && envs_per_wave != 4 && envs_per_wave != 8)
         return fail(MEV_E_INVALID, "envs per wave must be 0 (auto), 1, 2, 4 or 8");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->sp.step_pack = envs_per_wave;
     return MEV_OK;
@@ -1010,6 +1227,7 @@ int mev_set_step_split(mev_handle* h, int32_t mode) {
     if (mode < 0 || mode > 3)
         return fail(MEV_E_INVALID, "split mode must be 0 (auto), 1 (off), 2 (on) or 3 (early split)");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->sp.step_split = mode;
     return MEV_OK;
@@ -1029,6 +1247,7 @@ int mev_set_reset_routes(mev_handle* h, const int32_t* routes, int32_t count) {
     for (int32_t i = 0; i < count; ++i)
         if (routes[i] < 0 || routes[i] >= h->nroutes) return fail(MEV_E_RANGE, "route id out of range");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     if (count > 0) {
         HIP_TRY(hipMemcpyAsync(h->d_reset_routes, routes, size_t(count) * sizeof(int32_t), hipMemcpyHostToDevice, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1097,6 +1316,7 @@ int mev_snapshot_size(mev_handle* h, uint64_t* bytes) {
 int mev_snapshot(mev_handle* h, void* dst, uint32_t flags) {
     if (!h || !dst) return fail(MEV_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
     const size_t E = size_t(h->cfg.num_envs);
     if (h->last.lidar_u8) {  // compact gather row: the snapshot stores plain obs rows
@@ -1122,6 +1342,7 @@ int mev_snapshot(mev_handle* h, void* dst, uint32_t flags) {
 int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_t flags) {
     if (!h || !src) return fail(MEV_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const bool dev = (flags & MEV_DEVICE_PTRS) != 0;
     const size_t E = size_t(h->cfg.num_envs);
     SnapHeader hd{};
@@ -1260,6 +1481,7 @@ int mev_comm_init(mev_handle* h, const uint8_t* id, int32_t world, int32_t rank,
     if (slots <= 0) slots = h->cfg.num_envs;
     if (slots < h->cfg.num_envs) return fail(MEV_E_INVALID, "slots must be >= num_envs");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     int rc = mev_packed_layout2(slots, h->cfg.num_agents, h->D, h->lidar_slots, h->gather_fmt, h->pk_off, &h->pk_bytes);
     if (rc) return rc;
@@ -1289,6 +1511,7 @@ int mev_comm_init(mev_handle* h, const uint8_t* id, int32_t world, int32_t rank,
 int mev_comm_destroy(mev_handle* h) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (h->comm_stream) HIP_TRY(hipStreamSynchronize(h->comm_stream));
     h->free_comm();
@@ -1301,6 +1524,7 @@ int mev_gather_result(mev_handle* h, void** stacked, uint64_t* bytes_per_rank, i
     if (h->rank != h->root) return fail(MEV_E_INVALID, "the gather result lives on the root rank");
     if (h->gathers == 0) return fail(MEV_E_INVALID, "no step has been gathered yet");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const int b = int((h->gathers - 1) & 1);
     if (h->gather_pending[b]) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gather[b], 0));
     *stacked = h->pk_buf[b];
@@ -1323,6 +1547,7 @@ int mev_gather_wait(mev_handle* h, int32_t timeout_ms) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (!h->comm) return fail(MEV_E_INVALID, "no communicator (mev_comm_init)");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const auto t0 = std::chrono::steady_clock::now();
     for (int b = 0; b < 2; ++b) {
         if (!h->gather_pending[b]) continue;
@@ -1364,6 +1589,7 @@ int mev_output_dlpack(mev_handle* h, int32_t which, mev_dl_managed** out) {
     int64_t sh[3] = {E, 0, 0};
     mev_dl_dtype dt{1, 8, 1};  // u8
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     if (which != MEV_OUT_GATHERED) {
         if (int r = sync_internal(h)) return r;
     }
@@ -1408,6 +1634,7 @@ int mev_output_dlpack(mev_handle* h, int32_t which, mev_dl_managed** out) {
 int mev_npc_overflow(mev_handle* h, int64_t* count) {
     if (!h || !count) return fail(MEV_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     unsigned long long v = 0;
     HIP_TRY(hipMemcpyAsync(&v, h->sp.overflow, sizeof(v), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1418,6 +1645,7 @@ int mev_npc_overflow(mev_handle* h, int64_t* count) {
 int mev_npc_stats(mev_handle* h, int64_t* overflow, int64_t* sequential_turns) {
     if (!h || !overflow || !sequential_turns) return fail(MEV_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     unsigned long long v[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(v, h->sp.overflow, sizeof(v), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));

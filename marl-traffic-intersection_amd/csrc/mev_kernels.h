@@ -164,6 +164,37 @@ hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outpu
 // recompute the observation rows from the current state with LiDAR = max (after set_state)
 hipError_t launch_observe_reset_lidar(const SimParams& p, const Outputs& out, hipStream_t s);
 
+// Persistent step server (k_serve) of a small host-mode handle: the mailbox in
+// host-coherent pinned memory.  A posting writes the command line's fields, then
+// seq (release).  STEP carries a step number sid (a re-post after a relaunch keeps
+// it); workgroup b answers done[b] = sid once its outputs are in the pinned block,
+// and answers a sid it has served before with nothing.  STOP writes only cmd and
+// seq.  Every workgroup publishes exited[b] = its instance's epoch when it leaves
+// (STOP, or no posting for ServeArgs::idle_ticks).
+constexpr int kServeMaxWG = 64;
+constexpr int kServeLine = 9;  // words of the command line
+constexpr uint32_t kServeStep = 1, kServeStop = 2;
+struct ServeBox {
+    uint32_t seq, cmd, sid;     // host -> device: posting number, kind, step number
+    uint32_t dt, spawn_prob;    // f32 bits
+    uint32_t auto_reset, spawn;  // spawn: spawn_route holds this step's routes
+    uint32_t rng_lo, rng_hi;    // StepInputs::rng_counter
+    uint32_t pad0[23];
+    uint32_t done[kServeMaxWG];    // device -> host
+    uint32_t exited[kServeMaxWG];  // device -> host
+};
+struct ServeArgs {
+    ServeBox* box;               // device address of the mailbox
+    const float* actions;        // device address of the pinned actions
+    const int32_t* spawn_route;  // device address of the pinned spawn routes
+    uint32_t epoch;
+    uint32_t idle_ticks;         // 100 MHz ticks
+};
+// whether the handle's step can run as k_serve (fused, one workgroup per env, <= 64 envs)
+bool serve_fits(const SimParams& p);
+hipError_t launch_serve(const SimParams& p, const SimParams* dp, const ServeArgs& sa, const Outputs& out,
+                        hipStream_t s);
+
 // masked per-env copy of snapshot fields (mev_restore)
 constexpr int kMaxRestoreFields = 48;
 struct RestoreTab {

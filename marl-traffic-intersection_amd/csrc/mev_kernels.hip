@@ -3382,9 +3382,9 @@ struct RoadHook {
 #ifndef MEV_ESPLIT_ILP
 #define MEV_ESPLIT_ILP 1
 #endif
+// One step of the workgroup's envs (the body of k_step; k_serve runs it in a loop).
 template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
-__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_ESPLIT_WPE : (SPLIT ? MEV_SPLIT_WPE : 4)) void k_step(
-    const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
+__device__ __forceinline__ void step_body(const SimParams* __restrict__ pp, const StepInputs& in, const Outputs& out) {
     static_assert(!SPLIT || (!TRAFFIC && !MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE),
                   "split waves: the plain fused step");
     const SimParams& p = *pp;
@@ -3598,6 +3598,84 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_
     }
 #endif
 }
+
+template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
+__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_ESPLIT_WPE : (SPLIT ? MEV_SPLIT_WPE : 4)) void k_step(
+    const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
+    step_body<TRAFFIC, TAB, NM, KM, PK, SPLIT, ESPLIT>(pp, in, out);
+}
+
+// ------------------------------------------------- persistent step server ---
+// k_serve: the fused step of a small host-mode handle as a persistent kernel.  A
+// host step then costs a mailbox round trip over PCIe instead of a kernel launch
+// plus a stream synchronisation (the single env of the reference's env.py: 22 us
+// per step launched).  Wave 0 of each workgroup polls the command
+// line of the ServeBox (system-scope loads of host-coherent memory) until a new
+// command, a stop, or sa.idle_ticks of the 100 MHz clock without one; it hands the
+// command to the other wave through LDS.  A step runs step_body -- the same code
+// as k_step, the same grid -- reading the actions from and writing the outputs to
+// the handle's pinned block; then every wave releases its writes at system scope
+// and workgroup b publishes done[b] = the command's number.  Every exit (stop, or
+// idle) publishes exited[b] = the instance's epoch first, so the host knows to
+// launch a new instance; that instance starts from done[b] and never serves a
+// command twice.  Every wave reaches the exit: the poll loop is bounded by the
+// clock, a step by its own work.
+template <bool TRAFFIC, bool TAB, int NM, int KM, bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? MEV_SPLIT_WPE : 4) void k_serve(
+    const SimParams* __restrict__ pp, ServeArgs sa, Outputs out) {
+    __shared__ uint32_t cmdw[kServeLine];
+    const int lane = threadIdx.x & (WAVE - 1);
+    const bool w0 = threadIdx.x < WAVE;
+    ServeBox* box = sa.box;
+    uint32_t last_seq = 0xffffffffu;  // never a posted number: the first poll reads the line at once
+    uint32_t served = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&box->done[blockIdx.x], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+    for (;;) {
+        if (w0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t seq = last_seq, quit = 0u;
+            for (;;) {
+                seq = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(&box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM));
+                if (seq != last_seq) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > sa.idle_ticks) {
+                    quit = 1u;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            // the command line, written before seq: seq cmd sid dt spawn_prob auto_reset spawn rng_lo rng_hi
+            uint32_t word = 0u;
+            if (lane < kServeLine) word = __hip_atomic_load(&box->seq + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0) word = seq;
+            if (lane == 1 && quit) word = kServeStop;
+            if (lane < kServeLine) cmdw[lane] = word;
+        }
+        __syncthreads();
+        const uint32_t seq = cmdw[0], cmd = cmdw[1], sid = cmdw[2];
+        if (cmd != kServeStep) break;  // a stop, or idle
+        last_seq = seq;
+        if (sid == served) {  // a re-post of a step this workgroup has answered
+            __syncthreads();  // (wave 0 rewrites cmdw only after every wave has read it)
+            continue;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the actions the host wrote before seq
+        StepInputs in{};
+        in.actions = sa.actions;
+        in.spawn_route = cmdw[6] ? sa.spawn_route : nullptr;
+        in.dt = __uint_as_float(cmdw[3]);
+        in.spawn_prob = __uint_as_float(cmdw[4]);
+        in.auto_reset = (int32_t)cmdw[5];
+        in.rng_counter = (uint64_t)cmdw[7] | ((uint64_t)cmdw[8] << 32);
+        step_body<TRAFFIC, TAB, NM, KM, 1, SPLIT, false>(pp, in, out);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this wave's outputs and state written
+        __syncthreads();  // (also: nobody reads cmdw or the step's LDS any more)
+        if (threadIdx.x == 0) __hip_atomic_store(&box->done[blockIdx.x], sid, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        served = sid;
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&box->exited[blockIdx.x], sa.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 
 // ------------------------------------------------- reset / re-observe ---
 // IntersectionEnv::reset + add_car_with_route (cpp/IntersectionEnv.cpp:66-131)
@@ -3837,6 +3915,36 @@ hipError_t launch_step(const SimParams& p, const SimParams* dp, const StepInputs
         return e;
     }
     return launch_part(p, in, out, 0, p.E, s, ev);
+}
+
+// k_serve runs the handle's fused step (one workgroup per env): the compile-time
+// layouts of launch_fused for small batches -- the split kernel without traffic,
+// one ego with <= 32 NPC slots -- and, for more NPC slots (env.py's 64), the
+// dynamic traffic layout, which at one env may take more than a wave's 10 KB share
+bool serve_fits(const SimParams& p) {
+    if (step_kernel_for(p) == 0 || p.step_kernel == 1) return false;
+    if (p.E > kServeMaxWG) return false;
+    if (p.traffic) return fixed_fits<1, 32>(p) || (p.K > 32 && fused_fits(p));
+    return fixed_fits<8, 0>(p) && step_pack(p) == 1 && !step_esplit(p) && p.step_split != 1;
+}
+
+hipError_t launch_serve(const SimParams& p, const SimParams* dp, const ServeArgs& sa, const Outputs& out,
+                        hipStream_t s) {
+    if (!serve_fits(p)) return hipErrorInvalidValue;
+    if (p.traffic && fixed_fits<1, 32>(p)) {
+        const unsigned lds = (unsigned)FixedLayout<1, 32>::bytes;
+        if (p.dist_tab) hipLaunchKernelGGL((k_serve<true, true, 1, 32, false>), dim3(p.E), dim3(WAVE), lds, s, dp, sa, out);
+        else hipLaunchKernelGGL((k_serve<true, false, 1, 32, false>), dim3(p.E), dim3(WAVE), lds, s, dp, sa, out);
+    } else if (p.traffic) {
+        const unsigned lds = (unsigned)step_layout(p).bytes;  // + the static NpcLDST<64>
+        if (p.dist_tab) hipLaunchKernelGGL((k_serve<true, true, 0, 64, false>), dim3(p.E), dim3(WAVE), lds, s, dp, sa, out);
+        else hipLaunchKernelGGL((k_serve<true, false, 0, 64, false>), dim3(p.E), dim3(WAVE), lds, s, dp, sa, out);
+    } else {
+        const unsigned lds = (unsigned)FixedLayout<8>::bytes;
+        if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true>), dim3(p.E), dim3(2 * WAVE), lds, s, dp, sa, out);
+        else hipLaunchKernelGGL((k_serve<false, false, 8, MAXK, true>), dim3(p.E), dim3(2 * WAVE), lds, s, dp, sa, out);
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_reset(const SimParams& p, const uint8_t* env_mask, const Outputs& out, hipStream_t s,

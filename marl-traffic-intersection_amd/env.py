@@ -87,8 +87,7 @@ class IntersectionEnv:
         for start, end in self.ego_routes[: self.num_agents]:
             self.env.add_car_with_route(start, end)
         self.cars = self.env.cars
-        if self.traffic_flow:
-            self.traffic_cars = list(self.env.traffic_cars)
+        self._traffic_cars = None  # read from the device on first access (traffic_cars)
         obs = np.asarray(self.env.get_observations(), np.float32)
         return (obs[0], {}) if self.traffic_flow else (obs, {})
 
@@ -105,8 +104,7 @@ class IntersectionEnv:
     def step(self, actions, dt: float = 1.0 / 60.0):
         a = self._coerce_actions(actions)
         res = self.env.step(a[:, 0], a[:, 1], float(dt))
-        if self.traffic_flow:
-            self.traffic_cars = list(self.env.traffic_cars)
+        self._traffic_cars = None  # read from the device on first access (traffic_cars)
         obs = np.asarray(res.obs, np.float32)
         rewards = np.asarray(res.rewards, np.float32)
         first = float(rewards[0]) if len(rewards) else 0.0
@@ -123,6 +121,23 @@ class IntersectionEnv:
         if self.traffic_flow:
             return obs[0], first, info["terminated"], info["truncated"], info
         return obs, rewards, info["terminated"], info["truncated"], info
+
+    # The reference refreshes self.traffic_cars after every reset and step (env.py:155-157,
+    # :184-186: a copy of the C++ Car list).  Here the list is built when it is first read
+    # after a step -- the same cars, since nothing else moves them in between -- so a
+    # training loop that never looks at the NPCs does not pay a device read-back per step.
+    @property
+    def traffic_cars(self) -> List[cpp_backend.Car]:
+        if self._traffic_cars is None:
+            try:
+                self._traffic_cars = list(self.env.traffic_cars) if self.traffic_flow else []
+            except Exception:  # (the reference's fallback)
+                self._traffic_cars = []
+        return self._traffic_cars
+
+    @traffic_cars.setter
+    def traffic_cars(self, cars):
+        self._traffic_cars = cars
 
     def render(self, show_lane_ids: Optional[bool] = None, show_lidar: Optional[bool] = None):
         """The reference opens a GLFW window (Windows-only, Renderer.cpp).  Here

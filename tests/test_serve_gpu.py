@@ -1,0 +1,124 @@
+"""The persistent step server (k_serve, mev_set_serve, include/marlenv.h): host-mode
+steps of small handles answered by a resident kernel through a mailbox in pinned
+memory.  Every output and the state must equal the launched step's bit for bit --
+including across idle exits and relaunches, other calls that stop the server in the
+middle of a run (get_state, device-mode steps, reset) and recorded NPC spawns.  The
+single env of the reference's env.py (cpp/bindings.cpp:53-55) is the case it is for."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [
+    dict(num_envs=1, num_agents=1, lidar_rays=16),
+    dict(num_envs=1, num_agents=8, lidar_rays=64, use_team_reward=1),
+    dict(num_envs=16, num_agents=4, lidar_rays=96),
+    dict(num_envs=1, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32),
+    dict(num_envs=4, num_agents=1, lidar_rays=32, traffic_flow=1, traffic_density=3.0, max_npcs=32),
+    # env.py's traffic env: 64 NPC slots (the dynamic layout), 96 beams, the reference's 127-float rows
+    dict(num_envs=1, num_agents=1, lidar_rays=96, traffic_flow=1, traffic_density=2.0, max_npcs=64, obs_dim=127),
+]
+IDS = ["cfg1", "cfg3_one_env", "e16_n4_r96", "cfg4_one_env", "traffic_e4", "envpy_traffic_k64"]
+
+
+def _pair(mev, cfg):
+    a = mev.Handle(seed=7, **cfg)
+    b = mev.Handle(seed=7, **cfg)
+    b.set_serve(0)
+    return a, b
+
+
+def _same(oa, ob, what):
+    for k in oa:
+        assert np.array_equal(oa[k], ob[k]), (what, k)
+
+
+@pytest.mark.parametrize("cfg", SHAPES, ids=IDS)
+def test_served_steps_equal_launched_steps(mev, cfg):
+    a, b = _pair(mev, cfg)
+    E, N = a.E, a.N
+    rng = np.random.default_rng(3)
+    a.reset()
+    b.reset()
+    T = 240
+    acts = rng.uniform(-1, 1, (T, E, N, 2)).astype(np.float32)
+    traffic = bool(cfg.get("traffic_flow"))
+    for t in range(T):
+        spawn = None
+        if traffic and 60 <= t < 90:  # recorded spawns (the replay channel) for a while
+            spawn = rng.integers(-1, 4, E).astype(np.int32)
+        oa = a.step(acts[t], auto_reset=True, spawn_route=spawn)
+        ob = b.step(acts[t], auto_reset=True, spawn_route=spawn)
+        _same(oa, ob, t)
+        if t == 100:
+            time.sleep(0.2)  # longer than the server's idle limit: it leaves, the next step relaunches
+        if t == 150:
+            sa, sb = a.get_state(), b.get_state()  # stops the server
+            for k in sa:
+                assert np.array_equal(sa[k], sb[k]), k
+    st = a.serve_stats()
+    assert st["steps"] == T, st
+    assert st["launches"] >= 3, st  # first step, after the idle pause, after get_state
+    assert b.serve_stats()["steps"] == 0
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    a.close()
+    b.close()
+
+
+def test_serve_interleaved_with_device_steps_and_resets(mev):
+    import torch
+    cfg = dict(num_envs=2, num_agents=2, lidar_rays=32)
+    a, b = _pair(mev, cfg)
+    E, N = a.E, a.N
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(5)
+    a.reset()
+    b.reset()
+    dev_out = {k: torch.as_tensor(v).cuda() for k, v in a.alloc_outputs().items()}
+    for t in range(120):
+        act = rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)
+        if t % 7 == 3:  # a device-mode step between served host steps
+            ta = torch.as_tensor(act).cuda()
+            a.step(ta.data_ptr(), out={k: v.data_ptr() for k, v in dev_out.items()}, auto_reset=True, device=True)
+            torch.cuda.synchronize()
+            oa = {k: v.cpu().numpy() for k, v in dev_out.items()}
+        else:
+            oa = a.step(act, auto_reset=True)
+        ob = b.step(act, auto_reset=True)
+        _same(oa, ob, t)
+        if t == 60:
+            a.reset()
+            b.reset()
+    assert a.serve_stats()["steps"] > 90
+    a.close()
+    b.close()
+
+
+def test_serve_off_and_on(mev):
+    a = mev.Handle(num_envs=1, num_agents=1, lidar_rays=16)
+    a.reset()
+    act = np.zeros((1, 1, 2), np.float32)
+    a.step(act)
+    assert a.serve_stats()["running"]
+    a.set_serve(0)
+    assert not a.serve_stats()["running"]
+    a.step(act)
+    assert a.serve_stats()["steps"] == 1
+    a.set_serve(1)
+    a.step(act)
+    assert a.serve_stats()["steps"] == 2
+    with pytest.raises(Exception):
+        a.set_serve(2)
+    a.close()
+
+
+def test_large_handles_are_not_served(mev):
+    a = mev.Handle(num_envs=128, num_agents=1, lidar_rays=16)  # more than 64 workgroups
+    a.reset()
+    a.step(np.zeros((128, 1, 2), np.float32))
+    assert a.serve_stats()["steps"] == 0
+    a.close()
