@@ -9,6 +9,7 @@ device raises.
 from __future__ import annotations
 
 import ctypes
+import operator
 import os
 from typing import Dict, Optional
 
@@ -231,8 +232,8 @@ def _ptr(a) -> Optional[int]:
     if a is None:
         return None
     if isinstance(a, np.ndarray):
-        assert a.flags["C_CONTIGUOUS"], "arrays passed to libmarlenv_hip must be C-contiguous"
-        return a.ctypes.data
+        assert a.flags.c_contiguous, "arrays passed to libmarlenv_hip must be C-contiguous"
+        return a.__array_interface__["data"][0]
     if hasattr(a, "data_ptr"):  # torch tensor (device pointer mode)
         return int(a.data_ptr())
     return int(a)
@@ -419,13 +420,15 @@ class Handle:
         # the output pointers of the args struct are reused while `out` holds the same
         # arrays (a step loop passes one dict): numpy pointer lookups cost ~1.6 us each
         c = self._args_cache
-        if c is None or c[0] is not out or any(c[1][i] is not out.get(k) for i, k in enumerate(_OUT_KEYS)):
+        if c is None or c[0] is not out or not all(map(operator.is_, c[1], map(out.get, _OUT_KEYS))):
             a = MevStepArgs()
             for k in _OUT_KEYS:
                 setattr(a, k, _ptr(out.get(k)))
-            c = self._args_cache = (out, [out.get(k) for k in _OUT_KEYS], a)
+            c = self._args_cache = (out, tuple(map(out.get, _OUT_KEYS)), a, None)
         a = c[2]
-        a.actions = _ptr(actions)
+        if actions is not c[3]:  # (a loop that refills one actions array skips the pointer lookup)
+            a.actions = _ptr(actions)
+            c = self._args_cache = (c[0], c[1], a, actions)
         a.dt = float(dt)
         a.spawn_route = _ptr(spawn_route)
         a.flags = ((MEV_DEVICE_PTRS if device else 0) | (MEV_AUTO_RESET if auto_reset else 0) |

@@ -179,6 +179,7 @@ class IntersectionEnv:
         self._reward_dirty = True
         self._lidar = DEFAULT_LIDAR
         self._h: Optional[_capi.Handle] = None
+        self._out_h = None  # the handle step()'s buffers (_out, _act) belong to
         self._routes: List[int] = []     # ego route ids (add order)
         self._agent_ids: List[int] = []
         self._next_id = 1
@@ -305,26 +306,30 @@ class IntersectionEnv:
 
     def step(self, throttles: Sequence[float], steerings: Sequence[float], dt: float = 1.0 / 60.0) -> StepResult:
         """IntersectionEnv::step (cpp/IntersectionEnv.cpp:133-392) on the GPU."""
-        h = self._sync()
-        res = StepResult()
-        if h is None:
-            return res
+        h = self._h
+        if h is None or self._pending or self._reward_dirty or h.N != len(self._routes) or self._h_lidar != self._lidar:
+            h = self._sync()
+            if h is None:
+                return StepResult()
         n = h.N
-        act = np.zeros((1, n, 2), np.float32)
+        # one action buffer and one output dict per handle (its args struct is reused by
+        # Handle.step); the result's arrays are copies, like the reference's pybind conversions
+        if self._out_h is not h:
+            self._out_h, self._out, self._act = h, h.alloc_outputs(), np.zeros((1, n, 2), np.float32)
+        act = self._act
         t = np.asarray(throttles, np.float32).reshape(-1)[:n]
         s = np.asarray(steerings, np.float32).reshape(-1)[:n]
-        act[0, : len(t), 0] = t
-        act[0, : len(s), 1] = s
-        # one output dict per handle (its args struct is reused by Handle.step); the
-        # result's arrays are copies, like the reference's pybind conversions
-        if getattr(self, "_out_h", None) is not h:
-            self._out_h, self._out = h, h.alloc_outputs()
+        if t.size < n or s.size < n:  # missing inputs are zero
+            act.fill(0.0)
+        act[0, : t.size, 0] = t
+        act[0, : s.size, 1] = s
         out = h.step(act, float(dt), out=self._out)
         self._fresh = False
+        res = StepResult.__new__(StepResult)
         res.obs = out["obs"][0].copy()
         res.rewards = out["reward"][0].copy()
-        res.done = [int(x) for x in out["done"][0]]
-        res.status = [STATUS[int(x)] for x in out["status"][0]]
+        res.done = out["done"][0].tolist()
+        res.status = [STATUS[x] for x in out["status"][0].tolist()]
         res.agent_ids = list(self._agent_ids)
         res.agents_alive = int(out["agents_alive"][0])
         res.terminated = bool(out["terminated"][0])
