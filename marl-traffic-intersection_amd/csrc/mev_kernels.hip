@@ -3382,227 +3382,10 @@ struct RoadHook {
 #ifndef MEV_ESPLIT_ILP
 #define MEV_ESPLIT_ILP 1
 #endif
-// One step of the workgroup's envs (the body of k_step; k_serve runs it in a loop).
-template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
-__device__ __forceinline__ void step_body(const SimParams* __restrict__ pp, const StepInputs& in, const Outputs& out) {
-    static_assert(!SPLIT || (!TRAFFIC && !MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE),
-                  "split waves: the plain fused step");
-    const SimParams& p = *pp;
-    extern __shared__ __align__(16) unsigned char step_lds[];
-    const int wv = SPLIT ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
-    // PK envs per wave (few agents per env): envs e .. e + PK - 1, see cars_pre
-    const int e = (TRAFFIC && (in.deal & 1)) ? deal_env(p, in.deal_ring, (int)blockIdx.x)
-                                             : xcd_env((int)blockIdx.x, (int)gridDim.x) * PK;
-#if defined(MEV_STAMPS_R)
-    STAMP_RAW(0);
-#endif
-    constexpr int KF = TRAFFIC ? KM : 0;  // NPC obstacle slots of the compile-time layout
-    const StepLayout sl = step_layout_t<NM, KF>(p);
-    CarsLDS el = NM ? carve_cars_lds(step_lds, NM, KF) : carve_cars_lds(step_lds, p.N, cars_k(p));
-    el.head = reinterpret_cast<float*>(step_lds + sl.head);
-    el.rel = reinterpret_cast<float*>(step_lds + sl.rel);
-    el.envw = reinterpret_cast<int32_t*>(step_lds + sl.envw);
-    if constexpr (!TRAFFIC && NM > 0) {
-        static_assert(NM == 0 || FixedLayout<(NM ? NM : 1), 0>::lay.bytes >= kWinBytes, "LDS path windows");
-        el.win = reinterpret_cast<float4*>(step_lds + sl.lidar);
-    }
-    __shared__ typename std::conditional<TRAFFIC, NpcLDST<KM>, char>::type nl_storage;
-    NpcLDST<KM>* nl = nullptr;
-    if constexpr (TRAFFIC) nl = &nl_storage;
-    if (MEV_PRIO_CARS) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
-    if constexpr (ESPLIT) {
-        static_assert(SPLIT && !TRAFFIC && NM > 0, "early split: two waves, no traffic");
-        const int lane = threadIdx.x & (WAVE - 1);
-        const int g0 = e * p.N;
-        // the wave's agent slots: PK envs of N agents (consecutive in the SoA), one LiDAR pool
-        const int NE = p.N;
-        const int NS = PK == 1 ? NE : (p.E - e < PK ? p.E - e : PK) * NE;
-        unsigned char* lbase = step_lds + sl.lidar;
-        const LidarLayout lay = FixedLayout<(NM ? NM : 1), 0>::lay;
-        if (wv == 0) {
-            // the car part (its path windows through VGPRs: the LiDAR wave owns the LiDAR
-            // area from the start), barrier B at the end of cars_pre
-            ES_STAMP(0);
-            __builtin_amdgcn_s_setprio(MEV_PRIO_ESPLIT_CARS);
-            CarsCtx cx = cars_pre<false, true, NpcLDST<KM>, PK, false, true>(p, in, out, e, el, nl);
-            cars_post<false, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
-            ES_STAMP(3);
-        } else {
-#ifdef MEV_X_ES_NOLIDAR  // timing-only: the LiDAR wave only passes the barrier
-            __syncthreads();
-            return;
-#endif
-            __builtin_amdgcn_s_setprio(MEV_PRIO_ESPLIT_ROAD);
-            // the beam offsets (this wave stages them in the early split) and, lane i < N,
-            // agent i's pose after Car::update exactly as cars_pre computes it (an env
-            // whose previous step ended starts from its spawns; a dead agent keeps its
-            // pose): the road march needs nothing else from the car part
-            for (int b = lane; b < p.R; b += WAVE) el.rel[b] = gmem(p.rel_angles)[b];
-            const bool on = lane < NS;
-            const int il = on ? lane : 0;
-            const int ee = PK == 1 ? e : e + il / NE;  // the slot's env
-            const uint32_t ug = (uint32_t)(g0 + il);
-            const bool pend = ldu(gmem(p.pending_reset), (uint32_t)ee) != 0;
-            const int route_l = ldu(egoi(p, EF_ROUTE), ug);
-            Kin k{ldu(egof(p, EF_X), ug), ldu(egof(p, EF_Y), ug), ldu(egof(p, EF_V), ug), ldu(egof(p, EF_H), ug),
-                  ldu(egof(p, EF_ACC), ug), ldu(egof(p, EF_STEER), ug)};
-            bool alive = ldu(gmem(p.ego.alive), ug) != 0;
-            const float a0 = ldu(gmem(in.actions), 2 * ug), a1 = ldu(gmem(in.actions), 2 * ug + 1);
-            if (in.auto_reset && pend) {
-                const int rid = reset_route(p, in.rng_counter, ee, PK == 1 ? il : il - (ee - e) * NE, route_l);
-                k = Kin{gmem(p.rt.spawn)[3 * rid], gmem(p.rt.spawn)[3 * rid + 1], 0.0f, gmem(p.rt.spawn)[3 * rid + 2],
-                        0.0f, 0.0f};
-                alive = true;
-            }
-            {
-                Kin ku = k;
-                float sH, cH;
-                car_update_heading(ku, a0, a1, in.dt);
-                sincosf(alive ? ku.h : k.h, &sH, &cH);
-                car_update_move(ku, cH, sH);
-                if (alive) k = ku;
-            }
-            alive = on && alive;
-            const unsigned long long am = ballot(alive);
-            float4* ag = reinterpret_cast<float4*>(lbase + lay.ag);
-            if (alive) ag[lane_rank(am)] = make_float4(k.x, k.y, k.h, __int_as_float(g0 + il));
-            wave_lds_sync();
-            ES_STAMP(4);
-            lidar_body<TAB, MEV_ESPLIT_ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true, 1>(
-                p, out, LidarSrcLds{el, g0}, NS, g0, NS, lane, lbase, lay, 0ull, am);
-            ES_STAMP(5);
-            __syncthreads();  // barrier B: the car part's obstacle table, candidate masks and respawns
-            ES_STAMP(6);
-            // respawned egos: their spawn poses into ag[] and their beams marched again
-            const unsigned rmask = (unsigned)el.envw[6];
-            const bool rs = alive && lane < 32 && ((rmask >> (lane & 31)) & 1u);
-            const unsigned long long rl = ballot(rs);
-            unsigned long long redo = 0ull;
-            if (rl != 0ull) {
-                if (rs) ag[lane_rank(am)] = make_float4(el.x[lane], el.y[lane], el.h[lane], __int_as_float(g0 + lane));
-                for (unsigned long long m = rl; m; m &= m - 1ull) {
-                    const int i = __builtin_ctzll(m);
-                    redo |= 1ull << __popcll(am & ((1ull << i) - 1ull));
-                }
-                wave_lds_sync();
-            }
-            __builtin_amdgcn_s_setprio(MEV_PRIO_ESPLIT_CARPHASE);
-            lidar_body<TAB, MEV_ESPLIT_ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true, 2>(
-                p, out, LidarSrcLds{el, g0}, NS, g0, NS, lane, lbase, lay, redo, am);
-            ES_STAMP(7);
-        }
-        return;
-    }
-#ifdef MEV_EXP_SKEW  // experiment: odd workgroups start MEV_EXP_SKEW x 64 x 127 cycles late
-    if (blockIdx.x & 1) {
-        for (int t = 0; t < MEV_EXP_SKEW; ++t) __builtin_amdgcn_s_sleep(127);
-    }
-#endif
-#ifdef MEV_EXP_SKEWPRIO  // experiment: odd workgroups run the car part one priority level lower
-    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(MEV_PRIO_CARS - 1);
-#endif
-    constexpr bool MIXABLE = MEV_MIX && !TRAFFIC && !SPLIT && PK == 1 && NM > 0 && !MEV_FUSED_STAGED &&
-                             !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE;
-    if constexpr (MIXABLE) if (p.N * p.R <= kPoolBeams) {  // one LiDAR pool per env
-        const bool border = (blockIdx.x >> MEV_MIX_SHIFT) & 1;
-        const int lane = threadIdx.x & (WAVE - 1);
-        const int g0 = e * p.N;
-        unsigned char* lbase = step_lds + sl.lidar;
-        const LidarLayout lay = FixedLayout<(NM ? NM : 1), 0>::lay;
-        const RoadHook<TAB, MEV_PHASE1_ILP> hook{p, out, el, lbase, lay, g0, border};
-        CarsCtx cx = cars_pre<false, true, NpcLDST<KM>, 1, (MEV_EARLY_WINDOW && NM > 0), false, RoadHook<TAB, MEV_PHASE1_ILP>>(
-            p, in, out, e, el, nl, hook);
-        wave_lds_sync();
-        cars_post<false, true, NpcLDST<KM>, 1>(p, out, e, el, nl, cx);
-        wave_lds_sync();
-        if (border) {
-            // the respawned egos' spawn poses into ag[] and their beams marched again, then the car pairs
-            const unsigned rmask = (unsigned)el.envw[6];
-            const bool alive = lane < p.N && el.alive[lane < p.N ? lane : 0] != 0;
-            const unsigned long long am = ballot(alive);
-            const bool rs = alive && lane < 32 && ((rmask >> (lane & 31)) & 1u);
-            const unsigned long long rl = ballot(rs);
-            unsigned long long redo = 0ull;
-            if (rl != 0ull) {
-                float4* ag = reinterpret_cast<float4*>(lbase + lay.ag);
-                if (rs) ag[lane_rank(am)] = make_float4(el.x[lane], el.y[lane], el.h[lane], __int_as_float(g0 + lane));
-                for (unsigned long long m = rl; m; m &= m - 1ull) {
-                    const int i = __builtin_ctzll(m);
-                    redo |= 1ull << __popcll(am & ((1ull << i) - 1ull));
-                }
-                wave_lds_sync();
-            }
-            lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true, 2>(
-                p, out, LidarSrcLds{el, g0}, p.N, g0, p.N, lane, lbase, lay, redo, am);
-        } else {
-            __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
-            lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true>(
-                p, out, LidarSrcLds{el, g0}, p.N, g0, p.N, lane, lbase, lay);
-        }
-        return;
-    }
-    CarsCtx cx{};
-    if (wv == 0) cx = cars_pre<TRAFFIC, true, NpcLDST<KM>, PK, (MEV_EARLY_WINDOW && !TRAFFIC && NM > 0)>(p, in, out, e, el, nl);
-    if (SPLIT) __syncthreads();
-    else wave_lds_sync();
-#if !defined(MEV_EXP_STOP) || MEV_EXP_STOP != 0  // timing-only stop0: the car part without cars_post
-    if (!MEV_POST_AFTER_LIDAR && wv == 0) {
-        cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
-        wave_lds_sync();
-    }
-#endif
-    if (MEV_DEAL_LATE == 0) deal_append<TRAFFIC>(p, in, cx, e);
-#if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 0  // (stop0 keeps the deal: the env order stays the product's)
-    return;
-#endif
-    if (SPLIT && wv == 0) return;  // wave 1 runs the LiDAR
-#if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 1  // timing-only: the car part alone
-    return;
-#endif
-    // agent slots of this wave and its LiDAR pools of <= 512 beams (one at config 3)
-    const int NS = PK == 1 ? p.N : (p.E - e < PK ? p.E - e : PK) * p.N;
-    int G = 512 / (p.R > 0 ? p.R : 1);
-    G = G < 1 ? 1 : (G < NS ? G : NS);
-    if (PK == 1) G = step_pool(p);
-    const LidarLayout lay = NM ? FixedLayout<(NM ? NM : 1), KF>::lay : lidar_layout(G, p.R, lidar_cand_max(p), false);
-    unsigned char* lbase = step_lds + sl.lidar;
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int g0 = e * p.N;
-    for (int j0 = 0; j0 < NS; j0 += G) {  // pools of G agents (one at config 3)
-        if (j0 > 0) wave_lds_sync();
-        if (j0 > 0 || MEV_PRIO_CARS != MEV_PRIO_LIDAR) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);  // each pool
-        const int na = NS - j0 < G ? NS - j0 : G;
-        lidar_body<TAB, MEV_PHASE1_ILP, LidarSrcLds, TRAFFIC ? LIDAR_NPR : MEV_LIDAR_NPR_TAIL,
-                   !TRAFFIC || MEV_HELP_TRAFFIC>(
-            p, out, LidarSrcLds{el, g0}, G, g0 + j0, na, lane, lbase, lay);
-    }
-    if (MEV_POST_AFTER_LIDAR) {  // experiment (variant postlate): measured slower, 41.6 -> 44.1 us
-        if (MEV_PRIO_POST >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_POST);
-        cars_post<TRAFFIC, true, NpcLDST<KM>, PK>(p, out, e, el, nl, cx);
-    }
-    if (MEV_WB_LATE && !MEV_FUSED_STAGED) ego_writeback(p, e, p.N, NS, el, cx.do_reset, lane);
-    if constexpr (TRAFFIC) {
-        if (MEV_NPC_DEFER_WB) npc_writeback(p, e, *nl, cx.ncnt, lane);  // (deferred: see npc_phase)
-        if (MEV_DEAL_LATE) deal_append<TRAFFIC>(p, in, cx, e);
-    }
-    if (MEV_FUSED_STAGED) {
-        wave_lds_sync();
-        fused_store<TAB>(p, out, e, el, reinterpret_cast<const int*>(lbase + lay.res), lane);
-    }
-#if defined(MEV_STAMPS_R)  // slot 7: end of the wave (low 40 bits) | where it ran (HW_ID[15:0], XCC_ID[2:0]) << 40
-    if (!SPLIT || wv == 1) {
-        const unsigned long long t = __builtin_amdgcn_s_memrealtime() & ((1ull << 40) - 1);
-        const unsigned hw = __builtin_amdgcn_s_getreg((15 << 11) | 4) & 0xffffu;
-        const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
-        if (lane == 0) p.debug[e * 8 + 7] = t | ((unsigned long long)(hw | (xcc << 16)) << 40);
-    }
-#endif
-}
-
 template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
 __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_ESPLIT_WPE : (SPLIT ? MEV_SPLIT_WPE : 4)) void k_step(
     const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
-    step_body<TRAFFIC, TAB, NM, KM, PK, SPLIT, ESPLIT>(pp, in, out);
+#include "mev_step_body.inc"
 }
 
 // ------------------------------------------------- persistent step server ---
@@ -3612,7 +3395,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_
 // per step launched).  Wave 0 of each workgroup polls the command
 // line of the ServeBox (system-scope loads of host-coherent memory) until a new
 // command, a stop, or sa.idle_ticks of the 100 MHz clock without one; it hands the
-// command to the other wave through LDS.  A step runs step_body -- the same code
+// command to the other wave through LDS.  A step runs k_step's body (mev_step_body.inc) -- the same code
 // as k_step, the same grid -- reading the actions from and writing the outputs to
 // the handle's pinned block; then every wave releases its writes at system scope
 // and workgroup b publishes done[b] = the command's number.  Every exit (stop, or
@@ -3624,6 +3407,8 @@ template <bool TRAFFIC, bool TAB, int NM, int KM, bool SPLIT>
 __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? MEV_SPLIT_WPE : 4) void k_serve(
     const SimParams* __restrict__ pp, ServeArgs sa, Outputs out) {
     __shared__ uint32_t cmdw[kServeLine];
+    constexpr int PK = 1;
+    constexpr bool ESPLIT = false;
     const int lane = threadIdx.x & (WAVE - 1);
     const bool w0 = threadIdx.x < WAVE;
     ServeBox* box = sa.box;
@@ -3667,7 +3452,9 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? MEV_SPLIT_WPE : 4)
         in.spawn_prob = __uint_as_float(cmdw[4]);
         in.auto_reset = (int32_t)cmdw[5];
         in.rng_counter = (uint64_t)cmdw[7] | ((uint64_t)cmdw[8] << 32);
-        step_body<TRAFFIC, TAB, NM, KM, 1, SPLIT, false>(pp, in, out);
+        [&]() {  // one step: k_step's body (its returns end the lambda)
+#include "mev_step_body.inc"
+        }();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this wave's outputs and state written
         __syncthreads();  // (also: nobody reads cmdw or the step's LDS any more)
         if (threadIdx.x == 0) __hip_atomic_store(&box->done[blockIdx.x], sid, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
