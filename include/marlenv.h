@@ -259,8 +259,10 @@ int mev_get_step_split(const mev_handle* h, int32_t* split);
  * the host posts the step in a mailbox of pinned memory and the kernel answers
  * once its outputs are there -- a PCIe round trip instead of a kernel launch and
  * a stream synchronisation.  The kernel leaves after `idle` ms without a step
- * (MEV_SERVE_IDLE_MS, default 50) and is launched again by the next one; every
- * other call on the handle stops it first.  mode: 0 = off, 1 = automatic
+ * (MEV_SERVE_IDLE_MS, default 20) and is launched again by the next one; every
+ * other call on the handle stops it first.  Only on the handle's own stream (not
+ * after mev_set_stream).  While it is resident a device-wide synchronisation
+ * (hipDeviceSynchronize) waits for its idle exit.  mode: 0 = off, 1 = automatic
  * (default; MEV_NO_SERVE=1 in the environment turns it off).  mev_serve_stats:
  * steps served, server launches, whether one is running.  Replaces nothing in the
  * reference (its env.py steps one IntersectionEnv per call on the CPU,

@@ -728,7 +728,7 @@ inline void cpu_relax() {
 uint32_t serve_idle_ticks() {
     static const uint32_t ms = [] {
         const char* v = getenv("MEV_SERVE_IDLE_MS");
-        const int m = v ? atoi(v) : 50;
+        const int m = v ? atoi(v) : 20;
         return (uint32_t)(m < 1 ? 1 : (m > 1000 ? 1000 : m));
     }();
     return ms * 100000u;  // s_memrealtime: 100 MHz
@@ -782,7 +782,10 @@ static int serve_stop(mev_handle* h) {
 // whether a host-mode step of h (pinned block ready) goes to the server
 static bool serve_wanted(mev_handle* h) {
     static const bool off = [] { const char* v = getenv("MEV_NO_SERVE"); return v && v[0] == '1'; }();
-    if (off || h->serve_mode == 0 || !h->tev.empty() || !mev::serve_fits(h->sp)) return false;
+    // (only on the handle's own non-blocking stream: a resident server would hold back
+    // whatever a caller queues behind it on a stream it shares)
+    if (off || h->serve_mode == 0 || !h->tev.empty() || h->stream != h->own_stream || !mev::serve_fits(h->sp))
+        return false;
     if (h->sbox) return true;
     void* hp = nullptr;
     if (hipHostMalloc(&hp, sizeof(mev::ServeBox), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return false;

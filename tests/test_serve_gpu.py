@@ -122,3 +122,28 @@ def test_large_handles_are_not_served(mev):
     a.step(np.zeros((128, 1, 2), np.float32))
     assert a.serve_stats()["steps"] == 0
     a.close()
+
+
+def test_torch_work_runs_beside_a_resident_server(mev):
+    import torch
+    a = mev.Handle(num_envs=1, num_agents=1, lidar_rays=16)
+    a.reset()
+    act = np.zeros((1, 1, 2), np.float32)
+    a.step(act)
+    assert a.serve_stats()["running"]
+    x = torch.ones(4096, device="cuda")
+    (x * 2).sum().item()  # (the first torch kernels may take longer than the server's idle limit)
+    a.step(act)
+    n0 = a.serve_stats()["launches"]
+    t0 = time.perf_counter()
+    for _ in range(50):
+        a.step(act)
+        (x * 2).sum().item()  # torch's stream, synchronised every call, while the server stays resident
+    dt = (time.perf_counter() - t0) / 50
+    assert dt < 0.005, dt  # nothing waits for the server's idle exit
+    assert a.serve_stats()["launches"] == n0  # it stayed resident throughout
+    a.set_stream(torch.cuda.current_stream().cuda_stream)  # a shared stream: launched steps only
+    a.step(act)
+    assert not a.serve_stats()["running"]
+    assert a.serve_stats()["steps"] == 52
+    a.close()
