@@ -147,3 +147,37 @@ def test_torch_work_runs_beside_a_resident_server(mev):
     assert not a.serve_stats()["running"]
     assert a.serve_stats()["steps"] == 52
     a.close()
+
+
+@pytest.mark.parametrize("traffic", [False, True], ids=["egos", "traffic"])
+def test_env_py_through_the_server(traffic):
+    """The drop-in env.py (one env per call) with its handle served and not served:
+    the same observations, rewards, flags, info and traffic cars at every step."""
+    import pkgload
+    pkgload.load()
+    from marl_traffic_intersection_amd import env as envmod
+    cfg = {"num_agents": 1 if traffic else 3, "traffic_flow": traffic, "traffic_density": 2.0}
+    envs = [envmod.IntersectionEnv(dict(cfg)) for _ in range(2)]
+    rng = np.random.default_rng(11)
+    n = 1 if traffic else 3
+    first = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+    for e in envs:
+        e.step(first)
+    envs[1].env._sync().set_serve(0)
+    for t in range(150):
+        act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        ra, rb = envs[0].step(act), envs[1].step(act)
+        assert np.array_equal(ra[0], rb[0]), t
+        assert np.array_equal(np.asarray(ra[1]), np.asarray(rb[1])), t
+        assert ra[2:4] == rb[2:4] and ra[4] == rb[4], t
+        if traffic and t % 10 == 0:
+            ca, cb = envs[0].traffic_cars, envs[1].traffic_cars
+            assert [(c.state.x, c.state.y, c.state.heading, c.path_index) for c in ca] == \
+                   [(c.state.x, c.state.y, c.state.heading, c.path_index) for c in cb], t
+        if ra[2] or ra[3]:
+            envs[0].reset()
+            envs[1].reset()
+    assert envs[0].env._sync().serve_stats()["steps"] > 100
+    assert envs[1].env._sync().serve_stats()["steps"] == 0
+    for e in envs:
+        e.close()
