@@ -261,7 +261,9 @@ int mev_get_step_split(const mev_handle* h, int32_t* split);
  * a stream synchronisation.  The kernel leaves after `idle` ms without a step
  * (MEV_SERVE_IDLE_MS, default 20) and is launched again by the next one; every
  * other call on the handle stops it first.  Only on the handle's own stream (not
- * after mev_set_stream).  While it is resident a device-wide synchronisation
+ * after mev_set_stream); the kernel itself runs on a non-blocking highest-priority
+ * stream of its own; at most 2 servers are resident per process (other handles
+ * step launched).  While it is resident a device-wide synchronisation
  * (hipDeviceSynchronize) waits for its idle exit.  mode: 0 = off, 1 = automatic
  * (default; MEV_NO_SERVE=1 in the environment turns it off).  mev_serve_stats:
  * steps served, server launches, whether one is running.  Replaces nothing in the

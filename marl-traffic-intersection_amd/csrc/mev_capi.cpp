@@ -11,6 +11,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <mutex>
 #include <cstdio>
 #include <string>
 #include <thread>
@@ -164,6 +165,11 @@ struct mev_handle {
     int serve_wg = 0;                   // its workgroups
     uint32_t serve_seq = 0, serve_sid = 0, serve_epoch = 0;
     uint64_t serve_steps = 0, serve_launches = 0;
+    // the server's own stream: non-blocking, at the highest priority, whose hardware
+    // queues are not the ones normal-priority streams share (GPU_MAX_HW_QUEUES of them):
+    // a resident kernel holds back whatever another stream queues behind it on its queue
+    hipStream_t serve_stream = nullptr;
+    hipEvent_t serve_ev = nullptr;  // orders the server after the handle's stream
     uint8_t* gs_pin = nullptr;  // pinned staging of mev_get_state
     size_t gs_cap = 0;
     ~mev_handle() {
@@ -172,6 +178,8 @@ struct mev_handle {
         free_timing();
         if (pin) (void)hipHostFree(pin);
         if (sbox) (void)hipHostFree(sbox);
+        if (serve_ev) (void)hipEventDestroy(serve_ev);
+        if (serve_stream) (void)hipStreamDestroy(serve_stream);
         if (gs_pin) (void)hipHostFree(gs_pin);
         if (d_snap_stage) (void)hipFree(d_snap_stage);
         for (void* p : allocs) (void)hipFree(p);
@@ -182,6 +190,9 @@ struct mev_handle {
 extern "C" {
 
 static int serve_stop(mev_handle* h);  // with mev_step: the resident step server leaves the stream
+namespace {
+void serve_unlist(mev_handle* h);  // (with mev_step) the handle leaves the resident-server list
+}  // namespace
 
 const char* mev_last_error(void) { return g_err.c_str(); }
 int mev_abi_version(void) { return MEV_ABI_VERSION; }
@@ -438,6 +449,7 @@ int mev_destroy(mev_handle* h) {
     if (!h) return MEV_OK;
     (void)hipSetDevice(h->cfg.device);
     (void)serve_stop(h);
+    serve_unlist(h);
     (void)hipStreamSynchronize(h->stream);
     delete h;
     return MEV_OK;
@@ -750,11 +762,51 @@ int serve_launch(mev_handle* h) {
     sa.spawn_route = reinterpret_cast<const int32_t*>(h->pin_dev + h->pin_off[1]);
     sa.epoch = ++h->serve_epoch;
     sa.idle_ticks = serve_idle_ticks();
-    HIP_TRY(mev::launch_serve(h->sp, h->d_sp, sa, h->pin_out, h->stream));
+    HIP_TRY(hipEventRecord(h->serve_ev, h->stream));  // after whatever the handle's stream holds
+    HIP_TRY(hipStreamWaitEvent(h->serve_stream, h->serve_ev, 0));
+    HIP_TRY(mev::launch_serve(h->sp, h->d_sp, sa, h->pin_out, h->serve_stream));
     h->serve_running = true;
     h->serve_wg = h->sp.E;
     ++h->serve_launches;
     return MEV_OK;
+}
+
+// Resident servers per process are capped: their high-priority hardware queues are
+// few, and a server launched behind another one's on a shared queue would wait for its
+// idle exit.  Handles beyond the cap step launched (same results).
+constexpr int kMaxResidentServers = 2;
+std::mutex g_serve_mu;
+std::vector<mev_handle*> g_serving;  // handles whose server may be resident
+
+// whether h's server is still resident (some workgroup has not yet left)
+bool serve_resident(const mev_handle* h) {
+    if (!h->serve_running) return false;
+    const volatile mev::ServeBox* b = h->sbox;
+    for (int w = 0; w < h->serve_wg; ++w)
+        if (b->exited[w] != h->serve_epoch) return true;
+    return false;
+}
+
+// h may keep or start a resident server
+bool serve_slot(mev_handle* h) {
+    std::lock_guard<std::mutex> lk(g_serve_mu);
+    if (h->serve_running) return true;
+    int n = 0;
+    for (const mev_handle* x : g_serving) n += (x != h && serve_resident(x)) ? 1 : 0;
+    if (n >= kMaxResidentServers) return false;
+    bool listed = false;
+    for (const mev_handle* x : g_serving) listed |= x == h;
+    if (!listed) g_serving.push_back(h);
+    return true;
+}
+
+void serve_unlist(mev_handle* h) {
+    std::lock_guard<std::mutex> lk(g_serve_mu);
+    for (size_t i = 0; i < g_serving.size(); ++i)
+        if (g_serving[i] == h) {
+            g_serving.erase(g_serving.begin() + long(i));
+            break;
+        }
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -775,7 +827,7 @@ static int serve_stop(mev_handle* h) {
             cpu_relax();
         }
     h->serve_running = false;
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipStreamSynchronize(h->serve_stream));  // the server's grid has drained
     return MEV_OK;
 }
 
@@ -787,6 +839,20 @@ static bool serve_wanted(mev_handle* h) {
     if (off || h->serve_mode == 0 || !h->tev.empty() || h->stream != h->own_stream || !mev::serve_fits(h->sp))
         return false;
     if (h->sbox) return true;
+    if (!h->serve_stream || !h->serve_ev) {
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return false;
+        if (hipStreamCreateWithPriority(&h->serve_stream, hipStreamNonBlocking, hi) != hipSuccess) {
+            h->serve_stream = nullptr;
+            return false;
+        }
+        if (hipEventCreateWithFlags(&h->serve_ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamDestroy(h->serve_stream);
+            h->serve_stream = nullptr;
+            h->serve_ev = nullptr;
+            return false;
+        }
+    }
     void* hp = nullptr;
     if (hipHostMalloc(&hp, sizeof(mev::ServeBox), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return false;
     void* dp = nullptr;
@@ -875,7 +941,7 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     in.auto_reset = (a->flags & MEV_AUTO_RESET) ? 1 : 0;
     in.rng_counter = h->rng_counter++;
     const bool pinned = !dev && !gather && pin_ready(h);  // zero-copy host mode (small handles)
-    const bool serve = pinned && serve_wanted(h);         // ... answered by the resident step server
+    const bool serve = pinned && serve_wanted(h) && serve_slot(h);  // ... answered by the resident step server
     if (!serve)
         if (int r = serve_stop(h)) return r;
     if (dev) {

@@ -181,3 +181,49 @@ def test_env_py_through_the_server(traffic):
     assert envs[1].env._sync().serve_stats()["steps"] == 1  # (its first step, before set_serve(0))
     for e in envs:
         e.close()
+
+
+def test_several_served_handles_at_once(mev):
+    """Four single-env handles stepped round-robin (a process running several env.py envs)
+    against four launched twins: the first two get resident servers (the per-process cap)."""
+    served = [mev.Handle(seed=s, num_envs=1, num_agents=2, lidar_rays=32) for s in range(4)]
+    launched = [mev.Handle(seed=s, num_envs=1, num_agents=2, lidar_rays=32) for s in range(4)]
+    for h in launched:
+        h.set_serve(0)
+    for h in served + launched:
+        h.reset()
+    rng = np.random.default_rng(9)
+    t0 = time.perf_counter()
+    for t in range(100):
+        for i in range(4):
+            act = rng.uniform(-1, 1, (1, 2, 2)).astype(np.float32)
+            _same(served[i].step(act, auto_reset=True), launched[i].step(act, auto_reset=True), (t, i))
+    # nothing waits for a server's idle exit: each server has a hardware queue of its own
+    # (sharing one, each launched step would wait ~20 ms behind a resident server)
+    assert time.perf_counter() - t0 < 2.0
+    st = [h.serve_stats() for h in served]
+    assert [x["steps"] for x in st] == [100, 100, 0, 0], st  # two resident servers per process at most
+    for h in served + launched:
+        h.close()
+
+
+def test_resident_servers_are_capped(mev):
+    """More single-env handles than the per-process cap of resident servers: the rest step
+    launched, every handle stays exact, and nobody waits behind another handle's server."""
+    hs = [mev.Handle(seed=s, num_envs=1, num_agents=1, lidar_rays=16) for s in range(6)]
+    twins = [mev.Handle(seed=s, num_envs=1, num_agents=1, lidar_rays=16) for s in range(6)]
+    for h in twins:
+        h.set_serve(0)
+    for h in hs + twins:
+        h.reset()
+    rng = np.random.default_rng(4)
+    t0 = time.perf_counter()
+    for t in range(100):
+        for i in range(6):
+            act = rng.uniform(-1, 1, (1, 1, 2)).astype(np.float32)
+            _same(hs[i].step(act, auto_reset=True), twins[i].step(act, auto_reset=True), (t, i))
+    assert time.perf_counter() - t0 < 2.0
+    served = [h.serve_stats()["steps"] for h in hs]
+    assert sum(s > 0 for s in served) == 2, served  # kMaxResidentServers
+    for h in hs + twins:
+        h.close()
