@@ -227,3 +227,28 @@ def test_resident_servers_are_capped(mev):
     assert sum(s > 0 for s in served) == 2, served  # kMaxResidentServers
     for h in hs + twins:
         h.close()
+
+
+def test_get_state_partial_fields(mev):
+    """mev_get_state stages through pinned memory (one copy per SoA block): any subset of
+    fields reads the same values as the full call."""
+    import ctypes
+    from marl_traffic_intersection_amd import _capi
+    h = mev.Handle(num_envs=5, num_agents=3, lidar_rays=16, traffic_flow=1, traffic_density=4.0, max_npcs=32)
+    h.reset()
+    rng = np.random.default_rng(2)
+    for _ in range(60):
+        h.step(rng.uniform(-1, 1, (5, 3, 2)).astype(np.float32), auto_reset=True)
+    full = h.get_state()
+    for pick in (["heading"], ["intention", "npc_route"], ["npc_alive", "step_count"], ["alive", "npc_count", "y"]):
+        st = _capi.MevState()
+        got = {}
+        for name, dt, per in _capi.STATE_FIELDS:
+            if name in pick:
+                got[name] = np.full(h._shape(per), 77, dt)
+                setattr(st, name, got[name].ctypes.data)
+        _capi._check(h._lib.mev_get_state(h._h, ctypes.byref(st)))
+        for k, v in got.items():
+            assert np.array_equal(v, full[k]), (pick, k)
+    assert full["npc_count"].sum() > 0
+    h.close()
