@@ -3382,8 +3382,11 @@ struct RoadHook {
 #ifndef MEV_ESPLIT_ILP
 #define MEV_ESPLIT_ILP 1
 #endif
+#ifndef MEV_KSTEP_ATTR  // experiments: extra kernel attributes of k_step (e.g. a waves-per-EU cap)
+#define MEV_KSTEP_ATTR
+#endif
 template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
-__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_ESPLIT_WPE : (SPLIT ? MEV_SPLIT_WPE : 4)) void k_step(
+__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_ESPLIT_WPE : (SPLIT ? MEV_SPLIT_WPE : 4)) MEV_KSTEP_ATTR void k_step(
     const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
 #include "mev_step_body.inc"
 }

@@ -103,6 +103,9 @@ EXPERIMENTS = {"exp_noroad": ["-DMEV_EXP_NOROAD"], "exp_nocars": ["-DMEV_EXP_NOC
                "mixs0": ["-DMEV_MIX=1", "-DMEV_MIX_SHIFT=0"],
                # traffic: the NPC write-back and the deal's append at the end of k_step (product: where the
                # NPC phase / the car part ends)
+               # k_step's register allocation aimed at exactly 4 waves per SIMD (up to 128 VGPRs)
+               "wpe44": ["-DMEV_KSTEP_ATTR=__attribute__((amdgpu_waves_per_eu(4,4)))"],
+               "relaxocc": ["-mllvm", "--amdgpu-schedule-relaxed-occupancy"],
                "npcwblate": ["-DMEV_NPC_DEFER_WB=1"], "deallate": ["-DMEV_DEAL_LATE=1"],
                "bothlate": ["-DMEV_NPC_DEFER_WB=1", "-DMEV_DEAL_LATE=1"],
                # deliberately wrong: beam spans narrowed, to show the stress test catches it
