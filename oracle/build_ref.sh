@@ -1,7 +1,9 @@
 #!/usr/bin/env bash
 # TEST INFRASTRUCTURE ONLY.  Builds the reference simulator from its own source
 # files where they lie under /root/reference/cpp (nothing is copied into this
-# repo) plus our harness (oracle/ref_harness.cpp) into oracle/_ref/libref_harness.so.
+# repo) plus our harness (oracle/ref_harness.cpp) into $MEV_REF_BUILD/libref_harness.so
+# (default /tmp/marl_ref_build): OUTSIDE the repository tree, so nothing built from the
+# reference can travel to the GPU box with a repository snapshot.
 #
 # Recipe notes:
 #  * Only the simulation translation units are compiled: Car, Lidar, LineMask,
@@ -22,7 +24,7 @@
 set -euo pipefail
 HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 REF="${MARL_REFERENCE_DIR:-/root/reference}/cpp"
-OUT="$HERE/_ref"
+OUT="${MEV_REF_BUILD:-/tmp/marl_ref_build}"
 if [[ ! -f "$REF/IntersectionEnv.cpp" ]]; then
     echo "build_ref.sh: reference sources not found at $REF; skipping" >&2
     exit 0

@@ -2,7 +2,7 @@
 //
 // C-callable harness around the UNMODIFIED reference simulator
 // (/root/reference/cpp, compiled in place by oracle/build_ref.sh into
-// oracle/_ref/libref_harness.so).  It is used for exactly two things:
+// $MEV_REF_BUILD/libref_harness.so, outside the repository).  It is used for exactly two things:
 //   1. generating the golden vectors under tests/golden/ (tests/golden/gen_golden.py);
 //   2. the `cpu_baseline` leg of bench.py (kind "reference").
 //

@@ -1,7 +1,9 @@
-"""TEST INFRASTRUCTURE ONLY: ctypes driver for oracle/_ref/libref_harness.so.
+"""TEST INFRASTRUCTURE ONLY: ctypes driver for $MEV_REF_BUILD/libref_harness.so.
 
 The library is the UNMODIFIED reference simulator (cpp/*.cpp of the reference,
-built in place by oracle/build_ref.sh) plus oracle/ref_harness.cpp.  Only
+built in place by oracle/build_ref.sh) plus oracle/ref_harness.cpp.  The build
+lives outside the repository (default /tmp/marl_ref_build), so it never travels
+to the GPU box.  Only
 tests/golden/gen_golden.py and bench.py's ``cpu_baseline`` leg use it.
 """
 from __future__ import annotations
@@ -13,7 +15,8 @@ from typing import Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_ref", "libref_harness.so")
+REF_BUILD = os.environ.get("MEV_REF_BUILD", "/tmp/marl_ref_build")
+LIB_PATH = os.path.join(REF_BUILD, "libref_harness.so")
 
 NF = 15  # float fields per car record (see ref_harness.cpp car_to_rec)
 NI = 4   # int fields: alive, intention, path_index, route

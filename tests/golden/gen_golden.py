@@ -1,7 +1,7 @@
 """Generate the golden vectors in tests/golden/*.npz from the REAL reference.
 
 TEST INFRASTRUCTURE.  Runs only in the build container, where /root/reference
-exists and oracle/build_ref.sh has produced oracle/_ref/libref_harness.so (the
+exists and oracle/build_ref.sh has produced $MEV_REF_BUILD/libref_harness.so (the
 unmodified reference simulator + our harness).  The .npz files it writes are
 committed; the GPU box never needs the reference.
 
