@@ -252,6 +252,12 @@ int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave);
  * nothing in the reference. */
 int mev_set_step_split(mev_handle* h, int32_t mode);
 int mev_get_step_split(const mev_handle* h, int32_t* split);
+/* Scheduling (results are identical either way): the NPC-aware env deal of the
+ * fused traffic k_step -- workgroups take envs heaviest NPC count first, from
+ * orders the previous step built.  on: 1 (default; MEV_NO_DEAL=1 in the
+ * environment makes 0 the default), 0 = the XCD-aware identity order.  Replaces
+ * nothing in the reference. */
+int mev_set_env_deal(mev_handle* h, int32_t on);
 /* Host-mode steps as a persistent step server (results are identical either
  * way).  A step with host buffers (no MEV_DEVICE_PTRS) of a small handle (<= 64
  * envs, outputs <= 256 KB, the fused kernel, no traffic above one ego / 32 NPC

@@ -42,7 +42,7 @@ EXPORTED = (
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
     "mev_kernel_timing", "mev_kernel_times", "mev_set_reset_routes", "mev_snapshot_size", "mev_snapshot",
     "mev_restore", "mev_set_step_kernel", "mev_get_step_kernel", "mev_set_step_pack", "mev_get_step_pack",
-    "mev_set_step_split", "mev_get_step_split", "mev_set_serve", "mev_serve_stats",
+    "mev_set_step_split", "mev_get_step_split", "mev_set_env_deal", "mev_set_serve", "mev_serve_stats",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
     "mev_gather_wait", "mev_output_dlpack", "mev_packed_layout2", "mev_set_gather_format", "mev_lidar_decode_table",
 )
@@ -151,6 +151,7 @@ def load_library(variant: str = None):
     L.mev_set_step_pack.argtypes = [_vp, ctypes.c_int32]
     L.mev_get_step_pack.argtypes = [_vp, i32p]
     L.mev_set_step_split.argtypes = [_vp, ctypes.c_int32]
+    L.mev_set_env_deal.argtypes = [_vp, ctypes.c_int32]
     L.mev_get_step_split.argtypes = [_vp, i32p]
     L.mev_set_serve.argtypes = [_vp, ctypes.c_int32]
     L.mev_serve_stats.argtypes = [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), i32p]
@@ -579,6 +580,10 @@ class Handle:
         """Two waves per fused workgroup: 0 automatic, 1 off, 2 on, 3 early split (scheduling only;
         results identical)."""
         _check(self._lib.mev_set_step_split(self._h, int(mode)))
+
+    def set_env_deal(self, on: bool = True):
+        """The fused traffic kernel's NPC-aware env deal on / off (scheduling only; results identical)."""
+        _check(self._lib.mev_set_env_deal(self._h, 1 if on else 0))
 
     def step_split(self) -> int:
         """Two waves per fused workgroup in the next step: 0 no, 1 split, 2 early split."""

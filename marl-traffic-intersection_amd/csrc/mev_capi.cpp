@@ -101,6 +101,7 @@ struct mev_handle {
     // NPC-aware deal of the fused traffic kernel: valid while every step since the
     // last state change went through it (the rings then hold one entry per env)
     bool deal_valid = false;
+    bool deal_on = true;  // mev_set_env_deal (default: on unless MEV_NO_DEAL=1)
     int deal_ring = 0;
 
     template <class T>
@@ -257,6 +258,10 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
 
     auto* h = new mev_handle();
     h->cfg = c;
+    {
+        const char* nd = getenv("MEV_NO_DEAL");
+        h->deal_on = !(nd && nd[0] == '1');
+    }
     if (h->cfg.traffic_density < 0.0f) h->cfg.traffic_density = 0.0f;  // configure_traffic (:56-60)
     h->D = D;
     h->lidar_slots = std::min(c.lidar_rays, D - mev::OBS_HEAD);
@@ -349,7 +354,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&p.ob_box, size_t(E) * size_t(N + c.max_npcs)); A(&p.ob_cand, EN * 2);
     if (c.traffic_flow) {  // the fused traffic kernel's NPC-aware deal (mev_kernels.h, kDealLists)
         A(&p.deal_cnt, size_t(3) * mev::kDealRingInts);
-        A(&p.deal_order, size_t(mev::kDealLists) * mev::kDealClasses * size_t(E));
+        A(&p.deal_order, size_t(3) * mev::kDealLists * mev::kDealClasses * size_t(E));
     }
     // outputs
     A(&h->internal.obs, EN * size_t(D)); A(&h->internal.rew, EN); A(&h->internal.done, EN); A(&h->internal.status, EN);
@@ -1000,9 +1005,8 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         memcpy(&h->sp_dev, &h->sp, sizeof(mev::SimParams));
         h->sp_valid = true;
     }
-    // the NPC-aware deal (fused traffic k_step only; MEV_NO_DEAL=1 turns it off)
-    static const bool no_deal = [] { const char* v = getenv("MEV_NO_DEAL"); return v && v[0] == '1'; }();
-    const bool deal = !serve && h->sp.traffic && h->sp.deal_cnt && !no_deal && mev::step_kernel_for(h->sp) == 2;
+    // the NPC-aware deal (fused traffic k_step only; mev_set_env_deal)
+    const bool deal = !serve && h->sp.traffic && h->sp.deal_cnt && h->deal_on && mev::step_kernel_for(h->sp) == 2;
     if (deal) {
         if (!h->deal_valid) {  // fresh rings: this step deals by the identity order and builds the next
             HIP_TRY(hipMemsetAsync(h->sp.deal_cnt, 0, size_t(3) * mev::kDealRingInts * sizeof(int32_t), h->stream));
@@ -1299,6 +1303,14 @@ int mev_set_step_split(mev_handle* h, int32_t mode) {
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->sp.step_split = mode;
+    return MEV_OK;
+}
+
+int mev_set_env_deal(mev_handle* h, int32_t on) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    if (on != 0 && on != 1) return fail(MEV_E_INVALID, "env deal must be 0 (off) or 1 (on)");
+    h->deal_on = on != 0;
+    h->deal_valid = false;  // the next step deals by the identity order (and rebuilds the rings)
     return MEV_OK;
 }
 

@@ -114,7 +114,7 @@ struct SimParams {
     // NPC-aware env deal of the fused traffic kernel (see kDealLists): per (ring, list,
     // class) counters, each on its own 128-B line, and per (list, class) env orders
     int32_t* deal_cnt;    // [3][kDealLists][kDealClasses][kDealPad]
-    int32_t* deal_order;  // [kDealLists][kDealClasses][E]
+    int32_t* deal_order;  // [3][kDealLists][kDealClasses][E]: rings like the counters
 };
 
 // The fused traffic k_step deals envs to workgroups by their NPC count: every env
@@ -124,8 +124,10 @@ struct SimParams {
 // workgroups the dispatcher places -- one per SIMD -- hold the heaviest envs and
 // every SIMD's four wave slots get one env from each quarter of the NPC-count
 // order.  At the end of its step each env appends itself to the class list of
-// step t+1 (a counter atomic per (list, class)); rings of three counter sets:
-// step t reads ring t % 3, fills ring (t+1) % 3 and clears ring (t+2) % 3.
+// step t+1 (a counter atomic per (list, class)); rings of three counter sets and
+// three order sets: step t reads ring t % 3, fills ring (t+1) % 3 and clears the
+// counters of ring (t+2) % 3.  (With one order set, step t's early envs would
+// overwrite entries that workgroups starting later still have to read.)
 constexpr int kDealLists = 8;
 constexpr int kDealClasses = 8;  // NPC counts 0..6, 7 and more
 constexpr int kDealPad = 32;     // ints per counter (128 B)

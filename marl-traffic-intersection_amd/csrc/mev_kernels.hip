@@ -22,28 +22,24 @@ namespace mev {
 
 constexpr int WAVE = 64;
 
-// Diagnostic build only (-DMEV_STAMPS): per-env phase timestamps (s_memtime)
-// into SimParams::debug[e*8 + k]; never compiled into the product library.
-// -DMEV_STAMPS_X moves stamps 1-5 into k_cars' physics phase (STAMPX).
-// -DMEV_STAMPS_ES: the early split's per-env timeline (tools/es_timeline.py): wall clock
-// (s_memrealtime) of car-wave entry / barrier A / barrier B / end (slots 0-3) and
-// LiDAR-wave A passed / road end / B passed / end (4-7), lane 0 of the wave that gets there
-#ifdef MEV_STAMPS_ES
-#define ES_STAMP(k)                                                                              \
-    do {                                                                                         \
-        __builtin_amdgcn_wave_barrier();                                                         \
-        if ((threadIdx.x & 63) == 0) p.debug[e * 8 + (k)] = __builtin_amdgcn_s_memrealtime();   \
-    } while (0)
-#else
-#define ES_STAMP(k) do {} while (0)
-#endif
+// Diagnostic builds only, never compiled into the product library:
+//  -DMEV_STAMPS: per-env phase timestamps (s_memtime) into SimParams::debug[e*8 + k]
+//   (tools/phase_profile.py);
+//  -DMEV_STAMPS -DMEV_STAMPS_R: a wall-clock (s_memrealtime, 100 MHz) timeline of
+//   each wave -- entry, after the loads, end, and where it ran (tools/simd_balance.py);
+//   MEV_STAMPS_POSTEND=1 moves slot 2 to the end of cars_post;
+//  -DMEV_STAMPS_N: the NPC phase's parts (tools/npc_profile.py --parts);
+//  -DMEV_EXP_STOP=n: timing-only builds stopped after part n of k_step (phase budgets,
+//   tools/phase_budget.sh).
+// Experiment variants measured and rejected in earlier rounds are recorded in
+// DESIGN.md §9 and live in git history (before round 4), not here.
 #ifdef MEV_STAMPS
 #define STAMP_RAW(k)                                                     \
     do {                                                                 \
         __builtin_amdgcn_wave_barrier();                                 \
         if (threadIdx.x == 0) p.debug[e * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
-#if defined(MEV_STAMPS_R)  // wall-clock (s_memrealtime, 100 MHz) timeline: entry, after the loads, end
+#if defined(MEV_STAMPS_R)
 #undef STAMP_RAW
 #define STAMP_RAW(k)                                                     \
     do {                                                                 \
@@ -54,80 +50,32 @@ constexpr int WAVE = 64;
 #define MEV_STAMPS_POSTEND 0
 #endif
 #define STAMP(k) do { if ((k) == 0) STAMP_RAW(1); if ((k) == (MEV_STAMPS_POSTEND ? 6 : 5)) STAMP_RAW(2); } while (0)
-#define STAMPX(k) do {} while (0)
-#define STAMPY(k) do {} while (0)
-#elif defined(MEV_STAMPS_X)
-#define STAMP(k) do { if ((k) == 0 || (k) == 6) STAMP_RAW(k); } while (0)
-#define STAMPX(k) STAMP_RAW(k)
-#define STAMPY(k) do {} while (0)
-#elif defined(MEV_STAMPS_Y)  // stamps 1-5 in resolution, write-back, obstacles and the obs head
-#define STAMP(k) do { if ((k) == 0 || (k) == 6) STAMP_RAW(k); } while (0)
-#define STAMPX(k) do {} while (0)
-#define STAMPY(k) STAMP_RAW(k)
 #else
 #define STAMP(k) STAMP_RAW(k)
-#define STAMPX(k) do {} while (0)
-#define STAMPY(k) do {} while (0)
 #endif
 #else
 #define STAMP(k) do {} while (0)
-#define STAMPX(k) do {} while (0)
-#define STAMPY(k) do {} while (0)
 #endif
 constexpr int MAXN = 64;
 constexpr int MAXK = 64;
-constexpr int MAXOB = MAXN + MAXK;
 
 // k_step's issue priorities (s_setprio), falling as a wave's remaining work
 // shrinks: the four waves of a SIMD start together and the hardware otherwise
 // favours the oldest, so the wave with the most work left -- the one that sets
 // the SIMD's finish -- would be served last.  Cars and the first quarter of
 // LiDAR phase 1: 3, the rest of phase 1: 2, phase 2 (march): 1, phase 3 and the
-// block writes: 0 (measured +11 % over cars 1 / LiDAR 0).
-// -1 keeps the previous level.
-#ifndef MEV_PRIO_CARS
-#define MEV_PRIO_CARS 3
-#endif
-#ifndef MEV_PRIO_LIDAR
-#define MEV_PRIO_LIDAR 3
-#endif
-#ifndef MEV_PRIO_HEAD  // the car part's observation head
-#define MEV_PRIO_HEAD -1
-#endif
-#ifndef MEV_PRIO_P1B  // LiDAR phase 1 from MEV_PRIO_P1B_AT quarters of its agents on
-#define MEV_PRIO_P1B 2
-#endif
-#ifndef MEV_PRIO_P1B_AT
-#define MEV_PRIO_P1B_AT 1
-#endif
-#ifndef MEV_PRIO_P2
-#define MEV_PRIO_P2 1
-#endif
-#ifndef MEV_PRIO_P3
-#define MEV_PRIO_P3 0
-#endif
-// k_step runs cars_post right after cars_pre (0) or after the LiDAR (1: its
-// latency-bound chain then overlaps other waves' LiDAR, but the waves end later:
-// measured 41.6 -> 44.1 us per step at config 3)
-#ifndef MEV_POST_AFTER_LIDAR
-#define MEV_POST_AFTER_LIDAR 0
-#endif
-#ifndef MEV_PRIO_POST  // k_step's car part after the LiDAR (cars_post); -1 keeps the LiDAR's last level
-#define MEV_PRIO_POST -1
-#endif
-#ifndef MEV_PRIO_P4  // the LiDAR block writes
-#define MEV_PRIO_P4 -1
-#endif
-#ifndef MEV_PRIO_HBM  // the LiDAR phases' schedule in k_lidar too (two-kernel path: 54.4 -> 50.7 us/step)
-#define MEV_PRIO_HBM 1
-#endif
+// block writes: 0 (measured +11 % over cars 1 / LiDAR 0).  k_lidar
+// (two-kernel path) runs the LiDAR phases' levels too (54.4 -> 50.7 us/step).
+constexpr int kPrioCars = 3;
+constexpr int kPrioLidar = 3;
+constexpr int kPrioP1B = 2;  // LiDAR phase 1 after the first quarter of its agents
+constexpr int kPrioP2 = 1;
+constexpr int kPrioP3 = 0;
 
 // With traffic: issue priority of the NPC controller by the NPCs an env has to
-// control (level = NPCs / MEV_NPC_PRIO, capped at 3; 0: off).  The env with the
-// most NPCs is the kernel's critical path (config 4: k_cars 53.9 -> 48.3 us).
-#ifndef MEV_NPC_PRIO
-#define MEV_NPC_PRIO 2
-#endif
+// control (level = NPCs / kNpcPrio, capped at 3).  The env with the most NPCs is
+// the kernel's critical path (config 4: k_cars 53.9 -> 48.3 us).
+constexpr int kNpcPrio = 2;
 
 // --------------------------------------------------------------- helpers ---
 // A pointer the kernel reads through SimParams as a global-memory pointer.  The
@@ -191,15 +139,8 @@ __device__ inline int lane_rank(unsigned long long mask) {
 // zero / infinite / NaN operand (then fdlibm's atan2f for the wave); bit-identical
 // either way (mev_math.h).  The branchy form runs every range and quadrant the
 // wave's lanes fall into one after another.
-#ifndef MEV_ATAN_BF
-#define MEV_ATAN_BF 1
-#endif
-// the NPC ghost scans skip others no scanned path point can reach (route piece boxes)
-#ifndef MEV_NPC_PREFILTER
-#define MEV_NPC_PREFILTER 1
-#endif
 __device__ inline float atan2f_wave(float y, float x) {
-    if (!MEV_ATAN_BF || ballot(atan2f_special(y, x))) return atan2f(y, x);
+    if (ballot(atan2f_special(y, x))) return atan2f(y, x);
     return atan2f_bf(y, x);
 }
 
@@ -338,11 +279,7 @@ __device__ inline int path_index_update(const float* path, int idx, float x, flo
 // consecutive envs -- and their shared lines, and the partial lines between
 // their observation rows -- on one XCD instead of fetching/merging them in
 // four L2s.  (Placement is a performance hint only: any bijection is correct.)
-#ifndef MEV_XCD_REMAP
-#define MEV_XCD_REMAP 1
-#endif
 __device__ inline int xcd_env(int b, int E) {
-    if (!MEV_XCD_REMAP) return b;
     const int q = E >> 3;
     return b < 8 * q ? (b & 7) * q + (b >> 3) : b;
 }
@@ -364,7 +301,8 @@ __device__ inline int deal_env(const SimParams& p, int ring, int b) {
         if (c == k && i >= n[k]) { i -= n[k]; c = k - 1; }
     }
     i = i < p.E - 1 ? i : p.E - 1;  // (the host keeps the rings consistent; never out of bounds)
-    return __builtin_amdgcn_readfirstlane(gmem(p.deal_order)[((size_t)x * kDealClasses + c) * p.E + i]);
+    const size_t ring_off = (size_t)ring * kDealLists * kDealClasses * (size_t)p.E;
+    return __builtin_amdgcn_readfirstlane(gmem(p.deal_order)[ring_off + ((size_t)x * kDealClasses + c) * p.E + i]);
 }
 
 // -------------------------------------------------------- shared state ---
@@ -479,12 +417,6 @@ __device__ inline int wave_argmin_dpp(float d, int i) {
 // terms: pose, speed, cos/sin of its heading, distance to the centre.  The
 // front-car and ghost-scan tests need only these thresholds, so a turn's plan
 // is ballots over j, not reductions.
-#ifndef MEV_NPC_SCANPF  // ghost points of the next scan pass loaded during this one (1.5 % slower: off)
-#define MEV_NPC_SCANPF 0
-#endif
-#ifndef MEV_NPC_FAR  // no exact distance for NPC pairs farther than 130 px (exact, within noise: off)
-#define MEV_NPC_FAR 0
-#endif
 struct NpcPair {
     bool f30, f50, pok, yfar;
 };
@@ -492,18 +424,13 @@ struct NpcPair {
 __device__ __forceinline__ NpcPair npc_pair(int k, float x, float y, float h, float v, float ck, float sk,
                                             float my_dist_to_center, bool jvalid, int j, float oxj, float oyj,
                                             float ohj, float ovj, float ocj, float osj, float odcj) {
-    const float CXf = WIDTH * 0.5f, CYf = HEIGHT * 0.5f;
     NpcPair r{false, false, false, false};
     const float vx = ck, vy = -sk;
     // |wrap(h - h_j)| and the distance to j: shared by the front-car test and the
     // ghost-scan filters (the same expressions in the reference, :37/:101/:107)
     const float dxj = oxj - x;
     const float dyj = oyj - y;
-    // the exact distance decides only for pairs within 125.1 px (the front-car test
-    // at 80, the side-by-side test at |lon| < 108 and |lat| < 63); a pair whose f32
-    // squared distance exceeds 130^2 takes none of those branches with either value
-    float dist_j = 1.0e30f;
-    if (!MEV_NPC_FAR || !(dxj * dxj + dyj * dyj > 16900.0f)) dist_j = hypotf(dxj, dyj);
+    const float dist_j = hypotf(dxj, dyj);
     const float adiff_j = fabs_f(wrap_angle(h - ohj));
     if (jvalid) {
         const float dist = dist_j;
@@ -614,33 +541,6 @@ __device__ __forceinline__ float npc_throttle(float acc_thr, float min_conflict)
     return thr;
 }
 
-#ifndef MEV_SAT_CIRCLE  // the car-car SAT behind a circumcircle test
-#define MEV_SAT_CIRCLE 1
-#endif
-#ifndef MEV_NPC_ODC  // the others' distances to the centre precomputed per NPC, not per pair
-#define MEV_NPC_ODC 1
-#endif
-#ifndef MEV_NPC_SOLO  // at most one alive NPC: part 1 moves it too (measured 2 % slower at config 4: off)
-#define MEV_NPC_SOLO 0
-#endif
-#ifndef MEV_NPC_KEEPSKIP  // no compaction pass when no NPC is erased
-#define MEV_NPC_KEEPSKIP 1
-#endif
-// The NPC state write-back at the end of k_step (1) or of the NPC phase (0), and the
-// NPC-aware deal's append at the end of k_step (1) or after the car part (0).
-// (the timing-only stop builds return early: they keep both where the car part ends)
-#if defined(MEV_EXP_STOP)
-#define MEV_NPC_DEFER_WB 0
-#define MEV_DEAL_LATE 0
-#endif
-// Measured (profiles/r3_ab_deferwb.txt): config 4 33.1 us with both where the car part
-// ends, 33.4 with both at the end -- not a drain on the critical path; off.
-#ifndef MEV_NPC_DEFER_WB
-#define MEV_NPC_DEFER_WB 0
-#endif
-#ifndef MEV_DEAL_LATE
-#define MEV_DEAL_LATE 0
-#endif
 // the surviving NPCs' state back to HBM (npc_phase's result, in nl)
 template <class NL>
 __device__ __forceinline__ void npc_writeback(const SimParams& p, int e, const NL& nl, int newcnt, int lane) {
@@ -654,12 +554,11 @@ __device__ __forceinline__ void npc_writeback(const SimParams& p, int e, const N
     if (lane == 0) gmem(p.npc.count)[e] = newcnt;
 }
 
-// store: write the NPC state back here (k_cars); k_step defers it to its end
-// (npc_writeback), because on gfx950 vmcnt counts stores too: the first wait for
-// a later load (the egos' path windows) would also wait for these stores to land.
+// The NPC state goes back to HBM at the end of the phase (measured against a
+// write-back at the end of k_step: config 4 33.1 vs 33.4 us, r3_ab_deferwb.txt).
 template <class NL>
 __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NL& nl, int lane,
-                          const float* ego_x, const float* ego_y, const NpcRegs& nr, const bool store = true) {
+                          const float* ego_x, const float* ego_y, const NpcRegs& nr) {
     const int K = p.K;
 #ifdef MEV_STAMPS_N
     unsigned long long nt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -783,32 +682,12 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // (:50-63) and Car::update's steering part with its tangent (Car.cpp:11-23;
     // the steering input is known before the throttle), the cruise throttle
     // (:66-70) and the distance to the centre (:83).
-    // solo (at most one alive NPC: nobody to plan against, the throttle is the
-    // cruise one): part 1 also moves it (round A's move) from a 128-point window
-    // loaded with the first one -- no second path load round trip.
-    const bool solo = MEV_NPC_SOLO && cnt <= 8 && __popcll(ballot(lane < cnt && nl.alive[lane < cnt ? lane : 0] != 0)) < 2;
     for (int k0 = 0; k0 < cnt; k0 += 8) {
         const int k = k0 + grp;
         const bool act = k < cnt;
         const int kk = act ? k : 0;  // idle groups mirror NPC 0 so every lane reaches the DPP moves
         const float x = nl.x[kk], y = nl.y[kk];
-#ifndef MEV_NPC_PREFETCH  // touch the path lines the ghost scans and moves read, while part 1 runs
-#define MEV_NPC_PREFETCH 0
-#endif
-        float2 pf0 = make_float2(0.0f, 0.0f), pf1 = pf0;
-        if (MEV_NPC_PREFETCH) {
-            const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
-            const int s0 = (nl.pidx[kk] < 0 ? 0 : nl.pidx[kk]) + 64 + sub * 16;
-            pf0 = P[s0 < PATH_LEN ? s0 : PATH_LEN - 1];
-            pf1 = P[s0 + 8 < PATH_LEN ? s0 + 8 : PATH_LEN - 1];
-        }
-        float2 pt[8], pt2[8];
-        if (solo) {  // path[start_i + 64 .. start_i + 127], in flight with the first window
-            const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
-            const int s2 = (nl.pidx[kk] < 0 ? 0 : nl.pidx[kk]) + 64 + sub * 8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pt2[j] = P[s2 + j < PATH_LEN ? s2 + j : PATH_LEN - 1];
-        }
+        float2 pt[8];
         int start_i;
         const int pidx0 = npc_window(kk, nl.pidx[kk], x, y, pt, start_i);
         // the look-ahead point min(pidx0 + 12, 159) lies in the 64-point window
@@ -833,60 +712,11 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             nl.mdc[k] = hypotf(x - CXf, y - CYf);
             nl.pidx0[k] = pidx0;
         }
-        if (solo) {
-            // every lane of the group: the target point (from the lane holding it), the
-            // steering, Car::update with the cruise throttle and the second path index
-            // over path[pidx0, pidx0 + 50) among the 128 window points (first minimum)
-            float2 tl = pt[0];
-#pragma unroll
-            for (int j = 1; j < 8; ++j) tl = ((toff & 7) == j) ? pt[j] : tl;
-            const int src = (grp * 8 + (toff >> 3)) * 4;
-            const float tx = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(tl.x)));
-            const float ty = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(tl.y)));
-            const float h = nl.h[kk], v = nl.v[kk];
-            const float heading_err = wrap_angle(atan2f_wave(-(ty - y), tx - x) - h);
-            float steer_cmd = heading_err * 3.0f;
-            steer_cmd = (1.0f < steer_cmd) ? 1.0f : steer_cmd;
-            steer_cmd = (steer_cmd < -1.0f) ? -1.0f : steer_cmd;
-            const float ns = car_steer(nl.steer[kk], steer_cmd);
-            const float nt = tanf(ns);
-            const float target_speed = PHYSICS_MAX_SPEED * 0.4f;
-            const float accb = (v < target_speed) ? 0.5f : ((v > target_speed + 1.0f) ? -0.1f : 0.0f);
-            Kin kin{x, y, v, h, nl.acc[kk], nl.steer[kk]};
-            float cn, sn;
-            car_update_steered(kin, accb, ns, nt, in.dt, &cn, &sn);
-            float bd = __builtin_inff();
-            int bi = 0x7fffffff;
-            auto scan_pt = [&](float2 w, int q) {
-                if (q >= pidx0 && q < pidx0 + 50 && q < PATH_LEN) {
-                    const float wdx = w.x - kin.x, wdy = w.y - kin.y;
-                    const float d = wdx * wdx + wdy * wdy;
-                    if (d < bd) { bd = d; bi = q; }
-                }
-            };
-#pragma unroll
-            for (int j = 0; j < 8; ++j) scan_pt(pt[j], start_i + sub * 8 + j);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) scan_pt(pt2[j], start_i + 64 + sub * 8 + j);
-            auto take = [&](float od, int oi) {
-                if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
-            };
-            take(dpp_f(bd, 0xB1), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xf, 0xf, false));    // quad_perm [1,0,3,2]
-            take(dpp_f(bd, 0x4E), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xf, 0xf, false));    // quad_perm [2,3,0,1]
-            take(dpp_f(bd, 0x141), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xf, 0xf, false));  // row_half_mirror
-            if (act && sub == 0 && nl.alive[k]) {
-                nl.thr_a[k] = accb;
-                nl.xn[k] = kin.x; nl.yn[k] = kin.y; nl.vn[k] = kin.v; nl.hn[k] = kin.h;
-                nl.accn[k] = kin.acc; nl.steern[k] = kin.steer; nl.cn[k] = cn; nl.sn[k] = sn;
-                nl.pidxn[k] = bi == 0x7fffffff ? (pidx0 < 0 ? 0 : pidx0) : bi;
-            }
-        }
         if (act && sub == 7) {  // the route's end point, for the arrival test after the turns
             const float2 pe = gf2(p.rt.path + (size_t)nl.route[k] * (2 * PATH_LEN))[PATH_LEN - 1];
             nl.endx[k] = pe.x;
             nl.endy[k] = pe.y;
         }
-        if (MEV_NPC_PREFETCH) asm volatile("" ::"v"(pf0.x), "v"(pf1.x));  // keep the touches (values unused)
     }
     wave_lds_sync();
     NT(1);  // part 1
@@ -903,8 +733,8 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // Otherwise the first NPC k* that differs takes its round-B throttle (its
     // inputs were right) and the NPCs after it run the sequential turns.
     const unsigned long long alive_k = ballot(lane < cnt && nl.alive[lane < cnt ? lane : 0] != 0);
-    if (MEV_NPC_PRIO) {  // the env with the most NPCs to control sets the kernel's end: serve it first
-        const int lvl = __popcll(alive_k) / MEV_NPC_PRIO;
+    {  // the env with the most NPCs to control sets the kernel's end: serve it first
+        const int lvl = __popcll(alive_k) / kNpcPrio;
         if (lvl >= 3) __builtin_amdgcn_s_setprio(3);
         else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
         else if (lvl == 1) __builtin_amdgcn_s_setprio(1);
@@ -950,7 +780,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const float oxj = newj ? nl.xn[jj] : nl.x[jj], oyj = newj ? nl.yn[jj] : nl.y[jj];
             const float ohj = newj ? nl.hn[jj] : nl.h[jj], ovj = newj ? nl.vn[jj] : nl.v[jj];
             const float ocj = newj ? nl.cn[jj] : nl.c[jj], osj = newj ? nl.sn[jj] : nl.s[jj];
-            const float odcj = MEV_NPC_ODC ? (newj ? nl.mdcn[jj] : nl.mdc[jj]) : hypotf(oxj - CXf, oyj - CYf);
+            const float odcj = newj ? nl.mdcn[jj] : nl.mdc[jj];
             // k's route pieces (bounding boxes), in flight during the pair tests
             const GF4 PB = gf4(p.rt.pbox + (size_t)nl.route[kk] * 3);
             const float4 pb0 = PB[0], pb1 = PB[1], pb2 = PB[2];
@@ -962,7 +792,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             // (beyond any float rounding of the squared distance) from every box the
             // scan window overlaps never hits, and leaves the scan's candidates
             bool reach = false;
-            if (MEV_NPC_PREFILTER && pr.pok) {
+            if (pr.pok) {
                 const int g0 = nl.pidx0[kk], g1 = g0 + 120 < PATH_LEN ? g0 + 120 : PATH_LEN;
                 const float R2 = (CAR_WIDTH * 2.0f + 0.01f) * (CAR_WIDTH * 2.0f + 0.01f);
                 auto near_box = [&](float4 b) {
@@ -974,7 +804,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                         (g1 > 110 && near_box(pb2));
             }
             const unsigned long long b30 = ballot(pr.f30), b50 = ballot(pr.f50);
-            const unsigned long long bok = ballot(MEV_NPC_PREFILTER ? reach : pr.pok), byf = ballot(pr.yfar);
+            const unsigned long long bok = ballot(reach), byf = ballot(pr.yfar);
             const int sh = kl << lk;
             float acc_thr = nl.accb[kk];
             if ((b30 >> sh) & seg) acc_thr = -1.0f;
@@ -1006,9 +836,6 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         // distance is the minimum
         const float SAFE = CAR_WIDTH * 2.0f;
         const float SAFE_SQ = SAFE * SAFE;
-#ifdef MEV_X_NOSCAN
-        scan_m = 0;
-#endif
         // the next (up to) four NPCs of scan_m: ks, their count, this lane's NPC
         auto next_batch = [&](int* ksv, int& nbv) {
             nbv = 0;
@@ -1022,33 +849,14 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const int u = lane >> 4;
             return u == 0 ? ksv[0] : (u == 1 ? ksv[1] : (u == 2 ? ksv[2] : ksv[3]));
         };
-        // MEV_NPC_SCANPF: the next pass's ghost points are loaded before this pass's
-        // tests (their path loads in flight meanwhile)
-        int ks[4], nb = 0;
-        float2 gpn[8];
-        if (MEV_NPC_SCANPF) {
-            next_batch(ks, nb);
-            if (nb) load_ghost8(lane_npc(ks), gpn);
-        } else if (scan_m) {
-            nb = 1;  // (the loop picks its batch itself)
-        }
+        int ks[4], nb = scan_m ? 1 : 0;  // (the loop picks its batch itself)
         while (nb) {
 #ifdef MEV_STAMPS_N
             nt_acc[5] += 1;  // scan passes
 #endif
             float2 gp[8];
-            if (MEV_NPC_SCANPF) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) gp[i] = gpn[i];
-            } else {
-                next_batch(ks, nb);
-                load_ghost8(lane_npc(ks), gp);
-            }
-            int ks2[4], nb2 = 0;
-            if (MEV_NPC_SCANPF) {
-                next_batch(ks2, nb2);
-                if (nb2) load_ghost8(lane_npc(ks2), gpn);
-            }
+            next_batch(ks, nb);
+            load_ghost8(lane_npc(ks), gp);
             const int u = lane >> 4;
             const int k = lane_npc(ks);
             const bool act = u < nb;
@@ -1116,21 +924,14 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                 if (!mixed) nl.mc_a[kq] = mc;
             }
             wave_lds_sync();
-            if (MEV_NPC_SCANPF) {
-#pragma unroll
-                for (int v = 0; v < 4; ++v) ks[v] = ks2[v];
-                nb = nb2;
-            } else {
-                nb = scan_m ? 1 : 0;
-            }
+            nb = scan_m ? 1 : 0;
         }
         NT(6);  // the ghost scans
     };
     // move the NPCs in `which` with the throttles thr into the round-A arrays
     // (xn .. sn, pidxn): Car::update with the steering from part 1 (Car.cpp:9-40)
     // and the second update_path_index (:343) over path[idx0, idx0 + 50), 8 lanes
-    // per NPC (7 window points each, first minimum wins).  pre: the window points
-    // of the first 8 NPCs, loaded before the plans
+    // per NPC (7 window points each, first minimum wins)
     auto load_window = [&](int kk, float2* w) {
         const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
         const int pidx0 = nl.pidx0[kk];
@@ -1140,26 +941,13 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             w[t] = P[q < PATH_LEN ? q : PATH_LEN - 1];
         }
     };
-#ifndef MEV_NPC_PREWIN  // the first move pass's window points loaded before the plans
-#define MEV_NPC_PREWIN 0
-#endif
-    float2 w0[7];
-    if (MEV_NPC_PREWIN && cnt > 0) load_window(grp < cnt ? grp : 0, w0);  // cnt = 0: no valid route to read
-    auto move_all = [&](const float* thr, unsigned long long which, bool use_pre) {
-#ifdef MEV_X_NOMOVE
-        return;
-#endif
+    auto move_all = [&](const float* thr, unsigned long long which) {
         for (int k0 = 0; k0 < cnt; k0 += 8) {
             const int k = k0 + grp;
             const int kk = k < cnt ? k : 0;
             const bool act = k < cnt && ((which >> kk) & 1ull);
             float2 w[7];
-            if (MEV_NPC_PREWIN && k0 == 0 && use_pre) {
-#pragma unroll
-                for (int t = 0; t < 7; ++t) w[t] = w0[t];
-            } else {
-                load_window(kk, w);
-            }
+            load_window(kk, w);
             const int pidx0 = nl.pidx0[kk];
             Kin kin{nl.x[kk], nl.y[kk], nl.v[kk], nl.h[kk], nl.acc[kk], nl.steer[kk]};
             float cn, sn;
@@ -1190,26 +978,18 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         }
         wave_lds_sync();
     };
-#ifdef MEV_X_NOPLAN
-    if (false) {
-#else
     if (__popcll(alive_k) >= 2) {
-#endif
         plan_all(false, nl.thr_a);
-    } else if (lane < cnt && !solo) {
+    } else if (lane < cnt) {
         nl.thr_a[lane] = nl.accb[lane];  // no other NPC to plan against: the cruise throttle
         wave_lds_sync();
     }
     NT(2);  // round A: plans (pairs)
-    if (!solo) move_all(nl.thr_a, alive_k, true);  // (solo: moved in part 1)
+    move_all(nl.thr_a, alive_k);
     NT(3);  // round A: moves
     unsigned long long done_m = alive_k;  // NPCs whose round-A move is final
     int kseq = cnt;                       // the first NPC left to the sequential turns
-#if defined(MEV_X_NOPLAN) || defined(MEV_X_NOB)
-    if (false) {
-#else
     if (__popcll(alive_k) >= 2) {
-#endif
         plan_all(true, nl.thr_b);
         const bool differs = lane < cnt && ((alive_k >> lane) & 1ull) &&
                              __float_as_uint(nl.thr_a[lane < cnt ? lane : 0]) !=
@@ -1217,7 +997,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         const unsigned long long diff = ballot(differs);
         if (diff) {
             const int ks = __builtin_ctzll(diff);
-            move_all(nl.thr_b, 1ull << ks, false);  // its inputs were the sequential ones
+            move_all(nl.thr_b, 1ull << ks);  // its inputs were the sequential ones
             if (lane == 0) atomicAdd(p.overflow + 1, (unsigned long long)(cnt - ks - 1));  // diagnostics
             done_m = alive_k & ((ks == 63 ? ~0ull : ((2ull << ks) - 1ull)));
             kseq = ks + 1;
@@ -1232,9 +1012,6 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     }
     wave_lds_sync();
     // the sequential turns after a round-B disagreement (lane j = other NPC j)
-#ifdef MEV_X_NOSEQ
-    kseq = cnt;
-#endif
     float2 ga = make_float2(0.0f, 0.0f), gb = ga;
     if (kseq < cnt) fetch_ghost(kseq, ga, gb);
     for (int k = kseq; k < cnt; ++k) {
@@ -1294,7 +1071,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const int a = cnt <= 8 ? (lane >> 3) : pi / cnt, b = cnt <= 8 ? (lane & 7) : pi % cnt;
             const int aa = a < cnt ? a : 0, bb = b < cnt ? b : 0;
             const float cdx = nl.x[aa] - nl.x[bb], cdy = nl.y[aa] - nl.y[bb];
-            const bool close = !MEV_SAT_CIRCLE || !(cdx * cdx + cdy * cdy > 3600.0f);  // circumcircles (cars_pre)
+            const bool close = !(cdx * cdx + cdy * cdy > 3600.0f);  // circumcircles (cars_pre)
             if ((cnt <= 8 ? (a < cnt && b < cnt) : pi < cnt * cnt) && a < b && close &&
                 sat_collide(nl.cx[a], nl.cy[a], nl.c[a], nl.s[a], nl.cx[b], nl.cy[b], nl.c[b], nl.s[b]))
                 atomicOr(&nl.col[a], 1ull << b);
@@ -1323,7 +1100,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     const unsigned long long keep_m = ballot(keep);
     const int newcnt = __builtin_popcountll(keep_m);
     // (most steps erase nothing: the survivors already are the prefix 0 .. cnt - 1)
-    if (!MEV_NPC_KEEPSKIP || keep_m != (cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull))) {
+    if (keep_m != (cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull))) {
         const int dst = __builtin_popcountll(keep_m & ((1ull << lane) - 1ull));
         float kx = 0, ky = 0, kv = 0, kh = 0, ka = 0, ks = 0, kc = 0, ksn = 0;
         int kp = 0, kr = 0, ki = 0;
@@ -1339,7 +1116,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         wave_lds_sync();
     }
     // store back + corners of the survivors (for ego-NPC SAT)
-    if (MEV_NPC_DEFER_WB == 0 || store) npc_writeback(p, e, nl, newcnt, lane);
+    npc_writeback(p, e, nl, newcnt, lane);
     if (lane < newcnt) car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
     wave_lds_sync();
 #ifdef MEV_STAMPS_N
@@ -1424,11 +1201,6 @@ __device__ __forceinline__ void write_obs_head(const SimParams& p, int i, const 
 }
 
 // ------------------------------------------------------------- the step ---
-// the car part's per-agent physics without divergent branches: the kinematics, the
-// reward terms and the corner tests are evaluated by every lane and selected
-#ifndef MEV_BF_PHYS
-#define MEV_BF_PHYS 1
-#endif
 
 // Dynamic LDS of k_cars, carved for the handle's N egos and K NPC slots.
 // s_waitcnt vmcnt(0) (gfx9 encoding: expcnt and lgkmcnt left at their maximum)
@@ -1501,25 +1273,6 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
 }
 
 
-// phase 1's first path windows loaded from group-layout route / index registers
-// right after the state round (1), or after the state went through LDS (0)
-#ifndef MEV_EARLY_WINDOW
-#define MEV_EARLY_WINDOW 1
-#endif
-
-// k_step's output strategy: 0 = each part stores its outputs as it produces
-// them (the car part its rows' heads, the LiDAR part its blocks); 1 = staged in
-// LDS and written once at the end as whole coalesced rows (fused_store)
-#ifndef MEV_FUSED_STAGED
-#define MEV_FUSED_STAGED 0
-#endif
-
-// k_step writes the final ego state back at its end, after the LiDAR (1), or in
-// cars_post before it (0)
-#ifndef MEV_WB_LATE
-#define MEV_WB_LATE 0
-#endif
-
 // the final ego state of the wave's N agent slots back to HBM (lane = slot; agent
 // slot i is global agent e * NE + i); spawn poses, intent, alive and route only
 // for envs reset this step (do_reset: the lane's env)
@@ -1558,16 +1311,11 @@ struct CarsCtx {
 // computes the poses after the kinematics itself and marches the road while this
 // wave runs the car part; this wave leaves the beam offsets (el.rel) to it, records
 // the respawned egos (el.envw[6]) at the end and passes workgroup barrier B.
-// Hook: called right after the kinematics (the poses after Car::update in LDS); k_step's
-// mixed order runs the LiDAR road march there (RoadHook).  Hook::kMarks: record the
-// respawned egos in el.envw[6] as the early split does.
-struct NoHook {
-    static constexpr bool kMarks = false;
-    __device__ __forceinline__ void operator()() const {}
-};
-template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false, class Hook = NoHook>
+// EARLY: phase 1's first path windows come by LDS DMA from group-layout route /
+// index registers loaded in the state round (k_step without traffic).
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
-                                            const CarsLDS& el, NL* nl, const Hook& hook = Hook{}) {
+                                            const CarsLDS& el, NL* nl) {
     static_assert(!ESPLIT || (FUSED && !TRAFFIC), "early split: k_step without traffic");
     static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
@@ -1584,8 +1332,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // (consecutive envs are consecutive in the SoA).  N: the wave's agent slots.
     const int npk = PK == 1 ? 1 : (p.E - e < PK ? p.E - e : PK);
     const int N = PK == 1 ? NE : npk * NE;
-    // STAGE: every output and the state are written at the end of k_step (fused_store)
-    constexpr bool STAGE = FUSED && MEV_FUSED_STAGED;
 
     // ---- phase 0: ego state -> LDS (lane = agent).  An env whose previous
     // step ended starts from its spawns (vector auto-reset; reset +
@@ -1737,17 +1483,15 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
 
     STAMP(0);
     int ncnt = 0;
-    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg, !FUSED);
-#ifndef MEV_TRAFFIC_PRIO  // fused traffic: the rest of the step at a level by the env's NPC count (0: MEV_PRIO_CARS; 3: +1.4 % at config 4)
-#define MEV_TRAFFIC_PRIO 3
-#endif
-    if (TRAFFIC && FUSED && MEV_TRAFFIC_PRIO) {
+    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg);
+    if (TRAFFIC && FUSED) {
         // the envs with many NPCs set the kernel's end: the rest of their step goes first
-        if (ncnt >= 2 * MEV_TRAFFIC_PRIO) __builtin_amdgcn_s_setprio(3);
-        else if (ncnt >= MEV_TRAFFIC_PRIO) __builtin_amdgcn_s_setprio(2);
+        // (3 or more NPCs: level 2, 6 or more: 3; config 4 +1.4 % over a fixed level)
+        if (ncnt >= 6) __builtin_amdgcn_s_setprio(3);
+        else if (ncnt >= 3) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(1);
-    } else if (TRAFFIC && MEV_NPC_PRIO) {
-        __builtin_amdgcn_s_setprio(FUSED ? MEV_PRIO_CARS : 0);
+    } else if (TRAFFIC) {
+        __builtin_amdgcn_s_setprio(0);
     }
     STAMP(1);
 
@@ -1781,7 +1525,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         const bool alive = act && (early ? galive_b : el.alive[ii]) != 0;
         const float a0_i = early ? ga0 : el.a0[ii], a1_i = early ? ga1 : el.a1[ii];
         float cH, sH;
-#if MEV_BF_PHYS
         {
             // every lane runs the update; a dead agent keeps its state (one sincosf)
             Kin ku = k;
@@ -1790,11 +1533,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             car_update_move(ku, cH, sH);
             if (alive) k = ku;
         }
-#else
-        if (alive) car_update(k, a0_i, a1_i, in.dt, &cH, &sH);
-        else sincosf(k.h, &sH, &cH);
-#endif
-        STAMPX(1);
         if (early) {  // round B's window: wait for the LDS DMA, then 4 aligned 16-B reads per lane
             __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
             const float4* wl = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + grp * 128 + sub * 16);
@@ -1847,12 +1585,11 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
                 el.tgy[i] = P[tidx].y;
             }
         }
-        STAMPX(2);
         float rew = 0.0f, cur = 0.0f, an = 0.0f, sn = 0.0f;
         bool succ = false;
         float ccx[4], ccy[4];
         car_corners(k.x, k.y, cH, sH, ccx, ccy);
-        if (MEV_BF_PHYS || alive) {
+        {  // (branch-free: every lane evaluates the terms, a dead agent's are zeroed)
             // compute_progress / compute_stuck / compute_smooth (:15-46)
             cur = hypotf(k.x - pend.x, k.y - pend.y);
             const float prev = el.prev_dist[ii];
@@ -1875,13 +1612,11 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             const bool sx_ = fabs_f(k.y - pend.y) < 15.0f && fabs_f(k.x - pend.x) < 40.0f;
             const bool sy_ = fabs_f(k.x - pend.x) < 15.0f && fabs_f(k.y - pend.y) < 40.0f;
             succ = fabs_f(dxr) > fabs_f(dyr) ? sx_ : sy_;
-            if (MEV_BF_PHYS && !alive) { rew = 0.0f; cur = 0.0f; an = 0.0f; sn = 0.0f; succ = false; }
+            if (!alive) { rew = 0.0f; cur = 0.0f; an = 0.0f; sn = 0.0f; succ = false; }
         }
-        STAMPX(3);
         // corner tests, one per lane: sub 0-3 corner q (screen margin, road, yellow line,
         // line mask), sub 4-7 edge midpoint q (line mask)
         bool oos_q = false, off_q = false, line_q = false;
-#if MEV_BF_PHYS
         {
             // lane sub < 4: corner q (screen margin, road, yellow line, line mask);
             // sub >= 4: the midpoint of edge (q, q + 1) (line mask only)
@@ -1899,30 +1634,9 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             off_q = alive && corner && !is_on_road(qx, qy, p.rw);
             line_q = alive && ((corner && hits_yellow_line(qx, qy, p.rw)) || lm);
         }
-        if (false) {
-#else
-        if (alive) {
-#endif
-            const int q = sub & 3;
-            float qx = ccx[0], qy = ccy[0], rx = ccx[1], ry = ccy[1];
-#pragma unroll
-            for (int u = 1; u < 4; ++u) {
-                if (q == u) { qx = ccx[u]; qy = ccy[u]; rx = ccx[(u + 1) & 3]; ry = ccy[(u + 1) & 3]; }
-            }
-            if (sub < 4) {
-                const float M = 100.0f;
-                oos_q = qx < -M || qx > float(WIDTH) + M || qy < -M || qy > float(HEIGHT) + M;
-                off_q = !is_on_road(qx, qy, p.rw);
-                line_q = hits_yellow_line(qx, qy, p.rw) || is_line_px((int)qx, (int)qy, p.line_stop);
-            } else {
-                const float mx = 0.5f * (qx + rx), my = 0.5f * (qy + ry);
-                line_q = is_line_px((int)mx, (int)my, p.line_stop);
-            }
-        }
         const bool any_oos = (ballot(oos_q) & gmask) != 0ull;
         const bool any_off = (ballot(off_q) & gmask) != 0ull;
         const bool any_line = (ballot(line_q) & gmask) != 0ull;
-        STAMPX(4);
         if (act) {
             if (sub < 4) {
                 reinterpret_cast<float*>(&el.cx[i])[sub] = ccx[sub];
@@ -1942,11 +1656,8 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
                 el.col[i] = 0ull; el.colnpc[i] = 0;
             }
         }
-        STAMPX(5);
     }
     wave_lds_sync();
-    ES_STAMP(1);
-    hook();
 
     STAMP(2);
     // one ego per env and no NPCs: no car can touch another, and no LiDAR beam can
@@ -1954,7 +1665,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // candidate masks below are skipped (the masks stay empty)
     const bool lone = !TRAFFIC && NE == 1;
     // ---- car-car SAT (:292-318): ego pairs (i<j) and ego x NPC, one pair per lane
-#ifndef MEV_EXP_NOSAT  // timing-only: no car-car SAT
     for (int pbase = 0; pbase < (lone ? 0 : N * N); pbase += WAVE) {
         const int pi = pbase + tid;
         // (a, b) = (pi / N, pi % N); lane = 8a + b without the integer division when N <= 8
@@ -1964,7 +1674,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             // (2 x 29.55 px; 60 px with margin for the rounding of the corners) cannot
             // overlap: the SAT runs only for lanes (and waves) with a close pair
             const float cdx = el.x[a] - el.x[b], cdy = el.y[a] - el.y[b];
-            const bool close = !MEV_SAT_CIRCLE || !(cdx * cdx + cdy * cdy > 3600.0f);
+            const bool close = !(cdx * cdx + cdy * cdy > 3600.0f);
             if (a < b && (PK == 1 || a / NE == b / NE) && el.alive[a] && el.alive[b] && close &&
                 sat_collide(reinterpret_cast<const float*>(&el.cx[a]), reinterpret_cast<const float*>(&el.cy[a]),
                             el.c[a], el.s[a], reinterpret_cast<const float*>(&el.cx[b]),
@@ -1972,14 +1682,13 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
                 atomicOr(&el.col[a], 1ull << b);
         }
     }
-#endif
     if constexpr (TRAFFIC) {
         for (int pbase = 0; pbase < N * ncnt; pbase += WAVE) {
             const int pi = pbase + tid;
             if (pi < N * ncnt) {
                 const int a = pi / ncnt, b = pi % ncnt;
                 const float cdx = el.x[a] - nl->x[b], cdy = el.y[a] - nl->y[b];
-                const bool close = !MEV_SAT_CIRCLE || !(cdx * cdx + cdy * cdy > 3600.0f);  // as for the ego pairs
+                const bool close = !(cdx * cdx + cdy * cdy > 3600.0f);  // as for the ego pairs
                 if (el.alive[a] && close && sat_collide(reinterpret_cast<const float*>(&el.cx[a]),
                                                reinterpret_cast<const float*>(&el.cy[a]), el.c[a], el.s[a],
                                                nl->cx[b], nl->cy[b], nl->c[b], nl->s[b]))
@@ -2013,11 +1722,9 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
                 if (TRAFFIC && ((npcm >> a) & 1ull)) { donem |= 1ull << a; crash |= 1ull << a; }
             }
         }
-        STAMPY(1);
         if (in_env && ((crash >> i) & 1ull)) { el.done[i] = 1; el.status[i] = ST_CRASH_CAR; }
     }
     wave_lds_sync();
-    STAMPY(2);
     // respawn crashed egos (Car::respawn, Car.cpp:76-84; :339-351), lane = agent;
     // the final state is written back by cars_post
     for (int i = tid; i < N; i += WAVE) {
@@ -2032,7 +1739,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             el.tgx[i] = el.t10x[i]; el.tgy[i] = el.t10y[i];  // path[min(0 + 10, 159)]
         }
     }
-    if constexpr (ESPLIT || Hook::kMarks) {  // the respawned egos (agent slots), for the LiDAR after barrier B
+    if constexpr (ESPLIT) {  // the respawned egos (agent slots), for the LiDAR after barrier B
         const uint8_t st = el.status[tid < N ? tid : 0];
         const bool rs = tid < N && p.respawn && el.alive[tid < N ? tid : 0] && el.done[tid < N ? tid : 0] &&
                         (st == ST_CRASH_CAR || st == ST_CRASH_WALL || st == ST_CRASH_LINE);
@@ -2040,7 +1747,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         if (tid == 0) el.envw[6] = (int)(unsigned)m;
     }
     wave_lds_sync();
-    STAMPY(3);
 
     STAMP(4);
     // ---- LiDAR obstacle table (:374-388): every ego (alive or not), then NPCs,
@@ -2090,7 +1796,6 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     STAMP(5);
     if constexpr (ESPLIT) {
         __syncthreads();  // barrier B: obstacle table, candidate masks, respawns
-        ES_STAMP(2);
     }
     return CarsCtx{step_no, do_reset, ncnt, false};
 }
@@ -2106,7 +1811,6 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
     const int NE = p.N;  // agents per env (PK > 1: see cars_pre)
     const int npk = PK == 1 ? 1 : (p.E - e < PK ? p.E - e : PK);
     const int N = PK == 1 ? NE : npk * NE;
-    constexpr bool STAGE = FUSED && MEV_FUSED_STAGED;
     const int step_no = cx.step_no, ncnt = cx.ncnt;
     const bool do_reset = cx.do_reset;
     const int grp = tid >> 3, sub = tid & 7;
@@ -2158,47 +1862,23 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
         const bool truncated = p.max_steps > 0 && step_e >= p.max_steps;
         if (PK == 1) cx.ended = terminated || truncated;
         if (in_env) {
-            if (STAGE) el.rew[i] = rew_i;
-            else {
-                const int g = e * NE + i;
-                out.rew[g] = rew_i;
-                out.done[g] = done_i;
-                out.status[g] = st_i;
-            }
+            const int g = e * NE + i;
+            out.rew[g] = rew_i;
+            out.done[g] = done_i;
+            out.status[g] = st_i;
         }
         if (PK > 1 ? tid < npk : tid == 0) {
-            if constexpr (STAGE) {
-                el.envw[0] = terminated;
-                el.envw[1] = truncated;
-                el.envw[2] = alive_cnt;
-                el.envw[3] = step_no;
-                el.envw[4] = (terminated || truncated) ? 1 : 0;
-                el.envw[5] = do_reset;
-            } else {
-                const int ev = e + (PK > 1 ? tid : 0);
-                gmem(p.step_count)[ev] = step_e;
-                out.term[ev] = terminated;
-                out.trunc[ev] = truncated;
-                out.alive_cnt[ev] = alive_cnt;
-                out.step[ev] = step_e;
-                gmem(p.pending_reset)[ev] = (terminated || truncated) ? 1 : 0;
-            }
+            const int ev = e + (PK > 1 ? tid : 0);
+            gmem(p.step_count)[ev] = step_e;
+            out.term[ev] = terminated;
+            out.trunc[ev] = truncated;
+            out.alive_cnt[ev] = alive_cnt;
+            out.step[ev] = step_e;
+            gmem(p.pending_reset)[ev] = (terminated || truncated) ? 1 : 0;
         }
     }
-    // ---- the final ego state back to HBM (lane = agent); k_step's staged variant
-    // writes it at its end (fused_store)
-#ifdef MEV_EXP_NOWB  // timing-only: no state write-back
-    if (false) {
-#else
-    if (!STAGE && !(FUSED && MEV_WB_LATE)) {
-#endif
-        ego_writeback(p, e, NE, N, el, do_reset, tid);
-    }
-    STAMPY(4);
-    if (FUSED && MEV_PRIO_HEAD >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_HEAD < 0 ? 0 : MEV_PRIO_HEAD);
-#ifdef MEV_EXP_NOHEAD  // timing-only: no observation head
-    return;
-#endif
+    // ---- the final ego state back to HBM (lane = agent)
+    ego_writeback(p, e, NE, N, el, do_reset, tid);
     // ---- observation head (:418-520)
     const int C = PK > 1 ? NE : N + (TRAFFIC ? ncnt : 0);  // neighbour candidates per agent (+ itself)
     if (C <= 8) {
@@ -2243,7 +1923,6 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             before(dpp_f(dm, 0x4E), 7 - (sub ^ 2));
             before(dpp_f(dm, 0x1B), 7 - (sub ^ 3));
             const int nb = __builtin_popcountll(ballot(valid) & gmask);
-            STAMPY(5);
             // one straight-line block for every lane: the agent's own features (the
             // lane of its own index: never a candidate), its look-ahead terms, or a
             // neighbour's features -- the atan2f chain runs beside the divisions
@@ -2256,8 +1935,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             const float f2 = (self ? v : ov - v) / PHYSICS_MAX_SPEED;
             const float f3 = (self ? h : wrap_angle(oh - h)) / PI_F;
             if (act) {
-                // k_step stages the head in LDS (written with the LiDAR block by fused_store)
-                float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)(e * NE + i) * out.obs_ld;
+                float* row = out.obs + (size_t)(e * NE + i) * out.obs_ld;
                 if (!alv) {
                     for (int cc = sub; cc < OBS_HEAD; cc += 8) row[cc] = 0.0f;
                 } else {
@@ -2273,21 +1951,19 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
                         o[0] = o[1] = o[2] = o[3] = o[4] = 0.0f;
                     }
                 }
-                if (!STAGE)
-                    for (int cc = OBS_HEAD + p.lidar_slots + sub; cc < out.obs_ld; cc += 8) row[cc] = 0.0f;
+                for (int cc = OBS_HEAD + p.lidar_slots + sub; cc < out.obs_ld; cc += 8) row[cc] = 0.0f;
             }
         }
     } else {
         for (int i = tid; i < N; i += WAVE) {
             const int g = e * NE + i;
-            float* row = STAGE ? el.head + i * OBS_HEAD : out.obs + (size_t)g * out.obs_ld;
+            float* row = out.obs + (size_t)g * out.obs_ld;
             if (!el.alive[i]) {
                 for (int c = 0; c < OBS_HEAD; ++c) row[c] = 0.0f;
-                if (!STAGE)
-                    for (int c = OBS_HEAD + p.lidar_slots; c < out.obs_ld; ++c) row[c] = 0.0f;
+                for (int c = OBS_HEAD + p.lidar_slots; c < out.obs_ld; ++c) row[c] = 0.0f;
                 continue;
             }
-            write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row, !STAGE && out.obs_ld == p.D);
+            write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row, out.obs_ld == p.D);
         }
     }
     STAMP(6);
@@ -2336,22 +2012,11 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 // replaces the divergent branch -- exec-mask bookkeeping and a pipeline break --
 // the compiler would otherwise wrap around a short computation.  No instruction
 // is emitted for it.
-#ifndef MEV_LIDAR_STRAIGHT
-#define MEV_LIDAR_STRAIGHT 1
-#endif
 template <class T>
 __device__ __forceinline__ T lidar_keep(T v) {
-    if (MEV_LIDAR_STRAIGHT) asm volatile("" : "+v"(v));
+    asm volatile("" : "+v"(v));
     return v;
 }
-// the probe's integer road test / packed position (exact; measured 0.5-1.4 % slower
-// together at configs 2-3: off, the float forms)
-#ifndef MEV_PROBE_INT
-#define MEV_PROBE_INT 0
-#endif
-#ifndef MEV_PROBE_PK
-#define MEV_PROBE_PK 0
-#endif
 // beam steps over a provably safe stretch (0 when it is shorter than one step)
 __device__ __forceinline__ int safe_steps(float safe, float stp, float inv_stp) {
     const int j = lidar_keep((int)(safe * inv_stp));
@@ -2438,35 +2103,18 @@ __device__ inline void slab_clip(float c0, float dc, float idc, float a, float b
 // The road march's queue of unfinished beams, ushort[G*R], is only live
 // before the car phase and shares the segment area.
 
-// Probes tested per step of the road march (phase 1 and each pooled iteration).
-#ifndef MEV_LIDAR_NPR
-#define MEV_LIDAR_NPR 2
-#endif
-constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
+// Probes tested per step of the road march (phase 1's first probes after a beam's
+// safe stretch from the car centre, and each pooled iteration).
+constexpr int LIDAR_NPR = 2;
 // The march's tail (the queue empty, the few longest beams still running, lanes
-// mostly idle).  k_step without traffic: once at most MEV_MARCH_HELP beams run, each
-// gets a group of 2-8 lanes that test MEV_NPT_HELP consecutive probes each per step
-// (config 3 39.4 -> 35.6 us, config 2 19.4 -> 15.6 us).  Measured around it: a plain
-// tail with more probes per lane and step (MEV_LIDAR_NPR_TAIL 6: 38.0 / 18.1 us),
-// groups from 8 or 32 beams, 2 or 4 probes per helper lane.  With traffic and in
-// k_lidar the plain march (config 4: the 6-probe tail measured 1.6 % slower).
-#ifndef MEV_LIDAR_NPR_TAIL
-#define MEV_LIDAR_NPR_TAIL MEV_LIDAR_NPR
-#endif
-#ifndef MEV_MARCH_HELP
-#define MEV_MARCH_HELP 16
-#endif
-#ifndef MEV_NPT_HELP
-#define MEV_NPT_HELP 3
-#endif
-static_assert(MEV_MARCH_HELP <= 32, "helper groups have at least 2 lanes");
-#ifndef MEV_HELP_TRAFFIC  // the helper groups in the traffic kernel too (config 4 +0.6 %)
-#define MEV_HELP_TRAFFIC 1
-#endif
-// probes phase 1 tests after a beam's safe stretch from the car centre
-#ifndef MEV_LIDAR_NPR1
-#define MEV_LIDAR_NPR1 MEV_LIDAR_NPR
-#endif
+// mostly idle): once at most kMarchHelp beams run, each gets a group of 2-8 lanes
+// that test kNptHelp consecutive probes each per step (config 3 39.4 -> 35.6 us,
+// config 2 19.4 -> 15.6 us; in the traffic kernel +0.6 %).  Measured around it: a
+// plain tail with 6 probes per lane and step (38.0 / 18.1 us), groups from 8 or 32
+// beams, 2 or 4 probes per helper lane.  k_lidar marches plainly.
+constexpr int kMarchHelp = 16;
+constexpr int kNptHelp = 3;
+static_assert(kMarchHelp <= 32, "helper groups have at least 2 lanes");
 
 struct LidarLayout {
     int ag, dir, res, seg_jo, seg_rg, seg_bx, queue, scr, bytes;
@@ -2509,7 +2157,6 @@ int lidar_group(int R) {
 // HBM as k_cars published it (k_lidar), or the LDS of the same wave's
 // cars_body (k_step).
 struct LidarSrcHbm {
-    static constexpr bool kStaged = false;  // writes the LiDAR block (and dead rows) itself
     static constexpr bool kBoxLds = false;  // boxes come from HBM: cache one per segment in LDS
     const SimParams& p;
     __device__ float rel(int b) const { return gmem(p.rel_angles)[b]; }
@@ -2522,7 +2169,6 @@ struct LidarSrcHbm {
     __device__ int4 box(int g, int o) const { return p.ob_box[(size_t)(g / p.N) * p.ob_stride + o]; }
 };
 struct LidarSrcLds {
-    static constexpr bool kStaged = MEV_FUSED_STAGED;  // leave the results in LDS for fused_store
     static constexpr bool kBoxLds = true;  // the obstacle table is in this wave's LDS
     const CarsLDS& el;
     int g0;  // global index of the env's agent 0
@@ -2579,7 +2225,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const int g = a0 + lane;
         ag[lane_rank(am)] = src.pose(g);
     }
-    if (PART != 2 && !Src::kStaged && __popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
+    if (PART != 2 && __popcll(am) != na) {  // dead agents: LiDAR block of the observation is zero (:425-427)
         for (int j = 0; j < na; ++j) {
             if ((am >> j) & 1ull) continue;
             if (out.lidar_u8) {  // compact gather format: the dead-agent code
@@ -2599,7 +2245,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     const float crf = CORNER_RADIUS, ccen = rwf + crf;
     const float cr2p1 = crf * crf + 1.0f;
     const float rwm = rwf - 1.5f;
-    const int irw_i = p.irw, icen = p.irw + 84;
     // the reference's stop test of march probe k at (cx_, cy_) + d_k (dx_, dy_):
     // returns the beam's result (k << 1 | hit; S << 1 past the last probe) or -1
     // to go on, and the probe's real point
@@ -2607,16 +2252,8 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const bool past = k_ >= S;
         const int kc = past ? S - 1 : k_;
         const float d = TAB ? gmem(p.dist_tab)[kc] : (float)kc * stp;
-#if MEV_PROBE_PK
-        // the probe point as one packed multiply and add (v_pk_mul_f32, v_pk_add_f32:
-        // the same IEEE roundings as the scalar pair)
-        const f2v fp = f2v{cx_, cy_} + f2v{dx_, dy_} * d;
-        fx = fp.x;
-        fy = fp.y;
-#else
         fx = cx_ + dx_ * d;
         fy = cy_ + dy_ * d;
-#endif
         const int px = (int)fx, py = (int)fy;
         // exact reference predicates at the truncated pixel: screen, then
         // (k > 0) road == RoadGeometry::is_on_road at integer pixels:
@@ -2624,21 +2261,10 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         //               and (in a strip: min(ax, ay) <= rw  or  corner square: max <= rw + cr)
         const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
         const bool off_screen = pmax >= (unsigned)WIDTH;
-#if MEV_PROBE_INT
-        // in integers (every term is an integer below 2^12 on screen; off screen the
-        // road test is not used): off road <=> in the grass disc, or outside both the
-        // strips and the corner square
-        const int iax = abs(px - 375), iay = abs(py - 375);
-        const int qdx = iax - icen, qdy = iay - icen;
-        const int qd2 = __mul24(qdx, qdx) + __mul24(qdy, qdy);
-        const bool offroad = (min(iax, iay) > irw_i && max(iax, iay) > icen) || qd2 <= 84 * 84;
-        const bool stop = off_screen | ((k_ > 0) & offroad);
-#else
         const float iax = fabs_f((float)(px - 375)), iay = fabs_f((float)(py - 375));
         const float qdx = iax - ccen, qdy = iay - ccen;
         const float onv = fmaxf(fminf(fminf(iax, iay) - rwf, fmaxf(iax, iay) - ccen), cr2p1 - (qdx * qdx + qdy * qdy));
         const bool stop = off_screen | ((k_ > 0) & (onv > 0.0f));
-#endif
         const int code = lidar_keep(stop ? ((k_ << 1) | (off_screen ? 0 : 1)) : -1);
         return past ? (S << 1) : code;
     };
@@ -2677,9 +2303,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         else sincosf(a.z + rel_b, &sn, &cs);
         const float dx = cs, dy = -sn;
         d = make_float2(dx, dy);
-#ifdef MEV_EXP_NOROAD
-        return S << 1;
-#else
         const int px = (int)a.x, py = (int)a.y;
         const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
         const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
@@ -2687,9 +2310,8 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         // probes 1 .. j lie within j*step <= safe of the centre (car centre on screen)
         const int k1 = pmax < (unsigned)WIDTH ? 1 + safe_steps(safe, stp, inv_stp) : 0;
         float fx, fy;
-        const int r = probes_n(std::integral_constant<int, MEV_LIDAR_NPR1>{}, a.x, a.y, dx, dy, k1, fx, fy);
-        return r >= 0 ? r : -(k1 + MEV_LIDAR_NPR1) - 1;
-#endif
+        const int r = probes_n(std::integral_constant<int, LIDAR_NPR>{}, a.x, a.y, dx, dy, k1, fx, fy);
+        return r >= 0 ? r : -(k1 + LIDAR_NPR) - 1;
     };
     // one pass of the early split's re-march: compacted agent j (PART 2)
     auto pass1_one = [&](auto small, const int j) {
@@ -2718,8 +2340,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             for (unsigned long long tm = redo; tm; tm &= tm - 1ull) pass1_one(small, __builtin_ctzll(tm));
         } else {
         for (int j = 0; j < nal; j += ILP) {
-            if (PART == 0 && (Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P1B >= 0 && 4 * j >= MEV_PRIO_P1B_AT * nal)
-                __builtin_amdgcn_s_setprio(MEV_PRIO_P1B < 0 ? 0 : MEV_PRIO_P1B);
+            if (PART == 0 && 4 * j >= nal) __builtin_amdgcn_s_setprio(kPrioP1B);
             float4 a[ILP];
 #pragma unroll
             for (int u = 0; u < ILP; ++u) a[u] = ag[j + u < nal ? j + u : j];
@@ -2760,7 +2381,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 4] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    if (PART == 0 && (Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P2 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P2 < 0 ? 0 : MEV_PRIO_P2);
+    if (PART == 0) __builtin_amdgcn_s_setprio(kPrioP2);
     // ---- phase 2: pooled road + screen march of the queued beams
     // (Lidar.cpp:31-48, first stop wins): LIDAR_NPR exact probes, then a jump
     // over the provably safe stretch after the last one
@@ -2785,20 +2406,13 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     };
     if (slot >= 0) load_beam(slot);
     int* hscr = reinterpret_cast<int*>(base + lay.scr);  // phase 3's scratch, free until then
-#ifdef MEV_ITERS
-    int iters = 0, drained = -1, lanes_busy = 0;
-#endif
     bool help = false;
     while (ballot(slot >= 0) != 0ull) {
         // the tail down to <= 16 beams: continue with 4 lanes per beam (below)
-        if (HELP && MEV_MARCH_HELP && next >= qn && __popcll(ballot(slot >= 0)) <= MEV_MARCH_HELP) {
+        if (HELP && next >= qn && __popcll(ballot(slot >= 0)) <= kMarchHelp) {
             help = true;
             break;
         }
-#ifdef MEV_ITERS
-        lanes_busy += __popcll(ballot(slot >= 0));
-        if (drained < 0 && next >= qn) drained = iters;
-#endif
         // branch-free body: every lane evaluates its probes; idle lanes only skip the store
         const bool act = slot >= 0;
         float fx, fy;
@@ -2815,9 +2429,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const bool fin = act & ((r >= 0) | (kn >= S));
         if (fin) res[slot] = r >= 0 ? r : (S << 1);
         k = kn;
-#ifdef MEV_ITERS
-        ++iters;
-#endif
         const unsigned long long fm = ballot(fin);
         if (fm != 0ull) {
             if (fin) {
@@ -2828,13 +2439,13 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             next += __popcll(fm);
         }
     }
-    if (HELP && MEV_MARCH_HELP && help) {
-        // The last running beams (<= MEV_MARCH_HELP), GS lanes each (GS = 64 / the
+    if (HELP && help) {
+        // The last running beams (<= kMarchHelp), GS lanes each (GS = 64 / the
         // beams rounded up to a power of two, 2..8): lane j of a beam's group tests
         // probes k + j*NPH .. k + (j+1)*NPH - 1, the earliest stop of the group wins
         // (results are ordered by k: DPP min), and the group jumps from its last lane's
         // last probe (DPP broadcast) -- the same probes and jumps, in march order.
-        constexpr int NPH = MEV_NPT_HELP > 0 ? MEV_NPT_HELP : NPT;
+        constexpr int NPH = kNptHelp;
         const unsigned long long am = ballot(slot >= 0);
         const int nb = __popcll(am);
         if (slot >= 0) {
@@ -2851,10 +2462,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             if (slot >= 0) load_beam(slot);
             k = k_h;
             while (ballot(slot >= 0) != 0ull) {
-#ifdef MEV_ITERS
-                lanes_busy += __popcll(ballot(slot >= 0));
-                ++iters;
-#endif
                 float fx, fy;
                 const int k0 = k + j * NPH;
                 int r = probes_n(std::integral_constant<int, NPH>{}, cx, cy, dx, dy, k0, fx, fy);
@@ -2884,14 +2491,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         else if (nb <= 16) group_march(std::integral_constant<int, 4>{});
         else group_march(std::integral_constant<int, 2>{});
     }
-#ifdef MEV_ITERS  // per pool: iterations, queued beams, iteration at which the queue ran dry, busy lane-iterations
-    if (lane == 0 && a0 / G < p.E) {
-        p.debug[(a0 / G) * 8 + 0] = (unsigned long long)iters;
-        p.debug[(a0 / G) * 8 + 1] = (unsigned long long)qn;
-        p.debug[(a0 / G) * 8 + 2] = (unsigned long long)(drained < 0 ? iters : drained);
-        p.debug[(a0 / G) * 8 + 3] = (unsigned long long)lanes_busy;
-    }
-#endif
     wave_lds_sync();
     if constexpr (PART == 1) return;  // the early split's road march: phase 3 after the car part
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 3  // timing-only: stop after phase 2
@@ -2901,7 +2500,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (lane == 0 && na == p.N) p.debug[se_ * 8 + 6] = __builtin_amdgcn_s_memrealtime();
 #endif
 
-    if ((Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P3 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P3 < 0 ? 0 : MEV_PRIO_P3);
+    __builtin_amdgcn_s_setprio(kPrioP3);
     // ---- phase 3: cars (Lidar.cpp:50-80) as a list of (agent, box, beam) pairs.
     // A box can only stop the beams whose ray enters its slab box, i.e. the
     // beams inside the angular span of its real slab box seen from the agent:
@@ -2918,9 +2517,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // 3a: lane j < nal fetches agent j's candidate masks once; the loop then
     // reads them with readlane instead of two dependent LDS round trips per agent
     unsigned long long cl0 = 0ull, cl1 = 0ull;
-#ifndef MEV_EXP_NOCARS
     if (lane < nal) src.cand(__float_as_int(ag[lane].w), cl0, cl1);
-#endif
     for (int j = 0; j < nal; ++j) {
         const unsigned long long c0 = readlane64(cl0, j), c1 = readlane64(cl1, j);
         const int n0 = __popcll(c0);
@@ -2961,11 +2558,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             w -= 6.28318531f * floorf(w * 0.159154943f);  // [0, 2*pi)
             // beams b with rel0 + b*dphi in the span, widened by 2e-4 rad (20x the
             // error of atan2_fast and of the linear model of the host's angles)
-#ifdef MEV_EXP_BADRANGE
-            const float marg = -0.02f;  // test-of-the-test: spans too narrow, hits must be dropped
-#else
             const float marg = 2.0e-4f;
-#endif
             const float ulo = (w - marg) * idphi, uhi = (w + (dmax - dmin) + marg) * idphi;
             int lo[3], cn[3];
 #pragma unroll
@@ -2982,9 +2575,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         seg_rg[m] = rg;
     }
     wave_lds_sync();
-#ifdef MEV_ITERS
-    int p3_pairs = 0, p3_chunks = 0, p3_kk = 0;
-#endif
     // 3c: the pairs of all the group's agents packed into the 64 lanes
     for (int cb = 0; cb < M; cb += WAVE) {
         const int nseg = M - cb < WAVE ? M - cb : WAVE;
@@ -2993,13 +2583,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const int excl = incl - cnt;
         const int T = __builtin_amdgcn_readlane(incl, WAVE - 1);
         int carry = 0;  // (start << 8 | segment) of the segment running into this chunk
-#ifdef MEV_ITERS
-        p3_pairs += T;
-#endif
         for (int q0 = 0; q0 < T; q0 += WAVE) {
-#ifdef MEV_ITERS
-            ++p3_chunks;
-#endif
             const int q = q0 + lane;
             // segment of pair q: the last m with excl[m] <= q.  Each segment that
             // starts in this chunk writes (start << 8 | m) + 1 to the LDS slot of
@@ -3048,20 +2632,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 kb = kb < kr - 1 ? kb : kr - 1;
                 if (lo > hi) kb = 0;
                 // ... resolved by exact probes in march order
-#ifdef MEV_ITERS
-                {
-                    int tk = 0;
-                    for (int kk = ka; kk <= kb; ++kk) {
-                        ++tk;
-                        const float d = (float)kk * p.lidar_step;
-                        const int px = (int)(a.x + dd.x * d), py = (int)(a.y + dd.y * d);
-                        if (px >= bx.x && px <= bx.y && py >= bx.z && py <= bx.w) break;
-                    }
-                    int mx = tk;
-                    for (int o = 32; o >= 1; o >>= 1) { const int t2 = __shfl_xor(mx, o); mx = mx > t2 ? mx : t2; }
-                    p3_kk += mx;
-                }
-#endif
                 for (int kk = ka; kk <= kb; ++kk) {
                     // a runtime table test here, not march_dist<TAB>: measured 4 us per
                     // step faster in k_step, and without it k_lidar's 64-VGPR
@@ -3077,22 +2647,12 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         }
     }
     wave_lds_sync();
-#ifdef MEV_ITERS  // per pool: segments, pairs, 64-pair chunks, probe-loop trips (wave max per chunk)
-    if (lane == 0 && a0 / G < p.E) {
-        p.debug[(a0 / G) * 8 + 4] = (unsigned long long)M;
-        p.debug[(a0 / G) * 8 + 5] = (unsigned long long)p3_pairs;
-        p.debug[(a0 / G) * 8 + 6] = (unsigned long long)p3_chunks;
-        p.debug[(a0 / G) * 8 + 7] = (unsigned long long)p3_kk;
-    }
-#endif
 #if defined(MEV_STAMPS_R)
     if (lane == 0) p.debug[se_ * 8 + 5 + sp_] = __builtin_amdgcn_s_memrealtime();
 #endif
 #if defined(MEV_EXP_STOP) && MEV_EXP_STOP == 4  // timing-only: stop after phase 3 (no LiDAR block writes)
     if (Src::kBoxLds) return;
 #endif
-    if (Src::kStaged) return;  // k_step: fused_store writes the block from res
-    if ((Src::kBoxLds || MEV_PRIO_HBM) && MEV_PRIO_P4 >= 0) __builtin_amdgcn_s_setprio(MEV_PRIO_P4 < 0 ? 0 : MEV_PRIO_P4);
     // 3d: Lidar::normalized (:92-98), the LiDAR block of each alive agent's row
     auto lidar_value = [&](int r) {
         return ((r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max) * p.lidar_inv;
@@ -3144,72 +2704,15 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
     const int a0 = __builtin_amdgcn_readfirstlane(a_begin + (blk * (int)(blockDim.x / WAVE) + wv) * G);
     if (a0 >= a_end) return;  // wave-uniform exit: the kernel has no block-level barrier
     const int na = a_end - a0 < G ? a_end - a0 : G;
-    if (MEV_PRIO_HBM) __builtin_amdgcn_s_setprio(MEV_PRIO_LIDAR);
+    __builtin_amdgcn_s_setprio(kPrioLidar);
     const LidarLayout lay = lidar_layout(G, p.R, lidar_cand_max(p));
     lidar_body<TAB, 1>(p, out, LidarSrcHbm{p}, G, a0, na, lane, lds_raw + (size_t)wv * (size_t)lay.bytes, lay);
 }
 
-// End of k_step: every output of the env and its state, written once from LDS.
-// The env's observation rows [N][D] are one contiguous block of HBM, written
-// with 16-byte stores: head (staged by cars_body), LiDAR (Lidar::normalized,
-// :92-98, from the beam results res) and zero padding; a dead agent's row is zero.
-template <bool TAB>
-__device__ __forceinline__ void fused_store(const SimParams& p, const Outputs& out, const int e, const CarsLDS& el,
-                                            const int* res, const int lane) {
-    const int N = p.N, D = p.D, R = p.R, slots = p.lidar_slots;
-    const unsigned long long am = ballot(lane < N && el.alive[lane < N ? lane : 0] != 0);
-    const int total = N * D;
-    const float invD = 1.0f / (float)D;
-    // branch-free: both LDS reads are issued with clamped indices, then selected
-    auto value = [&](int idx) -> float {
-        int i = (int)((float)idx * invD);  // idx / D, corrected for the reciprocal's rounding
-        i -= i * D > idx ? 1 : 0;
-        i += (i + 1) * D <= idx ? 1 : 0;
-        const int c = idx - i * D;
-        const int b = c - OBS_HEAD;
-        const int j = __popcll(am & ((1ull << i) - 1ull));  // compacted LiDAR slot of agent i
-        const float hv = el.head[i * OBS_HEAD + (c < OBS_HEAD ? c : 0)];
-        const int r = res[j * R + (b >= 0 && b < slots ? b : 0)];
-        const float lv = ((r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max) * p.lidar_inv;
-        const float v = c < OBS_HEAD ? hv : (b < slots ? lv : 0.0f);
-        return ((am >> i) & 1ull) ? v : 0.0f;
-    };
-    float* blk = out.obs + (size_t)e * (size_t)total;
-    if ((total & 3) == 0) {
-        float4* b4 = reinterpret_cast<float4*>(blk);
-        for (int q = lane; q < total / 4; q += WAVE)
-            b4[q] = make_float4(value(4 * q), value(4 * q + 1), value(4 * q + 2), value(4 * q + 3));
-    } else {
-        for (int idx = lane; idx < total; idx += WAVE) blk[idx] = value(idx);
-    }
-    const bool do_reset = el.envw[5] != 0;
-    for (int i = lane; i < N; i += WAVE) {
-        const int g = e * N + i;
-        out.rew[g] = el.rew[i];
-        out.done[g] = el.done[i];
-        out.status[g] = el.status[i];
-        egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
-        egof(p, EF_ACC)[g] = el.acc[i]; egof(p, EF_STEER)[g] = el.steer[i]; egoi(p, EF_PIDX)[g] = el.pidx[i];
-        egof(p, EF_PREV_DIST)[g] = el.prev_dist[i]; egof(p, EF_PA0)[g] = el.pa0[i]; egof(p, EF_PA1)[g] = el.pa1[i];
-        if (do_reset) {
-            egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
-            egoi(p, EF_INTENT)[g] = el.intent[i]; gmem(p.ego.alive)[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
-        }
-    }
-    if (lane == 0) {
-        out.term[e] = el.envw[0];
-        out.trunc[e] = el.envw[1];
-        out.alive_cnt[e] = el.envw[2];
-        out.step[e] = el.envw[3];
-        gmem(p.step_count)[e] = el.envw[3];
-        gmem(p.pending_reset)[e] = el.envw[4];
-    }
-}
 
 // Agents per LiDAR pool in k_step: the env's N agents in pools of at most 512
-// beams (all N in one pool at config 3; the staged variant needs one pool).
+// beams (all N in one pool at config 3).
 __host__ __device__ inline int step_pool(const SimParams& p) {
-    if (MEV_FUSED_STAGED) return p.N;
     const int g = 512 / (p.R > 0 ? p.R : 1);
     return g < 1 ? 1 : (g < p.N ? g : p.N);
 }
@@ -3222,7 +2725,7 @@ struct StepLayout {
 __host__ __device__ inline StepLayout step_layout(const SimParams& p) {
     StepLayout L;
     int off = (int)lds_al(cars_lds_bytes(p.N, cars_k(p)));
-    L.head = off; off += MEV_FUSED_STAGED ? (int)lds_al((size_t)p.N * OBS_HEAD * 4) : 0;
+    L.head = off;  // (no staged heads: the car part writes its rows' heads itself)
     L.rel = off; off += (int)lds_al((size_t)p.R * 4);
     L.envw = off; off += 32;
     L.lidar = off; off += lidar_layout(step_pool(p), p.R, lidar_cand_max(p), false).bytes;
@@ -3262,20 +2765,20 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
     // R <= 128 puts every pool (step_pool agents) within the layout's beams
     const bool npcs = KM == 0 ? !p.traffic : (p.traffic && p.K <= KM);
     const size_t npc_lds = KM == 0 ? 0 : sizeof(NpcLDST<(KM ? KM : 1)>);
-    return p.N <= NM && p.R <= kFixedRays && npcs && !MEV_FUSED_STAGED &&
+    return p.N <= NM && p.R <= kFixedRays && npcs &&
            (size_t)FixedLayout<NM, KM>::bytes + npc_lds <= 10 * 1024;
 }
 
-// agents per phase-1 pass in k_step (independent dependency chains interleaved)
-#ifndef MEV_PHASE1_ILP
-#define MEV_PHASE1_ILP 2
-#endif
-
+// agents per phase-1 pass in k_step (independent dependency chains interleaved;
+// 3 or 4 raise register pressure and lose); 1 in the early split's LiDAR wave
+// (8 waves per SIMD)
+constexpr int kPhase1Ilp = 2;
+constexpr int kEsplitIlp = 1;
 
 // The whole step in one wave per env: cars_body, then the LiDAR of the env's
-// N agents as one pool, from the same wave's LDS, then every output written
-// once (fused_store).  No HBM hand-off, no second launch, and no global store
-// before the last phase (a later load's vmcnt wait would drain them); a wave
+// N agents in pools, from the same wave's LDS.  No HBM hand-off, no second
+// launch, and no global store before a later global load (its vmcnt wait would
+// drain them); a wave
 // whose env finishes its car logic early starts its LiDAR while other waves
 // on the SIMD are still in theirs.  The car part runs at a higher issue
 // priority: it is the latency-bound critical path of each wave.
@@ -3293,9 +2796,8 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 //
 // The NPC-aware deal of the next step (traffic, §3.1c): this env joins its list's
 // class for step t + 1 (an env that ended restarts without NPCs after its
-// auto-reset).  At the end of k_step (MEV_DEAL_LATE): waiting for the atomic's
-// returned value is a vmcnt wait, which on gfx950 also waits for every store
-// issued before it (the car part's outputs and state write-back).
+// auto-reset).  It runs where the car part ends (measured against the end of
+// k_step: no difference, r3_ab_deferwb.txt).
 template <bool TRAFFIC>
 __device__ __forceinline__ void deal_append(const SimParams& p, const StepInputs& in, const CarsCtx& cx, const int e) {
     if constexpr (TRAFFIC) {
@@ -3306,7 +2808,10 @@ __device__ __forceinline__ void deal_append(const SimParams& p, const StepInputs
         if (lane0 == 0) {
             const int c = (in.auto_reset && cx.ended) ? 0 : (cx.ncnt < kDealClasses - 1 ? cx.ncnt : kDealClasses - 1);
             const int slot = atomicAdd(p.deal_cnt + (size_t)nxt * kDealRingInts + (x * kDealClasses + c) * kDealPad, 1);
-            gmem(p.deal_order)[((size_t)x * kDealClasses + c) * p.E + slot] = e;
+            // (ring nxt of the orders too: workgroups of this step that start later still
+            // read ring deal_ring, so the orders are never overwritten while in use)
+            const size_t ring_off = (size_t)nxt * kDealLists * kDealClasses * (size_t)p.E;
+            gmem(p.deal_order)[ring_off + ((size_t)x * kDealClasses + c) * p.E + slot] = e;
         }
         if (blockIdx.x == 0 && lane0 < kDealLists * kDealClasses) {  // clear ring t + 2
             const int clr = nxt == 2 ? 0 : nxt + 1;
@@ -3315,48 +2820,6 @@ __device__ __forceinline__ void deal_append(const SimParams& p, const StepInputs
     }
 }
 
-// Mixed order (k_step with one wave per env, MEV_MIX): the four waves of a SIMD start
-// together and would all run their latency-bound car parts at once, then all their
-// VALU-bound LiDAR phases.  Every second residency slot (blockIdx >> 10 odd: the
-// dispatcher deals the first 1024 workgroups one per SIMD) runs the road march
-// (LiDAR phases 1-2) right after the kinematics instead, inside cars_pre (RoadHook),
-// then the rest of the car part, the respawned egos' re-march and the car pairs --
-// so each SIMD mixes two waves' car parts with two waves' LiDAR work.
-#ifndef MEV_MIX
-#define MEV_MIX 0
-#endif
-#ifndef MEV_MIX_SHIFT
-#define MEV_MIX_SHIFT 10
-#endif
-#ifndef MEV_PRIO_MIX_ROAD
-#define MEV_PRIO_MIX_ROAD 1
-#endif
-template <bool TAB, int ILP>
-struct RoadHook {
-    static constexpr bool kMarks = true;
-    const SimParams& p;
-    Outputs out;  // (by value: a reference to the kernel's local structs kept them in scratch memory)
-    CarsLDS el;
-    unsigned char* lbase;
-    LidarLayout lay;
-    int g0;
-    bool on;
-    __device__ __forceinline__ void operator()() const {
-        if (!on) return;
-        const int lane = threadIdx.x & (WAVE - 1);
-        const int N = p.N;
-        const bool alv = lane < N && el.alive[lane < N ? lane : 0] != 0;
-        const unsigned long long am = ballot(alv);
-        float4* ag = reinterpret_cast<float4*>(lbase + lay.ag);
-        if (alv) ag[lane_rank(am)] = make_float4(el.x[lane], el.y[lane], el.h[lane], __int_as_float(g0 + lane));
-        wave_lds_sync();
-        __builtin_amdgcn_s_setprio(MEV_PRIO_MIX_ROAD);
-        lidar_body<TAB, ILP, LidarSrcLds, MEV_LIDAR_NPR_TAIL, true, 1>(p, out, LidarSrcLds{el, g0}, N, g0, N, lane, lbase,
-                                                                       lay, 0ull, am);
-        __builtin_amdgcn_s_setprio(MEV_PRIO_CARS);
-    }
-};
-
 // ESPLIT (early split, large batches, one env per two-wave workgroup, 8 waves per
 // SIMD at <= 64 VGPRs): the LiDAR wave computes the agents' poses after Car::update
 // itself and marches the road (LiDAR phases 1-2) while the car wave runs the car
@@ -3364,29 +2827,17 @@ struct RoadHook {
 // the respawned egos' beams and resolves the cars (phase 3) while the car wave runs
 // cars_post.  The car waves' latency-bound chains and the LiDAR waves'
 // VALU-bound phases then share each SIMD instead of following each other.
-#ifndef MEV_SPLIT_WPE
-#define MEV_SPLIT_WPE 4
-#endif
-#ifndef MEV_ESPLIT_WPE
-#define MEV_ESPLIT_WPE 8
-#endif
-#ifndef MEV_PRIO_ESPLIT_ROAD  // the early split's LiDAR wave: kinematics and road march (its critical path)
-#define MEV_PRIO_ESPLIT_ROAD 3
-#endif
-#ifndef MEV_PRIO_ESPLIT_CARS  // the early split's car wave (slack until barrier B)
-#define MEV_PRIO_ESPLIT_CARS 2
-#endif
-#ifndef MEV_PRIO_ESPLIT_CARPHASE  // the LiDAR wave after barrier B (re-march, car pairs, block writes)
-#define MEV_PRIO_ESPLIT_CARPHASE 1
-#endif
-#ifndef MEV_ESPLIT_ILP
-#define MEV_ESPLIT_ILP 1
-#endif
-#ifndef MEV_KSTEP_ATTR  // experiments: extra kernel attributes of k_step (e.g. a waves-per-EU cap)
-#define MEV_KSTEP_ATTR
-#endif
+// Issue levels: the LiDAR wave's kinematics and road march 3 (its critical path),
+// the car wave 2 (slack until barrier B), the LiDAR wave after B (re-march, car
+// pairs, block writes) 1.  Waves per SIMD: 4 (split), 8 (early split, one env per
+// workgroup).
+constexpr int kSplitWpe = 4;
+constexpr int kEsplitWpe = 8;
+constexpr int kPrioEsplitRoad = 3;
+constexpr int kPrioEsplitCars = 2;
+constexpr int kPrioEsplitCarPhase = 1;
 template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
-__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_ESPLIT_WPE : (SPLIT ? MEV_SPLIT_WPE : 4)) MEV_KSTEP_ATTR void k_step(
+__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? kEsplitWpe : (SPLIT ? kSplitWpe : 4)) void k_step(
     const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
 #include "mev_step_body.inc"
 }
@@ -3407,7 +2858,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? MEV_
 // command twice.  Every wave reaches the exit: the poll loop is bounded by the
 // clock, a step by its own work.
 template <bool TRAFFIC, bool TAB, int NM, int KM, bool SPLIT>
-__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? MEV_SPLIT_WPE : 4) void k_serve(
+__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? kSplitWpe : 4) void k_serve(
     const SimParams* __restrict__ pp, ServeArgs sa, Outputs out) {
     __shared__ uint32_t cmdw[kServeLine];
     constexpr int PK = 1;
@@ -3576,7 +3027,6 @@ static size_t fused_lds_bytes(const SimParams& p) {
 // choice when it also fits a wave's share at 4 waves per SIMD (128 VGPRs): a CU
 // holds 16 waves, so a wave may take 160 KB / 16 = 10 KB.
 static bool fused_fits(const SimParams& p) {
-    if (MEV_FUSED_STAGED && (p.traffic || p.N * p.R > 512)) return false;
     return fused_lds_bytes(p) <= 64 * 1024;
 }
 
@@ -3612,9 +3062,7 @@ int step_pack(const SimParams& p) {
 
 // two waves per fused workgroup (k_step SPLIT) when that keeps <= 4 waves per SIMD
 // (<= 2048 workgroups; 256 CUs x 4 SIMDs)
-#ifndef MEV_SPLIT_MAX_WG
-#define MEV_SPLIT_MAX_WG 2048
-#endif
+constexpr int kSplitMaxWg = 2048;
 // Envs per workgroup of the early split (k_step ESPLIT; 0: it does not apply).  An
 // explicit mev_set_step_pack is kept (reduced to <= 8 agent slots) when the slots'
 // beams fit one 512-beam LiDAR pool.  Automatic: 4 envs while their beams stay
@@ -3647,7 +3095,7 @@ bool step_split(const SimParams& p) {
     if (p.traffic || !fixed_fits<8, 0>(p) || p.step_split == 1 || step_esplit(p)) return false;
     if (p.step_split == 2) return true;
     const int pk = step_pack(p);
-    return (p.E + pk - 1) / pk <= MEV_SPLIT_MAX_WG;
+    return (p.E + pk - 1) / pk <= kSplitMaxWg;
 }
 
 template <bool TAB>
@@ -3666,7 +3114,6 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         const unsigned lds = (unsigned)FixedLayout<8>::bytes;
         const int pk = step_pack(p);
         const int wg = (p.E + pk - 1) / pk;
-        if constexpr (!MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE)  // (experiment builds: no split)
         if (step_esplit(p)) {  // early split: a car wave and a LiDAR wave per workgroup
             if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
@@ -3674,7 +3121,6 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
             else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             return;
         }
-        if constexpr (!MEV_FUSED_STAGED && !MEV_POST_AFTER_LIDAR && !MEV_WB_LATE)
         if (step_split(p)) {  // two waves per workgroup (<= 4 waves per SIMD)
             if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);

@@ -172,6 +172,38 @@ def test_fused_and_two_kernel_paths_agree_traffic_full_size(mev):
         h.close()
 
 
+def test_env_deal_exact_beyond_residency(mev):
+    """The fused traffic kernel's NPC-aware env deal is scheduling only: with
+    16384 envs (four residency rounds of 4 waves per SIMD, so workgroups start
+    while earlier ones of the same step have already appended to the next
+    step's orders) the deal and the identity order agree bit for bit, every
+    output each step and the whole state (NPC fleets included) every 25 steps,
+    with auto-resets and busy intersections."""
+    E4 = 16384
+    cfg = dict(num_envs=E4, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=2.0, max_npcs=32,
+               max_steps=90, seed=21)
+    hs = [mev.Handle(**cfg) for _ in range(2)]
+    hs[1].set_env_deal(False)
+    for h in hs:
+        assert h.step_kernel() == 2
+    rng = np.random.default_rng(22)
+    most = 0
+    for t in range(150):
+        a = rng.uniform(-1, 1, (E4, 1, 2)).astype(np.float32)
+        o1 = hs[0].step(a, auto_reset=True)
+        o2 = hs[1].step(a, auto_reset=True)
+        for k in o1:
+            assert np.array_equal(o1[k], o2[k]), (t, k)
+        if t % 25 == 24:
+            s1, s2 = hs[0].get_state(), hs[1].get_state()
+            for k in s1:
+                assert np.array_equal(s1[k], s2[k]), (t, k)
+            most = max(most, int(s1["npc_count"].max()))
+    assert most >= 5  # the deal sorted envs over several NPC classes
+    for h in hs:
+        h.close()
+
+
 def test_step_kernel_selection(mev):
     h = _handle(mev)
     assert h.step_kernel() == 2  # automatic: fused at 4096 envs

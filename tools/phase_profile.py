@@ -17,12 +17,6 @@ import numpy as np  # noqa: E402
 import pkgload  # noqa: E402
 
 PHASES = ["npc", "physics+status", "SAT", "resolve+respawn+writeback", "obstacles+candidates", "obs head"]
-# MEV_LIB_VARIANT=stampsx: stamps 1-5 inside the physics phase
-PHASES_X = ["npc+car_update", "path index+target", "reward+success", "corner tests", "LDS writes",
-            "rest of the kernel"]
-# MEV_LIB_VARIANT=stampsy: stamps 1-5 after the physics phase
-PHASES_Y = ["npc..SAT, greedy resolution", "bonuses, team mix, flags", "respawn + state write-back",
-            "obstacles + candidates", "obs head: neighbour ranks", "obs head: row writes"]
 
 
 def main():
@@ -51,8 +45,7 @@ def main():
     tot = d.sum(1)
     print(f"envs={args.envs} agents={args.agents} rays={args.rays} traffic={args.traffic}: "
           f"total per env median {np.median(tot):.0f} cycles")
-    names = {"stampsx": PHASES_X, "stampsy": PHASES_Y}.get(os.environ.get("MEV_LIB_VARIANT"), PHASES)
-    for k, name in enumerate(names):
+    for k, name in enumerate(PHASES):
         print(f"  {name:24s} median {np.median(d[:, k]):9.0f}  mean {d[:, k].mean():9.0f}  share {d[:, k].sum() / tot.sum():6.1%}")
 
 
