@@ -224,35 +224,53 @@ def dry_run(args):
         dist.destroy_process_group()
 
 
-def verify_gather(env, _capi, E, N, D, world, gfmt, ls, dev):
-    """Root: decode the last gathered step's [world][bytes] buffer (sharding.PackedOutputs) and
-    check it: every rank's rows finite with valid status codes, and the root's own row equal,
-    bit for bit, to the library's decode of the same step (mev_get_outputs)."""
+def verify_gather(env, _capi, E, N, D, world, rank, gfmt, ls, dev, act, timeout_ms):
+    """Every rank (the gathered step is collective): snapshot the state, take one more step
+    with the gather, restore the snapshot and take the same step plainly (no gather, its own
+    output buffers).  The root decodes every rank's gathered rows (sharding.PackedOutputs; the
+    state format through mev_unpack_gathered on the device) and checks them: finite, valid
+    status codes, and its own row equal, bit for bit, to the plain step's outputs."""
     import torch
     import torch.utils.dlpack as tdl
     from marl_traffic_intersection_amd import sharding
 
-    ptr, per_rank, w = env.gather_result()
-    if not ptr or w != world:
-        return "missing"
-    lay = sharding.PackedOutputs(E, N, D, fmt=gfmt, lidar_slots=ls,
-                                 table=env.lidar_decode_table() if gfmt else None)
-    stacked = tdl.from_dlpack(env.output_dlpack("gathered"))
-    got = lay.unpack_gathered(stacked, world * E, world)
+    snap = torch.empty(env.snapshot_size(), dtype=torch.uint8, device=dev)
+    env.snapshot(snap, device=True)
+    env.step(act.data_ptr(), 1.0 / 60.0, auto_reset=True, device=True, gather=True)
+    env.gather_wait(timeout_ms)
+    got = None
+    if rank == 0:
+        ptr, per_rank, w = env.gather_result()
+        if not ptr or w != world:
+            got = "missing"
+        else:
+            lay = sharding.PackedOutputs(E, N, D, fmt=gfmt, lidar_slots=ls,
+                                         table=env.lidar_decode_table() if gfmt == 1 else None,
+                                         handle=env if gfmt == 2 else None)
+            stacked = tdl.from_dlpack(env.output_dlpack("gathered"))
+            got = {k: v.clone() for k, v in lay.unpack_gathered(stacked, world * E, world).items()}
     torch.cuda.synchronize(dev)
+    env.restore(snap, device=True)
+    plain = {k: torch.zeros_like(torch.as_tensor(v), device=dev) for k, v in env.alloc_outputs().items()}
+    env.step(act.data_ptr(), 1.0 / 60.0, out=plain, auto_reset=True, device=True)
+    torch.cuda.synchronize(dev)
+    if rank != 0:
+        return None
+    if isinstance(got, str):
+        return got
     if not (torch.isfinite(got["obs"]).all().item() and torch.isfinite(got["reward"]).all().item()
             and int(got["status"].max().item()) <= 5):
         return "FAILED: non-finite or invalid rows"
-    mine = env.get_outputs()
     for k in sharding.PackedOutputs.FIELDS:
-        a = got[k][:E].cpu().numpy()
-        b = mine[k]
-        if a.dtype.kind == "f":
-            a, b = a.view("u4"), b.view("u4")
-        if not (a == b).all():
-            return f"FAILED: root row {k} differs from the library's decode"
-    return (f"decoded {world} rank rows ({'u8 LiDAR codes' if gfmt else 'f32 rows'}): finite, valid status codes; "
-            f"the root's row bit-equal to mev_get_outputs of the same step")
+        a, b = got[k][:E].contiguous(), plain[k]
+        if a.dtype == torch.float32:
+            a, b = a.view(torch.int32), b.view(torch.int32)
+        if not torch.equal(a, b):
+            return f"FAILED: root row {k} differs from the plain step"
+    what = {0: "f32 rows", 1: "31-float heads + u8 LiDAR codes", 2: "post-step state + u8 LiDAR codes, heads rebuilt "
+            "on the root"}[gfmt]
+    return (f"decoded {world} rank rows ({what}): finite, valid status codes; the root's row bit-equal to the same "
+            f"step taken without the gather from the same snapshot")
 
 
 def main():
@@ -264,8 +282,10 @@ def main():
     ap.add_argument("--no-gather", action="store_true",
                     help="skip the second timed phase (every step's outputs gathered to rank 0 over RCCL)")
     ap.add_argument("--gather-timeout", type=float, default=120.0, help="seconds before a stuck gather is aborted")
-    ap.add_argument("--gather-format", choices=("u8", "f32"), default="u8",
-                    help="packed gather rows: u8 = 31-float heads + one LiDAR code per beam (lossless), f32 = plain rows")
+    ap.add_argument("--gather-format", choices=("state", "u8", "f32"), default="state",
+                    help="packed gather rows (all lossless): state = each agent's post-step state + one LiDAR code "
+                         "per beam, the 31-float heads rebuilt on the root; u8 = 31-float heads + LiDAR codes; "
+                         "f32 = plain rows")
     ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="untimed steps for this long before the warm-up (SIMD clock ramp from idle); 0 = none")
     ap.add_argument("--no-kernel-events", action="store_true", help="do not record per-kernel HIP events")
@@ -404,7 +424,8 @@ def main():
             import threading
             init_err = []
 
-            gfmt = _capi.MEV_GATHER_LIDAR_U8 if args.gather_format == "u8" else _capi.MEV_GATHER_F32
+            gfmt = {"f32": _capi.MEV_GATHER_F32, "u8": _capi.MEV_GATHER_LIDAR_U8,
+                    "state": _capi.MEV_GATHER_STATE}[args.gather_format]
             env.set_gather_format(gfmt)
 
             def _init():
@@ -459,15 +480,22 @@ def main():
                     "ms_per_step": round(g_elapsed / K * 1e3, 5), "format": args.gather_format,
                     "bytes_per_rank_per_step": per, "bytes_per_rank_per_step_f32_rows": per_f32,
                     "root_ingress_GBs": round(per * (world - 1) / (g_elapsed / K) / 1e9, 2),
-                    "what": "phase 1's steps with every step's packed outputs (obs|reward|done|status|"
-                            "terminated|truncated; u8: 31-float obs heads + one LiDAR code per beam, decoded "
-                            "bit-exactly on the root) gathered to rank 0: one grouped ncclSend/ncclRecv per step "
-                            "from the C ABI (MEV_GATHER_TO_ROOT), on a communication stream overlapping the next step",
+                    "what": "phase 1's steps with every step's packed outputs (reward|done|status|terminated|"
+                            "truncated and the observations; state: each agent's post-step state (22 B) + one LiDAR "
+                            "code per beam, the 31-float heads rebuilt bit-exactly on the root by mev_unpack_gathered; "
+                            "u8: 31-float heads + LiDAR codes; f32: plain rows) gathered to rank 0: one grouped "
+                            "ncclSend/ncclRecv per step from the C ABI (MEV_GATHER_TO_ROOT), on a communication "
+                            "stream overlapping the next step",
                     "bound": "at N > 1 the root receives (N - 1) x bytes_per_rank_per_step every step over its xGMI "
                              "links, so this phase is bound by the root's ingress, not by the step kernel; at N = 1 "
                              "the root's row is written in place and nothing moves"})
+                try:
+                    v = verify_gather(env, _capi, E, N, D, world, rank, gfmt, ls, dev, actions[W + K - 1],
+                                      int(args.gather_timeout * 1000))
+                except Exception as exc:
+                    v = f"FAILED: rank {rank}: {exc}"[:300]
                 if rank == 0:
-                    gather["verified"] = verify_gather(env, _capi, E, N, D, world, gfmt, ls, dev)
+                    gather["verified"] = v
             elif "error" not in gather:
                 gather["error"] = "another rank failed in the gather phase"
         elif "error" not in gather:
@@ -494,7 +522,9 @@ def main():
             pb = algorithmic_bytes_per_agent_step(RAYS) * E * N
             achieved = pb / (stream_ms * 1e-3) / 1e9
             tab = 'true' if dist_table_needed() else 'false'
-            kname = f"mev::k_step<false, {tab}, {8 if N_AGENTS <= 8 and RAYS <= 128 else 0}, 64, 1, false>"
+            # the instantiation launch_fused picks at this shape (rocprofv3 prints the same 7 arguments:
+            # TRAFFIC, TAB, NM, KM, PK, SPLIT, ESPLIT -- one env per wave, no split at >= 2048 workgroups)
+            kname = f"mev::k_step<false, {tab}, {8 if N_AGENTS <= 8 and RAYS <= 128 else 0}, 64, 1, false, false>"
             roofline = {
                 "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic_of.get("k_step"),

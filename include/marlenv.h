@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 1
+#define MEV_ABI_VERSION 2  /* 2: MEV_GATHER_STATE, MEV_PK_STATE (MEV_PK_FIELDS 7 -> 8), mev_unpack_gathered */
 
 enum {
     MEV_OK = 0,
@@ -164,7 +164,12 @@ int mev_reset(mev_handle* h, const uint8_t* env_mask, float* obs, uint32_t flags
 /* One step of every env. */
 int mev_step(mev_handle* h, const mev_step_args* args);
 
-/* Outputs of the last step / reset, from the handle's own device buffers. */
+/* Outputs of the last step / reset, from the handle's own device buffers.
+ * Lifetime: after a step that wrote caller-owned output buffers (device
+ * pointers in mev_step_args), this call, mev_device_outputs and
+ * mev_output_dlpack read those buffers -- keep them allocated and unmodified
+ * until the next mev_step / mev_reset of the handle (or read the outputs from
+ * them directly). */
 int mev_get_outputs(mev_handle* h, float* obs, float* reward, uint8_t* done, uint8_t* status,
                     uint8_t* terminated, uint8_t* truncated, int32_t* agents_alive, int32_t* step,
                     uint32_t flags);
@@ -177,8 +182,9 @@ int mev_set_state(mev_handle* h, const mev_state* in);
 /* Device pointers of the handle's internal output buffers (zero-copy consumers),
  * holding the last step's / reset's outputs: a step that wrote elsewhere (caller
  * buffers, the pinned block of a small host-mode step, a packed gather row) is
- * first copied into them on the handle's stream.  Device-mode steps without
- * output pointers write them in place. */
+ * first copied into them on the handle's stream (caller buffers must still be
+ * valid then: see mev_get_outputs).  Device-mode steps without output pointers
+ * write them in place. */
 int mev_device_outputs(mev_handle* h, float** obs, float** reward, uint8_t** done, uint8_t** status,
                        uint8_t** terminated, uint8_t** truncated);
 
@@ -264,17 +270,22 @@ int mev_set_env_deal(mev_handle* h, int32_t on);
  * slots) is answered by a kernel that stays resident between steps (k_serve):
  * the host posts the step in a mailbox of pinned memory and the kernel answers
  * once its outputs are there -- a PCIe round trip instead of a kernel launch and
- * a stream synchronisation.  The kernel leaves after `idle` ms without a step
- * (MEV_SERVE_IDLE_MS, default 20) and is launched again by the next one; every
- * other call on the handle stops it first.  Only on the handle's own stream (not
- * after mev_set_stream); the kernel itself runs on a non-blocking highest-priority
+ * a stream synchronisation.  The kernel leaves when no step is posted for its
+ * idle limit and is launched again by the next one; every other call on the
+ * handle stops it first.  Only on the handle's own stream (not after
+ * mev_set_stream); the kernel itself runs on a non-blocking highest-priority
  * stream of its own; at most 2 servers are resident per process (other handles
- * step launched).  While it is resident a device-wide synchronisation
- * (hipDeviceSynchronize) waits for its idle exit.  mode: 0 = off, 1 = automatic
- * (default; MEV_NO_SERVE=1 in the environment turns it off).  mev_serve_stats:
- * steps served, server launches, whether one is running.  Replaces nothing in the
- * reference (its env.py steps one IntersectionEnv per call on the CPU,
- * cpp/bindings.cpp:53-55). */
+ * step launched).  While it is resident, every device-wide wait of the process
+ * (hipDeviceSynchronize, torch.cuda.synchronize(), frees that wait for the
+ * device) waits for its idle exit, so the idle limit is adaptive: 8 x the
+ * moving average of the host's time between an answer and the next post,
+ * within [0.2, 2] ms; after 4 consecutive posts that found the server already
+ * gone (a device-wide wait or a slow host between steps) the next 1024 host
+ * steps are launched instead.  MEV_SERVE_IDLE_MS=n (1..1000) fixes the limit.
+ * mode: 0 = off, 1 = automatic (default; MEV_NO_SERVE=1 in the environment
+ * turns it off).  mev_serve_stats: steps served, server launches, whether one
+ * is running.  Replaces nothing in the reference (its env.py steps one
+ * IntersectionEnv per call on the CPU, cpp/bindings.cpp:53-55). */
 int mev_set_serve(mev_handle* h, int32_t mode);
 int mev_serve_stats(const mev_handle* h, uint64_t* steps, uint64_t* launches, int32_t* running);
 
@@ -294,7 +305,7 @@ int mev_serve_stats(const mev_handle* h, uint64_t* steps, uint64_t* launches, in
 #define MEV_GATHER_TO_ROOT 0x4u /* mev_step: write the outputs packed and gather them to the root rank */
 #define MEV_COMM_ID_BYTES 128   /* == NCCL_UNIQUE_ID_BYTES */
 enum { MEV_PK_OBS = 0, MEV_PK_REWARD, MEV_PK_DONE, MEV_PK_STATUS, MEV_PK_TERMINATED, MEV_PK_TRUNCATED, MEV_PK_COUNT,
-       MEV_PK_LIDAR = MEV_PK_COUNT /* compact format only */, MEV_PK_FIELDS };
+       MEV_PK_LIDAR = MEV_PK_COUNT /* compact formats only */, MEV_PK_STATE /* state format only */, MEV_PK_FIELDS };
 int mev_packed_layout(int32_t slots, int32_t num_agents, int32_t obs_dim, uint64_t* offsets /*[MEV_PK_COUNT]*/,
                       uint64_t* bytes);
 /* Gather formats (mev_set_gather_format, before mev_comm_init):
@@ -305,10 +316,19 @@ int mev_packed_layout(int32_t slots, int32_t num_agents, int32_t obs_dim, uint64
  *     are table[code] (mev_lidar_decode_table, 256 entries), bit-identical to the plain
  *     step's; padding columns beyond 31 + lidar_slots are zero.  At R = 64, N = 8 a row
  *     shrinks from 380 B to 194 B (the message from 12.66 MB to 6.37 MB at 4096 envs).
- * mev_packed_layout2: offsets of all MEV_PK_FIELDS fields for either format (the LiDAR
- * field is empty in MEV_GATHER_F32).  Host-only. */
+ *   MEV_GATHER_STATE (no traffic): no observation field at all; the LiDAR codes as in
+ *     MEV_GATHER_LIDAR_U8, and a field MEV_PK_STATE with each agent's post-step state
+ *     as arrays of n = slots * N: x, y, v, heading f32 | route, path index i16 |
+ *     intention, alive u8 (22 B per agent).  get_observations (cpp/IntersectionEnv.cpp:
+ *     418-520) is a pure function of that state, so the root rebuilds the 31-float
+ *     head with the step's own device code (mev_unpack_gathered), bit-identical to
+ *     the plain step's rows.  At R = 64, N = 8 a row is 92 B instead of 380 B (the
+ *     message 3.03 MB instead of 12.66 MB at 4096 envs); the ranks also skip the head.
+ * mev_packed_layout2: offsets of all MEV_PK_FIELDS fields for any format (fields a
+ * format does not use are empty).  Host-only. */
 #define MEV_GATHER_F32 0
 #define MEV_GATHER_LIDAR_U8 1
+#define MEV_GATHER_STATE 2
 int mev_packed_layout2(int32_t slots, int32_t num_agents, int32_t obs_dim, int32_t lidar_slots, int32_t format,
                        uint64_t* offsets /*[MEV_PK_FIELDS]*/, uint64_t* bytes);
 int mev_set_gather_format(mev_handle* h, int32_t format);
@@ -340,6 +360,15 @@ int mev_comm_destroy(mev_handle* h);
  * MEV_E_HIP returned, so a lost peer cannot hang the caller forever. */
 int mev_gather_result(mev_handle* h, void** stacked, uint64_t* bytes_per_rank, int32_t* world);
 int mev_gather_wait(mev_handle* h, int32_t timeout_ms);
+/* Root (any gather format): the float observation rows of a gathered buffer
+ * `stacked` (device, [world][bytes] as mev_gather_result returns it, in the
+ * handle's gather format and slots) into obs (device, [world][slots][N][D]), on
+ * the handle's stream -- the rows each rank's plain step would have written, bit
+ * for bit (F32: copied; LIDAR_U8: heads + decoded codes; STATE: heads rebuilt from
+ * the shipped state).  Slots beyond a rank's envs hold whatever their (zeroed)
+ * message decodes to.  Reward, done, status, terminated and truncated are read
+ * from the buffer directly (mev_packed_layout2). */
+int mev_unpack_gathered(mev_handle* h, const void* stacked, int32_t world, float* obs);
 
 /* ---- Zero-copy export (DLPack) -----------------------------------------
  * the handle's device output buffers as DLPack tensors for

@@ -25,8 +25,10 @@ MEV_GATHER_TO_ROOT = 0x4
 MEV_COMM_ID_BYTES = 128
 MEV_GATHER_F32 = 0
 MEV_GATHER_LIDAR_U8 = 1
+MEV_GATHER_STATE = 2
+STATE_BYTES_PER_AGENT = 22
 # packed-output fields (mev_packed_layout2) and DLPack outputs (mev_output_dlpack), include/marlenv.h order
-PACKED_FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated", "lidar")
+PACKED_FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated", "lidar", "state")
 DLPACK_OUTPUTS = ("obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step", "gathered")
 
 STATUS_NAMES = ("ALIVE", "DEAD", "SUCCESS", "CRASH_WALL", "CRASH_LINE", "CRASH_CAR")
@@ -45,6 +47,7 @@ EXPORTED = (
     "mev_set_step_split", "mev_get_step_split", "mev_set_env_deal", "mev_set_serve", "mev_serve_stats",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
     "mev_gather_wait", "mev_output_dlpack", "mev_packed_layout2", "mev_set_gather_format", "mev_lidar_decode_table",
+    "mev_unpack_gathered",
 )
 
 
@@ -170,6 +173,7 @@ def load_library(variant: str = None):
     L.mev_comm_destroy.argtypes = [_vp]
     L.mev_gather_result.argtypes = [_vp, ctypes.POINTER(_vp), u64p, i32p]
     L.mev_gather_wait.argtypes = [_vp, ctypes.c_int32]
+    L.mev_unpack_gathered.argtypes = [_vp, _vp, ctypes.c_int32, _vp]
     L.mev_output_dlpack.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(_vp)]
     _libs[variant] = L
     return L
@@ -446,8 +450,9 @@ class Handle:
         self.comm = dict(world=int(world), rank=int(rank), root=int(root), slots=int(slots) or self.E)
 
     def set_gather_format(self, fmt: int):
-        """MEV_GATHER_F32 (plain obs rows) or MEV_GATHER_LIDAR_U8 (31-float heads + one LiDAR code per
-        beam, lossless); before comm_init."""
+        """MEV_GATHER_F32 (plain obs rows), MEV_GATHER_LIDAR_U8 (31-float heads + one LiDAR code per
+        beam) or MEV_GATHER_STATE (post-step state + LiDAR codes, the heads rebuilt on the root);
+        all lossless; before comm_init."""
         _check(self._lib.mev_set_gather_format(self._h, int(fmt)))
         self.gather_format = int(fmt)
 
@@ -474,6 +479,11 @@ class Handle:
     def gather_wait(self, timeout_ms: int = 0):
         """Host wait for every gather issued so far (timeout: the communicator is aborted, MevError)."""
         _check(self._lib.mev_gather_wait(self._h, int(timeout_ms)))
+
+    def unpack_gathered(self, stacked_ptr: int, world: int, obs_ptr: int):
+        """Root: the float observation rows [world][slots][N][D] (device, obs_ptr) of a gathered
+        [world][bytes] device buffer in this handle's format (mev_unpack_gathered, on its stream)."""
+        _check(self._lib.mev_unpack_gathered(self._h, _vp(int(stacked_ptr)), int(world), _vp(int(obs_ptr))))
 
     # -- zero-copy export (DLPack) ----------------------------------------
     def output_dlpack(self, which: str):
@@ -657,7 +667,8 @@ def car_check_collision(box_a, box_b) -> bool:
 
 def packed_layout(slots: int, agents: int, obs_dim: int, fmt: int = MEV_GATHER_F32, lidar_slots: int = 0):
     """(offsets by field, total bytes) of one rank's packed outputs (mev_packed_layout2; host-only, no GPU).
-    fmt MEV_GATHER_LIDAR_U8: "obs" holds [slots][N][31] heads and "lidar" [slots][N][lidar_slots] codes."""
+    fmt MEV_GATHER_LIDAR_U8: "obs" holds [slots][N][31] heads and "lidar" [slots][N][lidar_slots] codes;
+    MEV_GATHER_STATE: "obs" is empty, "state" holds the post-step state arrays (22 B per agent)."""
     off = (ctypes.c_uint64 * len(PACKED_FIELDS))()
     n = ctypes.c_uint64()
     _check(load_library().mev_packed_layout2(int(slots), int(agents), int(obs_dim), int(lidar_slots), int(fmt), off,

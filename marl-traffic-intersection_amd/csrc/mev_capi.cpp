@@ -162,10 +162,25 @@ struct mev_handle {
     int serve_mode = 1;                 // 0 off, 1 automatic
     mev::ServeBox* sbox = nullptr;      // host address of the mailbox (mapped, coherent)
     mev::ServeBox* sbox_dev = nullptr;  // its device address
-    bool serve_running = false;         // an instance may be resident on `stream`
-    int serve_wg = 0;                   // its workgroups
-    uint32_t serve_seq = 0, serve_sid = 0, serve_epoch = 0;
+    // (atomic: serve_slot reads other handles' flags, which their own threads write)
+    std::atomic<bool> serve_running{false};  // an instance may be resident on `stream`
+    int serve_wg = 0;                        // its workgroups
+    uint32_t serve_seq = 0, serve_sid = 0;
+    std::atomic<uint32_t> serve_epoch{0};
     uint64_t serve_steps = 0, serve_launches = 0;
+    // Adaptive idle limit: a resident server makes every device-wide
+    // wait of the process (hipDeviceSynchronize, torch.cuda.synchronize, some frees)
+    // wait for its idle exit, so it stays only a few host gaps long: 8 x the moving
+    // average of the host's time between an answer and the next post (each gap
+    // counted up to 2 ms), within [0.2, 2] ms; it starts at the cap and follows the
+    // host's pace.  Posts that keep finding the server gone (a device-wide wait, or
+    // a host slower than 2 ms between steps) pause serving: the next kPausedSteps
+    // host steps are launched.
+    double serve_gap_us = 250.0;
+    int serve_misses = 0;
+    uint64_t serve_pause = 0;
+    uint64_t serve_misses_total = 0;
+    std::chrono::steady_clock::time_point serve_t_answer{};
     // the server's own stream: non-blocking, at the highest priority, whose hardware
     // queues are not the ones normal-priority streams share (GPU_MAX_HW_QUEUES of them):
     // a resident kernel holds back whatever another stream queues behind it on its queue
@@ -742,13 +757,23 @@ inline void cpu_relax() {
 #endif
 }
 
-uint32_t serve_idle_ticks() {
-    static const uint32_t ms = [] {
+constexpr double kServeIdleMinUs = 200.0, kServeIdleMaxUs = 2000.0;
+constexpr int kServeMissLimit = 4;        // consecutive posts that found the server gone ...
+constexpr uint64_t kPausedSteps = 1024;  // ... pause serving for this many host steps
+
+// the idle limit of the next instance, in ticks of s_memrealtime (100 MHz):
+// MEV_SERVE_IDLE_MS fixes it (1..1000 ms); otherwise adaptive (mev_handle::serve_gap_us)
+uint32_t serve_idle_ticks(const mev_handle* h) {
+    static const int fixed_ms = [] {
         const char* v = getenv("MEV_SERVE_IDLE_MS");
-        const int m = v ? atoi(v) : 20;
-        return (uint32_t)(m < 1 ? 1 : (m > 1000 ? 1000 : m));
+        if (!v) return 0;
+        const int m = atoi(v);
+        return m < 1 ? 1 : (m > 1000 ? 1000 : m);
     }();
-    return ms * 100000u;  // s_memrealtime: 100 MHz
+    if (fixed_ms > 0) return (uint32_t)fixed_ms * 100000u;
+    double us = 8.0 * h->serve_gap_us;
+    us = us < kServeIdleMinUs ? kServeIdleMinUs : (us > kServeIdleMaxUs ? kServeIdleMaxUs : us);
+    return (uint32_t)(us * 100.0);
 }
 
 // post a command: the line's fields are written by the caller, then cmd, then seq (release)
@@ -766,7 +791,7 @@ int serve_launch(mev_handle* h) {
     sa.actions = reinterpret_cast<const float*>(h->pin_dev + h->pin_off[0]);
     sa.spawn_route = reinterpret_cast<const int32_t*>(h->pin_dev + h->pin_off[1]);
     sa.epoch = ++h->serve_epoch;
-    sa.idle_ticks = serve_idle_ticks();
+    sa.idle_ticks = serve_idle_ticks(h);
     HIP_TRY(hipEventRecord(h->serve_ev, h->stream));  // after whatever the handle's stream holds
     HIP_TRY(hipStreamWaitEvent(h->serve_stream, h->serve_ev, 0));
     HIP_TRY(mev::launch_serve(h->sp, h->d_sp, sa, h->pin_out, h->serve_stream));
@@ -795,7 +820,7 @@ bool serve_resident(const mev_handle* h) {
 // h may keep or start a resident server
 bool serve_slot(mev_handle* h) {
     std::lock_guard<std::mutex> lk(g_serve_mu);
-    if (h->serve_running) return true;
+    if (serve_resident(h)) return true;  // (one that left idle competes for a slot again)
     int n = 0;
     for (const mev_handle* x : g_serving) n += (x != h && serve_resident(x)) ? 1 : 0;
     if (n >= kMaxResidentServers) return false;
@@ -843,6 +868,10 @@ static bool serve_wanted(mev_handle* h) {
     // whatever a caller queues behind it on a stream it shares)
     if (off || h->serve_mode == 0 || !h->tev.empty() || h->stream != h->own_stream || !mev::serve_fits(h->sp))
         return false;
+    if (h->serve_pause > 0) {  // repeated idle exits between posts: launched steps for a while
+        --h->serve_pause;
+        return false;
+    }
     if (h->sbox) return true;
     if (!h->serve_stream || !h->serve_ev) {
         int lo = 0, hi = 0;
@@ -877,6 +906,19 @@ static bool serve_wanted(mev_handle* h) {
 // posted again and a new instance launched; workgroups that had answered skip it.
 static int serve_step(mev_handle* h, const mev::StepInputs& in) {
     volatile mev::ServeBox* b = h->sbox;
+    if (h->serve_running) {  // the host gap since the last answer, and whether the server waited for it
+        const double gap_us = 1000.0 * ms_since(h->serve_t_answer);
+        h->serve_gap_us = 0.875 * h->serve_gap_us + 0.125 * (gap_us < kServeIdleMaxUs ? gap_us : kServeIdleMaxUs);
+        if (b->exited[0] != h->serve_epoch) {  // still resident: a hit
+            h->serve_misses = 0;
+        } else {  // it left (idle) before this post
+            ++h->serve_misses_total;
+            if (++h->serve_misses >= kServeMissLimit) {
+                h->serve_misses = 0;
+                h->serve_pause = kPausedSteps;
+            }
+        }
+    }
     const uint32_t sid = ++h->serve_sid;
     uint32_t u;
     b->sid = sid;
@@ -909,6 +951,7 @@ static int serve_step(mev_handle* h, const mev::StepInputs& in) {
     }
     std::atomic_thread_fence(std::memory_order_seq_cst);
     ++h->serve_steps;
+    h->serve_t_answer = std::chrono::steady_clock::now();
     return MEV_OK;
 }
 
@@ -985,7 +1028,13 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         o.status = base + h->pk_off[MEV_PK_STATUS];
         o.term = base + h->pk_off[MEV_PK_TERMINATED];
         o.trunc = base + h->pk_off[MEV_PK_TRUNCATED];
-        if (h->gather_fmt == MEV_GATHER_LIDAR_U8) {  // heads [slots][N][31] + one LiDAR code per beam
+        if (h->gather_fmt == MEV_GATHER_STATE) {  // post-step state + one LiDAR code per beam, no heads
+            o.obs = nullptr;
+            o.obs_ld = 0;
+            o.lidar_u8 = base + h->pk_off[MEV_PK_LIDAR];
+            o.state = base + h->pk_off[MEV_PK_STATE];
+            o.state_n = int64_t(h->slots) * h->cfg.num_agents;
+        } else if (h->gather_fmt == MEV_GATHER_LIDAR_U8) {  // heads [slots][N][31] + one LiDAR code per beam
             o.obs_ld = mev::OBS_HEAD;
             o.lidar_u8 = base + h->pk_off[MEV_PK_LIDAR];
         }
@@ -1190,7 +1239,10 @@ static int sync_internal(mev_handle* h) {
         if (!src || src == dst) return hipSuccess;
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, h->stream);
     };
-    if (L.lidar_u8)  // a compact-format gather row: decode heads + LiDAR codes into the obs rows
+    if (L.state)  // a state-format gather row: rebuild the heads, decode the LiDAR codes
+        HIP_TRY(mev::launch_decode_state(h->sp, L.state, L.lidar_u8, 0, int(L.state_n / h->cfg.num_agents), int(E),
+                                         h->d_lidar_table, I.obs, h->stream));
+    else if (L.lidar_u8)  // a compact-format gather row: decode heads + LiDAR codes into the obs rows
         HIP_TRY(mev::launch_unpack_lidar_u8(L.obs, L.lidar_u8, h->d_lidar_table, I.obs, int(EN), h->D, h->lidar_slots,
                                             h->stream));
     else
@@ -1512,12 +1564,14 @@ int mev_packed_layout2(int32_t slots, int32_t num_agents, int32_t obs_dim, int32
     if (!offsets || !bytes) return fail(MEV_E_INVALID, "null argument");
     if (slots < 1 || num_agents < 1 || obs_dim < mev::OBS_HEAD || lidar_slots < 0 || lidar_slots > obs_dim - mev::OBS_HEAD)
         return fail(MEV_E_INVALID, "slots and agents must be >= 1, obs_dim >= 31, 0 <= lidar_slots <= obs_dim - 31");
-    if (format != MEV_GATHER_F32 && format != MEV_GATHER_LIDAR_U8) return fail(MEV_E_INVALID, "unknown gather format");
+    if (format != MEV_GATHER_F32 && format != MEV_GATHER_LIDAR_U8 && format != MEV_GATHER_STATE)
+        return fail(MEV_E_INVALID, "unknown gather format");
     const uint64_t C = uint64_t(slots), N = uint64_t(num_agents);
-    const bool u8 = format == MEV_GATHER_LIDAR_U8;
-    const uint64_t row = u8 ? uint64_t(mev::OBS_HEAD) : uint64_t(obs_dim);
+    const bool codes = format != MEV_GATHER_F32, st = format == MEV_GATHER_STATE;
+    const uint64_t row = st ? 0 : (codes ? uint64_t(mev::OBS_HEAD) : uint64_t(obs_dim));
     const uint64_t sizes[MEV_PK_FIELDS] = {C * N * row * 4, C * N * 4, C * N, C * N, C, C,
-                                           u8 ? C * N * uint64_t(lidar_slots) : 0};
+                                           codes ? C * N * uint64_t(lidar_slots) : 0,
+                                           st ? C * N * uint64_t(mev::kStateBytesPerAgent) : 0};
     uint64_t off = 0;
     for (int f = 0; f < MEV_PK_FIELDS; ++f) {
         off = (off + 255) & ~uint64_t(255);
@@ -1530,10 +1584,13 @@ int mev_packed_layout2(int32_t slots, int32_t num_agents, int32_t obs_dim, int32
 
 int mev_set_gather_format(mev_handle* h, int32_t format) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
-    if (format != MEV_GATHER_F32 && format != MEV_GATHER_LIDAR_U8) return fail(MEV_E_INVALID, "unknown gather format");
+    if (format != MEV_GATHER_F32 && format != MEV_GATHER_LIDAR_U8 && format != MEV_GATHER_STATE)
+        return fail(MEV_E_INVALID, "unknown gather format");
     if (h->comm) return fail(MEV_E_INVALID, "set the gather format before mev_comm_init");
-    if (format == MEV_GATHER_LIDAR_U8 && h->sp.lidar_steps + 1 >= mev::kLidarCodeDead)
-        return fail(MEV_E_INVALID, "the compact gather format needs at most 253 LiDAR march probes");
+    if (format != MEV_GATHER_F32 && h->sp.lidar_steps + 1 >= mev::kLidarCodeDead)
+        return fail(MEV_E_INVALID, "the compact gather formats need at most 253 LiDAR march probes");
+    if (format == MEV_GATHER_STATE && (h->cfg.traffic_flow || h->cfg.num_agents > 64))
+        return fail(MEV_E_INVALID, "the state gather format is for handles without traffic (N <= 64)");
     h->gather_fmt = format;
     return MEV_OK;
 }
@@ -1611,6 +1668,32 @@ int mev_gather_result(mev_handle* h, void** stacked, uint64_t* bytes_per_rank, i
     *stacked = h->pk_buf[b];
     *bytes_per_rank = h->pk_bytes;
     *world = h->world;
+    return MEV_OK;
+}
+
+int mev_unpack_gathered(mev_handle* h, const void* stacked, int32_t world, float* obs) {
+    if (!h || !stacked || !obs) return fail(MEV_E_INVALID, "null argument");
+    if (!h->comm) return fail(MEV_E_INVALID, "no communicator (mev_comm_init): the layout is the handle's");
+    if (world < 1) return fail(MEV_E_INVALID, "world must be >= 1");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
+    const uint8_t* sb = static_cast<const uint8_t*>(stacked);
+    const size_t C = size_t(h->slots), N = size_t(h->cfg.num_agents), D = size_t(h->D);
+    const size_t rows = C * N;
+    for (int r = 0; r < world; ++r) {
+        const uint8_t* m = sb + size_t(r) * h->pk_bytes;
+        float* o = obs + size_t(r) * rows * D;
+        if (h->gather_fmt == MEV_GATHER_F32)
+            HIP_TRY(hipMemcpyAsync(o, m + h->pk_off[MEV_PK_OBS], rows * D * sizeof(float), hipMemcpyDeviceToDevice,
+                                   h->stream));
+        else if (h->gather_fmt == MEV_GATHER_LIDAR_U8)
+            HIP_TRY(mev::launch_unpack_lidar_u8(reinterpret_cast<const float*>(m + h->pk_off[MEV_PK_OBS]),
+                                                m + h->pk_off[MEV_PK_LIDAR], h->d_lidar_table, o, int(rows), h->D,
+                                                h->lidar_slots, h->stream));
+    }
+    if (h->gather_fmt == MEV_GATHER_STATE)  // one launch over every rank's envs
+        HIP_TRY(mev::launch_decode_state(h->sp, sb + h->pk_off[MEV_PK_STATE], sb + h->pk_off[MEV_PK_LIDAR], h->pk_bytes,
+                                         int(C), int(C) * world, h->d_lidar_table, obs, h->stream));
     return MEV_OK;
 }
 

@@ -67,12 +67,30 @@ struct Outputs {
     // beyond 31 + lidar_slots are not written)
     int32_t obs_ld;
     uint8_t* lidar_u8;
+    // The state gather format (MEV_GATHER_STATE; obs == nullptr, lidar_u8 set): no
+    // observation head is written; instead every agent's post-step state, from which
+    // the root rebuilds the head (launch_decode_state), as SoA arrays of state_n
+    // elements at `state` (layout: kStateBytesPerAgent).  Agent a = e * N + i.
+    uint8_t* state;
+    int64_t state_n;
 };
-// the LiDAR code of a dead agent's beam in the compact gather format
+// the LiDAR code of a dead agent's beam in the compact gather formats
 constexpr int kLidarCodeDead = 255;
 // decode the compact format's rows: obs [n][D] from heads [n][31] and codes [n][slots]
 hipError_t launch_unpack_lidar_u8(const float* head, const uint8_t* codes, const float* table, float* obs, int n,
                                   int D, int slots, hipStream_t s);
+// The state format's per-agent arrays, n elements each: x, y, v, heading f32 at
+// byte offsets 0, 4n, 8n, 12n; route, path index i16 at 16n, 18n; intention,
+// alive u8 at 20n, 21n -- 22 bytes per agent.
+constexpr int kStateBytesPerAgent = 22;
+struct SimParams;
+// Rebuild the float observation rows of state-format messages (no traffic): n_env
+// envs, env g in message g / C (messages `stride` bytes apart), slot g % C; each
+// message's state arrays (C * N elements) at state0 and LiDAR codes [C*N][lidar_slots]
+// at codes0 (+ the message offset); obs [n_env][N][D] -- the rows the plain step
+// writes, bit for bit (write_obs_head_tg + the decode table).
+hipError_t launch_decode_state(const SimParams& p, const uint8_t* state0, const uint8_t* codes0, size_t stride, int C,
+                               int n_env, const float* table, float* obs, hipStream_t s);
 
 struct SimParams {
     int32_t E, N, R, K, D;   // envs, agents, beams, npc slots, obs_dim
@@ -112,7 +130,7 @@ struct SimParams {
     // two waves per fused workgroup (host side): 0 auto (<= 2048 workgroups), 1 off, 2 on
     int32_t step_split;
     // NPC-aware env deal of the fused traffic kernel (see kDealLists): per (ring, list,
-    // class) counters, each on its own 128-B line, and per (list, class) env orders
+    // class) counters, each on its own 128-B line, and per (ring, list, class) env orders
     int32_t* deal_cnt;    // [3][kDealLists][kDealClasses][kDealPad]
     int32_t* deal_order;  // [3][kDealLists][kDealClasses][E]: rings like the counters
 };

@@ -1879,6 +1879,24 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
     }
     // ---- the final ego state back to HBM (lane = agent)
     ego_writeback(p, e, NE, N, el, do_reset, tid);
+    if (out.state) {
+        // the state gather format: the post-step state the root rebuilds the head from
+        // (launch_decode_state), instead of the head itself
+        const size_t n = (size_t)out.state_n;
+        __attribute__((address_space(1))) uint8_t* sb = gmem(out.state);
+        for (int i = tid; i < N; i += WAVE) {
+            const size_t a = (size_t)e * NE + i;
+            reinterpret_cast<__attribute__((address_space(1))) float*>(sb)[a] = el.x[i];
+            reinterpret_cast<__attribute__((address_space(1))) float*>(sb + 4 * n)[a] = el.y[i];
+            reinterpret_cast<__attribute__((address_space(1))) float*>(sb + 8 * n)[a] = el.v[i];
+            reinterpret_cast<__attribute__((address_space(1))) float*>(sb + 12 * n)[a] = el.h[i];
+            reinterpret_cast<__attribute__((address_space(1))) int16_t*>(sb + 16 * n)[a] = (int16_t)el.route[i];
+            reinterpret_cast<__attribute__((address_space(1))) int16_t*>(sb + 18 * n)[a] = (int16_t)el.pidx[i];
+            sb[20 * n + a] = (uint8_t)el.intent[i];
+            sb[21 * n + a] = el.alive[i];
+        }
+        return;
+    }
     // ---- observation head (:418-520)
     const int C = PK > 1 ? NE : N + (TRAFFIC ? ncnt : 0);  // neighbour candidates per agent (+ itself)
     if (C <= 8) {
@@ -3218,6 +3236,67 @@ hipError_t launch_unpack_lidar_u8(const float* head, const uint8_t* codes, const
     if (total == 0) return hipSuccess;
     hipLaunchKernelGGL(k_unpack_lidar_u8, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, head, codes, table,
                        obs, n, D, slots);
+    return hipGetLastError();
+}
+
+// The state gather format's decode (root): one wave per env rebuilds its agents'
+// rows from the shipped post-step state -- get_observations (IntersectionEnv.cpp:
+// 418-520) is a pure function of it -- with the step's own write_obs_head_tg,
+// and the LiDAR block from the codes through the decode table.  No traffic (the
+// format is refused for traffic handles: NPC states would outweigh the rows).
+__global__ __launch_bounds__(WAVE) void k_decode_state(SimParams p, const uint8_t* state0, const uint8_t* codes0,
+                                                       size_t stride, int C, const float* table, float* obs) {
+    struct StateLDS {
+        float x[MAXN], y[MAXN], v[MAXN], h[MAXN];
+        int32_t intent[MAXN];
+        uint8_t alive[MAXN];
+    };
+    __shared__ StateLDS el;
+    const int lane = threadIdx.x;
+    const int g = blockIdx.x, r = g / C, c = g - r * C;
+    const int N = p.N, D = p.D, L = p.lidar_slots;
+    const size_t n = (size_t)C * N;
+    const uint8_t* sb = state0 + (size_t)r * stride;
+    const uint8_t* cb = codes0 + (size_t)r * stride;
+    int route = 0, pidx = 0;
+    if (lane < N) {
+        const size_t a = (size_t)c * N + lane;
+        el.x[lane] = reinterpret_cast<const float*>(sb)[a];
+        el.y[lane] = reinterpret_cast<const float*>(sb + 4 * n)[a];
+        el.v[lane] = reinterpret_cast<const float*>(sb + 8 * n)[a];
+        el.h[lane] = reinterpret_cast<const float*>(sb + 12 * n)[a];
+        route = reinterpret_cast<const int16_t*>(sb + 16 * n)[a];
+        pidx = reinterpret_cast<const int16_t*>(sb + 18 * n)[a];
+        el.intent[lane] = sb[20 * n + a];
+        el.alive[lane] = sb[21 * n + a];
+    }
+    __syncthreads();
+    for (int i = lane; i < N; i += WAVE) {
+        float* row = obs + ((size_t)g * N + i) * D;
+        if (!el.alive[i]) {
+            for (int q = 0; q < OBS_HEAD; ++q) row[q] = 0.0f;
+            continue;
+        }
+        const int rt = route < 0 ? 0 : (route >= p.rt.nroutes ? p.rt.nroutes - 1 : route);
+        const int ti = pidx + 10 < PATH_LEN - 1 ? (pidx + 10 < 0 ? 0 : pidx + 10) : PATH_LEN - 1;
+        const float* path = p.rt.path + (size_t)rt * (2 * PATH_LEN);
+        write_obs_head_tg<false>(p, i, el, (const NpcLDS*)nullptr, 0, path[2 * ti], path[2 * ti + 1], row, false);
+    }
+    // LiDAR block and padding, every lane: (agent, column) pairs
+    const int tail = D - OBS_HEAD;
+    for (int t = lane; t < N * tail; t += WAVE) {
+        const int i = t / tail, b = t - i * tail;
+        const size_t a = (size_t)c * N + i;
+        obs[((size_t)g * N + i) * D + OBS_HEAD + b] = b < L ? table[cb[a * L + b]] : 0.0f;
+    }
+}
+
+hipError_t launch_decode_state(const SimParams& p, const uint8_t* state0, const uint8_t* codes0, size_t stride, int C,
+                               int n_env, const float* table, float* obs, hipStream_t s) {
+    if (n_env <= 0) return hipSuccess;
+    if (p.traffic || p.N > MAXN) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_decode_state, dim3((unsigned)n_env), dim3(WAVE), 0, s, p, state0, codes0, stride, C, table,
+                       obs);
     return hipGetLastError();
 }
 

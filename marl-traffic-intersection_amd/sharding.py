@@ -45,21 +45,32 @@ class PackedOutputs:
     fmt = MEV_GATHER_LIDAR_U8 (the compact format): the message holds each row's
     31-float head and one u8 code per LiDAR beam; unpack() rebuilds the float
     rows through the library's decode table (`table`, Handle.lidar_decode_table()),
-    bit-identical to the plain step's."""
+    bit-identical to the plain step's.
+
+    fmt = MEV_GATHER_STATE: the message holds each agent's post-step state (22 B)
+    and the LiDAR codes, no observation head; the rows are rebuilt on the device by
+    the library (`handle`: a Handle with a communicator of this layout,
+    mev_unpack_gathered), so unpack() takes torch device buffers only."""
 
     FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated")
 
-    def __init__(self, slots: int, agents: int, obs_dim: int, fmt: int = 0, lidar_slots: int = 0, table=None):
+    def __init__(self, slots: int, agents: int, obs_dim: int, fmt: int = 0, lidar_slots: int = 0, table=None,
+                 handle=None):
         from . import _capi
 
         self.C, self.N, self.D = int(slots), int(agents), int(obs_dim)
         self.fmt, self.L = int(fmt), int(lidar_slots)
         if self.fmt == _capi.MEV_GATHER_LIDAR_U8 and table is None:
             raise ValueError("the compact gather format needs the decode table (Handle.lidar_decode_table())")
+        if self.fmt == _capi.MEV_GATHER_STATE and handle is None:
+            raise ValueError("the state gather format is decoded by the library: pass the root's Handle")
         self.table = table
+        self.handle = handle
         self.offsets, self.nbytes = _capi.packed_layout(self.C, self.N, self.D, self.fmt, self.L)
         self.offsets: Dict[str, int]
-        self.used = self.offsets["lidar"] + (self.C * self.N * self.L if self.fmt else 0)
+        self.used = (self.offsets["state"] + self.C * self.N * _capi.STATE_BYTES_PER_AGENT
+                     if self.fmt == _capi.MEV_GATHER_STATE else
+                     self.offsets["lidar"] + (self.C * self.N * self.L if self.fmt else 0))
 
     def pointers(self, base: int) -> Dict[str, int]:
         """Field pointers (for mev_step's output arguments) inside a buffer at `base`."""
@@ -69,6 +80,8 @@ class PackedOutputs:
         C, N, D = self.C, self.N, self.D
         sh = {"obs": ((C, N, 31 if self.fmt else D), 4), "reward": ((C, N), 4), "done": ((C, N), 1),
               "status": ((C, N), 1), "terminated": ((C,), 1), "truncated": ((C,), 1)}
+        if self.fmt == 2:  # MEV_GATHER_STATE: no observation field
+            del sh["obs"]
         if self.fmt:
             sh["lidar"] = ((C, N, self.L), 1)
         return sh
@@ -92,7 +105,17 @@ class PackedOutputs:
                 import numpy as np
                 a = raw.view(np.float32) if isz == 4 else raw
                 out[name] = a.reshape(shape)
-        if self.fmt:
+        if self.fmt == 2:  # MEV_GATHER_STATE: the library rebuilds the rows on the device
+            import torch
+            if not is_torch or not buf.is_cuda:
+                raise ValueError("the state gather format decodes device buffers (torch) only")
+            out.pop("lidar")
+            obs = torch.empty((self.C, self.N, self.D), dtype=torch.float32, device=buf.device)
+            torch.cuda.current_stream(buf.device).synchronize()  # buf (and obs) ready for the handle's stream
+            self.handle.unpack_gathered(buf.data_ptr(), 1, obs.data_ptr())
+            self.handle.sync()
+            out["obs"] = obs
+        elif self.fmt:
             head, codes = out["obs"], out.pop("lidar")
             C, N, D, L = self.C, self.N, self.D, self.L
             if is_torch:

@@ -21,7 +21,7 @@ E, N, RAYS, G, T, MAXS = 32768, 8, 128, 8, 50, 2000
 FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated")
 
 
-@pytest.mark.parametrize("fmt", [0, 1], ids=["f32", "lidar_u8"])
+@pytest.mark.parametrize("fmt", [0, 1, 2], ids=["f32", "lidar_u8", "state"])
 def test_cfg5_shards_reassembled_from_packed_rows_equal_one_handle(mev, fmt):
     import torch
     import torch.utils.dlpack as tdl
@@ -50,11 +50,12 @@ def test_cfg5_shards_reassembled_from_packed_rows_equal_one_handle(mev, fmt):
         h.set_stream(stream.cuda_stream)
         h.set_state({k: v[s0:s0 + cnt] for k, v in st.items()})
         if fmt:
-            h.set_gather_format(_capi.MEV_GATHER_LIDAR_U8)
+            h.set_gather_format(fmt)
         h.comm_init(_capi.comm_unique_id(), world=1, rank=0, root=0, slots=cnt)
         shards.append((s0, cnt, h))
     lay = sharding.PackedOutputs(E // G, N, D, fmt=fmt, lidar_slots=big.lidar_slots(),
-                                 table=shards[0][2].lidar_decode_table() if fmt else None)
+                                 table=shards[0][2].lidar_decode_table() if fmt == 1 else None,
+                                 handle=shards[0][2] if fmt == 2 else None)
     out = {k: torch.zeros_like(torch.as_tensor(v), device="cuda:0") for k, v in big.alloc_outputs().items()}
     extra = [{"agents_alive": torch.zeros(cnt, dtype=torch.int32, device="cuda:0"),
               "step": torch.zeros(cnt, dtype=torch.int32, device="cuda:0")} for _, cnt, _ in shards]

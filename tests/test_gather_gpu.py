@@ -29,10 +29,12 @@ def _bits(a):
     return a.view(np.uint32) if a.dtype == np.float32 else a
 
 
-@pytest.mark.parametrize("fmt", [0, 1], ids=["f32", "lidar_u8"])
+@pytest.mark.parametrize("fmt", [0, 1, 2], ids=["f32", "lidar_u8", "state"])
 def test_gather_world1_row_equals_plain_step(mev, fmt):
     """fmt 1: the compact format (heads + one u8 code per beam), decoded through the
-    library's table -- bit-identical to the plain rows, dead agents included."""
+    library's table -- bit-identical to the plain rows, dead agents included.  fmt 2:
+    the state format (post-step state + codes; the ranks write no heads), the rows
+    rebuilt on the device by mev_unpack_gathered -- bit-identical too."""
     import torch
     import torch.utils.dlpack as tdl
     from marl_traffic_intersection_amd import _capi, sharding
@@ -44,12 +46,13 @@ def test_gather_world1_row_equals_plain_step(mev, fmt):
     gat = mev.Handle(**cfg)
     try:
         if fmt:
-            gat.set_gather_format(_capi.MEV_GATHER_LIDAR_U8)
+            gat.set_gather_format(fmt)
         gat.comm_init(_capi.comm_unique_id(), world=1, rank=0, root=0, slots=E + 3)
         lay = sharding.PackedOutputs(E + 3, N, plain.D, fmt=fmt, lidar_slots=gat.lidar_slots(),
-                                     table=gat.lidar_decode_table() if fmt else None)
+                                     table=gat.lidar_decode_table() if fmt == 1 else None,
+                                     handle=gat if fmt == 2 else None)
         if fmt:
-            assert lay.nbytes < 0.6 * sharding.PackedOutputs(E + 3, N, plain.D).nbytes
+            assert lay.nbytes < (0.6 if fmt == 1 else 0.3) * sharding.PackedOutputs(E + 3, N, plain.D).nbytes
         rng = np.random.default_rng(5)
         for t in range(T):
             act = rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)
@@ -59,12 +62,15 @@ def test_gather_world1_row_equals_plain_step(mev, fmt):
             gat.gather_wait(30000)
             ptr, nbytes, world = gat.gather_result()
             assert world == 1 and nbytes == lay.nbytes and ptr
-            buf = tdl.from_dlpack(gat.output_dlpack("gathered")).cpu().numpy()
-            assert buf.shape == (1, lay.nbytes)
-            got = lay.unpack(buf[0])
+            dbuf = tdl.from_dlpack(gat.output_dlpack("gathered"))
+            assert tuple(dbuf.shape) == (1, lay.nbytes)
+            if fmt == 2:  # decoded on the device by the library
+                got = {k: v.cpu().numpy() for k, v in lay.unpack(dbuf[0]).items()}
+            else:
+                got = lay.unpack(dbuf.cpu().numpy()[0])
             for k in FIELDS:
                 assert np.array_equal(_bits(got[k][:E]), _bits(ref[k])), (t, k)
-                tail = got[k][E:, :, :31] if (fmt and k == "obs") else got[k][E:]
+                tail = got[k][E:, :, :31] if (fmt == 1 and k == "obs") else got[k][E:]
                 assert not np.any(tail), (t, k)  # unused slots stay zero
             assert np.array_equal(extra["agents_alive"], ref["agents_alive"])
             assert np.array_equal(extra["step"], ref["step"])

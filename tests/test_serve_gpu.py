@@ -141,12 +141,56 @@ def test_torch_work_runs_beside_a_resident_server(mev):
         (x * 2).sum().item()  # torch's stream, synchronised every call, while the server stays resident
     dt = (time.perf_counter() - t0) / 50
     assert dt < 0.005, dt  # nothing waits for the server's idle exit
-    assert a.serve_stats()["launches"] == n0  # it stayed resident throughout
+    # it stayed resident (a rare host hiccup longer than the adaptive idle limit
+    # only costs a relaunch)
+    assert a.serve_stats()["launches"] - n0 <= 3
     a.set_stream(torch.cuda.current_stream().cuda_stream)  # a shared stream: launched steps only
     a.step(act)
     assert not a.serve_stats()["running"]
     assert a.serve_stats()["steps"] == 52
     a.close()
+
+
+def test_device_wide_sync_between_served_steps():
+    """An RL loop that calls torch.cuda.synchronize() (a device-wide wait, which also
+    waits for a resident server's idle exit) between env.py steps: the adaptive idle
+    limit (<= 2 ms, then launched steps after repeated idle exits) keeps each step
+    well under 2 ms; without the synchronisation the same env is served."""
+    import torch
+
+    import pkgload
+    pkgload.load()
+    from marl_traffic_intersection_amd import env as envmod
+    env = envmod.IntersectionEnv({"num_agents": 1})
+    act = np.zeros((1, 2), np.float32)
+    x = torch.ones(1024, device="cuda")
+    (x * 2).sum().item()
+    for _ in range(20):
+        env.step(act)
+    h = env.env._sync()
+    s0 = h.serve_stats()
+    t0 = time.perf_counter()
+    n = 300
+    for _ in range(n):
+        env.step(act)
+        torch.cuda.synchronize()
+    per_step = (time.perf_counter() - t0) / n
+    assert per_step < 0.002, per_step
+    s1 = h.serve_stats()
+    # (most of these steps ran launched: the server kept leaving before the next post)
+    assert s1["steps"] - s0["steps"] < n
+    # without device-wide waits, served again once the pause is over
+    for _ in range(1100):
+        env.step(act)
+    s2 = h.serve_stats()
+    t0 = time.perf_counter()
+    for _ in range(200):
+        env.step(act)
+    served_dt = (time.perf_counter() - t0) / 200
+    s3 = h.serve_stats()
+    assert s3["steps"] - s2["steps"] >= 190, (s2, s3)
+    assert served_dt < 0.001, served_dt
+    env.close()
 
 
 @pytest.mark.parametrize("traffic", [False, True], ids=["egos", "traffic"])
@@ -193,16 +237,20 @@ def test_several_served_handles_at_once(mev):
     for h in served + launched:
         h.reset()
     rng = np.random.default_rng(9)
-    t0 = time.perf_counter()
-    for t in range(100):
+    s0 = None
+    for t in range(110):
+        if t == 10:  # (after the first rounds: kernel code loading may outlast an idle limit)
+            t0 = time.perf_counter()
+            s0 = [h.serve_stats()["steps"] for h in served]
         for i in range(4):
             act = rng.uniform(-1, 1, (1, 2, 2)).astype(np.float32)
             _same(served[i].step(act, auto_reset=True), launched[i].step(act, auto_reset=True), (t, i))
     # nothing waits for a server's idle exit: each server has a hardware queue of its own
-    # (sharing one, each launched step would wait ~20 ms behind a resident server)
+    # (sharing one, each launched step would wait for the idle exit behind a resident server)
     assert time.perf_counter() - t0 < 2.0
-    st = [h.serve_stats() for h in served]
-    assert [x["steps"] for x in st] == [100, 100, 0, 0], st  # two resident servers per process at most
+    d = [h.serve_stats()["steps"] - a for h, a in zip(served, s0)]
+    # two resident servers per process at most: two handles served (almost) throughout
+    assert sorted(d)[-2:] >= [95, 95] and sum(sorted(d)[:-2]) <= 10, d
     for h in served + launched:
         h.close()
 
@@ -217,14 +265,18 @@ def test_resident_servers_are_capped(mev):
     for h in hs + twins:
         h.reset()
     rng = np.random.default_rng(4)
-    t0 = time.perf_counter()
-    for t in range(100):
+    s0 = None
+    for t in range(110):
+        if t == 10:  # (after the first rounds: kernel code loading may outlast an idle limit)
+            t0 = time.perf_counter()
+            s0 = [h.serve_stats()["steps"] for h in hs]
         for i in range(6):
             act = rng.uniform(-1, 1, (1, 1, 2)).astype(np.float32)
             _same(hs[i].step(act, auto_reset=True), twins[i].step(act, auto_reset=True), (t, i))
     assert time.perf_counter() - t0 < 2.0
-    served = [h.serve_stats()["steps"] for h in hs]
-    assert sum(s > 0 for s in served) == 2, served  # kMaxResidentServers
+    d = [h.serve_stats()["steps"] - a for h, a in zip(hs, s0)]
+    # kMaxResidentServers: two handles served (almost) throughout, the others launched
+    assert sorted(d)[-2:] >= [95, 95] and sum(sorted(d)[:-2]) <= 10, d
     for h in hs + twins:
         h.close()
 

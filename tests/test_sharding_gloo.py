@@ -150,3 +150,20 @@ def test_packed_layout_is_the_library_layout():
         assert total % 256 == 0 and prev_end <= total < prev_end + 256
         lay = sharding.PackedOutputs(C, Nn, Dd)
         assert lay.offsets == off and lay.nbytes == total
+
+
+def test_state_gather_layout():
+    """MEV_GATHER_STATE: no observation field, one LiDAR code per beam and 22 B of post-step
+    state per agent (x, y, v, heading f32 | route, path index i16 | intention, alive u8); at
+    config 3 (4096 envs x 8 agents x 64 beams) the message fits the 8-GPU root-ingress budget
+    (<= 5.3 MB per rank per step at a 34.7 us step)."""
+    from marl_traffic_intersection_amd import _capi
+    C, Nn, Dd, L = 4096, 8, 95, 64
+    off, total = _capi.packed_layout(C, Nn, Dd, _capi.MEV_GATHER_STATE, L)
+    assert off["reward"] == off["obs"] == 0  # the observation field is empty
+    assert off["state"] >= off["lidar"] + C * Nn * L
+    assert total >= off["state"] + C * Nn * _capi.STATE_BYTES_PER_AGENT
+    assert total < 5.3e6 and total == 32768 * 92 + 2 * 4096, total  # 3.02 MB
+    u8 = _capi.packed_layout(C, Nn, Dd, _capi.MEV_GATHER_LIDAR_U8, L)[1]
+    f32 = _capi.packed_layout(C, Nn, Dd)[1]
+    assert total < 0.5 * u8 and total < 0.25 * f32
