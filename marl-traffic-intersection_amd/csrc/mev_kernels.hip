@@ -1657,6 +1657,14 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             }
         }
     }
+    // The LDS DMA of round B has landed (the loop waited for it before reading the
+    // window), but the compiler cannot see that on every path into here, and with an
+    // LDS DMA possibly pending it puts an s_waitcnt vmcnt(0) in front of every later
+    // LDS access -- which then also waits for every global store issued before it
+    // (cars_post's outputs and state write-back in front of the LiDAR's first LDS
+    // access).  An explicit wait here (nothing else is in flight) retires the DMA for
+    // the compiler too.
+    if constexpr (early) __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
     wave_lds_sync();
 
     STAMP(2);
@@ -3287,7 +3295,8 @@ __global__ __launch_bounds__(WAVE) void k_decode_state(SimParams p, const uint8_
     for (int t = lane; t < N * tail; t += WAVE) {
         const int i = t / tail, b = t - i * tail;
         const size_t a = (size_t)c * N + i;
-        obs[((size_t)g * N + i) * D + OBS_HEAD + b] = b < L ? table[cb[a * L + b]] : 0.0f;
+        // (a dead agent's codes decode to 0 anyway; an unused slot's zeroed message has alive 0)
+        obs[((size_t)g * N + i) * D + OBS_HEAD + b] = (b < L && el.alive[i]) ? table[cb[a * L + b]] : 0.0f;
     }
 }
 
