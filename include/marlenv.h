@@ -150,6 +150,15 @@ int mev_route_id(const mev_handle* h, int32_t start_point, int32_t end_point, in
 /* path [160][2], intent, spawn (x, y, heading) of a route */
 int mev_route_info(const mev_handle* h, int32_t route, float* path, int32_t* intent, float* spawn);
 int mev_path_len(void);
+/* A route of the caller's own: path [160][2] (the length of every path the
+ * reference generates, RouteGen.cpp:111-205) and intent (0 straight, 1 left,
+ * 2 right) appended to the handle's route table; *route receives its id (>=
+ * P*P, the lane-layout routes).  Cars and NPCs then take it like any route
+ * (mev_set_ego_routes, mev_set_state); a reset spawns at path[0] heading to
+ * path[1].  Replaces assigning Car.path in the reference (cpp/bindings.cpp:29,
+ * a read-write std::vector member); paths of another length are not
+ * supported. */
+int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* route);
 /* Ego routes for every (env, agent): route ids [E][N] (reference env.py:104-106,148-151). */
 int mev_set_ego_routes(mev_handle* h, const int32_t* routes);
 /* NPC route list (reference configure_routes / init_traffic_routes, TrafficFlow.cpp:198-238). */

@@ -47,7 +47,7 @@ EXPORTED = (
     "mev_set_step_split", "mev_get_step_split", "mev_set_env_deal", "mev_set_serve", "mev_serve_stats",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
     "mev_gather_wait", "mev_output_dlpack", "mev_packed_layout2", "mev_set_gather_format", "mev_lidar_decode_table",
-    "mev_unpack_gathered",
+    "mev_unpack_gathered", "mev_add_route",
 )
 
 
@@ -174,6 +174,7 @@ def load_library(variant: str = None):
     L.mev_gather_result.argtypes = [_vp, ctypes.POINTER(_vp), u64p, i32p]
     L.mev_gather_wait.argtypes = [_vp, ctypes.c_int32]
     L.mev_unpack_gathered.argtypes = [_vp, _vp, ctypes.c_int32, _vp]
+    L.mev_add_route.argtypes = [_vp, f32p, ctypes.c_int32, i32p]
     L.mev_output_dlpack.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(_vp)]
     _libs[variant] = L
     return L
@@ -372,6 +373,17 @@ class Handle:
         _check(self._lib.mev_route_info(self._h, int(route), path.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
                                         ctypes.byref(intent), spawn.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
         return path, intent.value, spawn
+
+    def add_route(self, path, intent: int) -> int:
+        """Append a route of the caller's own (path [160, 2] f32, intent 0 straight / 1 left / 2 right) to
+        the route table (mev_add_route); returns its id."""
+        a = np.ascontiguousarray(path, np.float32)
+        if a.shape != (PATH_LEN, 2):
+            raise ValueError(f"a route path has {PATH_LEN} points (x, y), got shape {a.shape}")
+        r = ctypes.c_int32()
+        _check(self._lib.mev_add_route(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), int(intent),
+                                       ctypes.byref(r)))
+        return r.value
 
     def point_xy(self, point: int):
         xy = np.zeros(2, np.float32)

@@ -13,6 +13,10 @@ Deviations from MARLEnv (all outside the hot path):
    inside step, on an unknown end lane; an unknown start lane never spawns);
  * all cars share one LiDAR configuration (MARLEnv keeps one Lidar per car);
    assigning `lidars` reconfigures every car;
+ * Car.path may be any 160-point path (every path MARLEnv itself generates has
+   160 points, RouteGen.cpp:111-205); a path that is not a lane-layout route is
+   appended to the device route table (mev_add_route); other lengths raise
+   ValueError;
  * Car.length / Car.width are honoured by Car.check_collision but the
    environment simulates the reference's fixed 54 x 24 px cars;
  * observations after set_state() / mid-episode add_car_with_route() carry a
@@ -172,6 +176,8 @@ class IntersectionEnv:
         self._device = int(device)
         self._max_npcs = int(max_npcs)
         self._paths = {}  # route id -> its 160 path points as (x, y) tuples (Car.path)
+        self._route_ids = None  # path bytes (f32 [160, 2]) -> route id, built on first use
+        self._custom: List[Tuple[np.ndarray, int]] = []  # Car.path routes of the caller's own, in id order
         self._use_team, self._respawn, self._max_steps = False, True, 2000
         self._traffic, self._density = False, 0.5
         self._reward = RewardConfig()
@@ -242,12 +248,15 @@ class IntersectionEnv:
         self._next_id += 1
 
     def _create(self, n: int, lidar):
-        return _capi.Handle(num_envs=1, num_agents=n, num_lanes=self.num_lanes, lidar_rays=lidar[0],
-                            lidar_fov_deg=lidar[1], lidar_max_dist=lidar[2], lidar_step=lidar[3], obs_dim=OBS_W,
-                            traffic_flow=int(self._traffic), traffic_density=self._density,
-                            use_team_reward=int(self._use_team), respawn_enabled=int(self._respawn),
-                            max_steps=self._max_steps, reward=self._reward.as_list(),
-                            max_npcs=self._max_npcs, device=self._device)
+        h = _capi.Handle(num_envs=1, num_agents=n, num_lanes=self.num_lanes, lidar_rays=lidar[0],
+                         lidar_fov_deg=lidar[1], lidar_max_dist=lidar[2], lidar_step=lidar[3], obs_dim=OBS_W,
+                         traffic_flow=int(self._traffic), traffic_density=self._density,
+                         use_team_reward=int(self._use_team), respawn_enabled=int(self._respawn),
+                         max_steps=self._max_steps, reward=self._reward.as_list(),
+                         max_npcs=self._max_npcs, device=self._device)
+        for path, intent in self._custom:  # the caller's own routes keep their ids on a new handle
+            h.add_route(path, intent)
+        return h
 
     def _sync(self) -> Optional[_capi.Handle]:
         n = len(self._routes)
@@ -448,34 +457,74 @@ class IntersectionEnv:
         return s
 
     def _route_of(self, c: Car) -> int:
-        if c._route >= 0:
-            return c._route
-        if len(c.path) >= 2:
-            want = np.asarray(c.path, np.float32)
+        """The route id of Car.path (read-write in MARLEnv, cpp/bindings.cpp:29): a lane-layout route or one
+        registered before, else a new route of the caller's own (mev_add_route; 160 points)."""
+        if len(c.path) == 0:
+            if c._route >= 0:
+                return c._route
+            raise ValueError("Car.path is empty")
+        want = np.asarray(c.path, np.float32).reshape(-1, 2)
+        if self._route_ids is None:
             P = 8 * self.num_lanes
-            for r in range(P * P):  # a path built from the lane layout: find its route
-                path = self._h.route_info(r)[0]
-                if path.shape == want.shape and np.array_equal(path, want):
-                    return r
-        raise ValueError("Car.path must be one of the lane-layout routes")
+            self._route_ids = {self._h.route_info(r)[0].tobytes(): r for r in range(P * P)}
+            for k, (path, _) in enumerate(self._custom):
+                self._route_ids[path.tobytes()] = P * P + k
+        r = self._route_ids.get(want.tobytes())
+        if r is not None:
+            return r
+        if want.shape != (_capi.PATH_LEN, 2):
+            raise ValueError(f"Car.path must have {_capi.PATH_LEN} points (every path the reference generates "
+                             f"does, RouteGen.cpp:111-205); got {len(want)}")
+        intent = min(max(int(c.intention), 0), 2)
+        r = self._h.add_route(want, intent)
+        self._custom.append((want.copy(), intent))
+        self._route_ids[want.tobytes()] = r
+        return r
 
     def set_state(self, s: EnvState):
         """cpp/IntersectionEnv.cpp:406-416; like the reference, the LiDAR objects
         are rebuilt with Lidar() defaults (72 rays) from here on."""
-        n = len(s.cars)
         self._agent_ids = list(s.agent_ids)
         self._next_id = int(s.next_agent_id)
+        self._apply_state(s, CTOR_LIDAR)
+
+    @cars.setter
+    def cars(self, cars: Sequence[Car]):
+        """IntersectionEnv.cars is read-write (cpp/bindings.cpp:66): the ego vector is replaced as given
+        (state, path, hidden fields); the LiDAR configuration, agent ids, NPCs and step count stay."""
+        s = self.get_state()
+        s.cars = list(cars)
+        n = len(s.cars)
+        ids = list(self._agent_ids[:n])
+        while len(ids) < n:  # (MARLEnv leaves agent_ids as they were; they index the egos here)
+            ids.append(self._next_id)
+            self._next_id += 1
+        self._agent_ids = ids
+        self._apply_state(s, self._lidar)
+
+    @traffic_cars.setter
+    def traffic_cars(self, cars: Sequence[Car]):
+        """IntersectionEnv.traffic_cars is read-write (cpp/bindings.cpp:67): the NPC vector is replaced."""
+        s = self.get_state()
+        s.traffic_cars = list(cars)
+        if self._routes:
+            self._apply_state(s, self._lidar)
+        elif s.traffic_cars:
+            raise ValueError("traffic cars need at least one ego car in this backend")
+
+    def _apply_state(self, s: EnvState, lidar):
+        n = len(s.cars)
         if n == 0:
             self._routes = []
             return
-        if self._h is None or self._h.N != n or self._h_lidar != CTOR_LIDAR:
+        if self._h is None or self._h.N != n or self._h_lidar != lidar:
             if self._h is not None:
                 self._h.close()
-            self._h = self._create(n, CTOR_LIDAR)
-            self._h_lidar = CTOR_LIDAR
+            self._h = self._create(n, lidar)
+            self._h_lidar = lidar
         routes = [self._route_of(c) for c in s.cars]
         self._routes = routes
-        self._lidar = CTOR_LIDAR
+        self._lidar = lidar
         if self._traffic_routes is not None:
             self._h.set_traffic_routes(self._traffic_routes)
         self._h.set_ego_routes(np.asarray(routes, np.int32)[None])

@@ -618,6 +618,69 @@ int mev_route_info(const mev_handle* h, int32_t route, float* path, int32_t* int
     return MEV_OK;
 }
 
+int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* route) {
+    if (!h || !path || !route) return fail(MEV_E_INVALID, "null argument");
+    if (intent < 0 || intent > 2) return fail(MEV_E_INVALID, "intent must be 0 (straight), 1 (left) or 2 (right)");
+    for (int i = 0; i < 2 * mev::PATH_LEN; ++i)
+        if (!(fabsf(path[i]) < 1.0e6f)) return fail(MEV_E_INVALID, "path points must be finite (|coordinate| < 1e6)");
+    if (h->nroutes >= 32767) return fail(MEV_E_INVALID, "too many routes (the state gather format ships i16 ids)");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    const int r = h->nroutes;
+    h->h_paths.insert(h->h_paths.end(), path, path + 2 * mev::PATH_LEN);
+    h->h_intent.push_back(intent);
+    h->h_spawn.push_back(path[0]);  // add_car_with_route's spawn: the path's first point (RouteGen.cpp:111-205)
+    h->h_spawn.push_back(path[1]);
+    h->h_spawn.push_back(mev::spawn_heading(path));
+    {
+        const int cut[4] = {0, 50, 110, mev::PATH_LEN};
+        for (int q = 0; q < 3; ++q) {
+            float x0 = path[2 * cut[q]], x1 = x0, y0 = path[2 * cut[q] + 1], y1 = y0;
+            for (int i = cut[q]; i < cut[q + 1]; ++i) {
+                x0 = std::min(x0, path[2 * i]); x1 = std::max(x1, path[2 * i]);
+                y0 = std::min(y0, path[2 * i + 1]); y1 = std::max(y1, path[2 * i + 1]);
+            }
+            h->h_pbox.push_back(x0); h->h_pbox.push_back(x1); h->h_pbox.push_back(y0); h->h_pbox.push_back(y1);
+        }
+    }
+    // the four route tables, reallocated one route larger and uploaded whole
+    hipError_t e = hipSuccess;
+    void* np[4] = {nullptr, nullptr, nullptr, nullptr};
+    const size_t bytes[4] = {h->h_paths.size() * sizeof(float), h->h_intent.size() * sizeof(int32_t),
+                             h->h_spawn.size() * sizeof(float), h->h_pbox.size() * sizeof(float)};
+    const void* src[4] = {h->h_paths.data(), h->h_intent.data(), h->h_spawn.data(), h->h_pbox.data()};
+    for (int k = 0; k < 4 && e == hipSuccess; ++k) {
+        e = hipMalloc(&np[k], bytes[k]);
+        if (e == hipSuccess) e = hipMemcpy(np[k], src[k], bytes[k], hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+        for (void* q : np) if (q) (void)hipFree(q);
+        h->h_paths.resize(h->h_paths.size() - 2 * mev::PATH_LEN);
+        h->h_intent.pop_back();
+        h->h_spawn.resize(h->h_spawn.size() - 3);
+        h->h_pbox.resize(h->h_pbox.size() - 12);
+        return fail(MEV_E_NOMEM, std::string("route table: ") + hipGetErrorString(e));
+    }
+    void* old[4] = {h->d_paths, h->d_intent, h->d_spawn_tab, h->d_pbox};
+    for (int k = 0; k < 4; ++k) {
+        for (auto& a : h->allocs)
+            if (a == old[k]) { (void)hipFree(a); a = np[k]; break; }
+    }
+    h->d_paths = static_cast<float*>(np[0]);
+    h->d_intent = static_cast<int32_t*>(np[1]);
+    h->d_spawn_tab = static_cast<float*>(np[2]);
+    h->d_pbox = static_cast<float*>(np[3]);
+    h->nroutes = r + 1;
+    h->sp.rt.path = h->d_paths;
+    h->sp.rt.intent = h->d_intent;
+    h->sp.rt.spawn = h->d_spawn_tab;
+    h->sp.rt.pbox = reinterpret_cast<const float4*>(h->d_pbox);
+    h->sp.rt.nroutes = h->nroutes;  // (the next launch refreshes the device copy of the parameters)
+    *route = r;
+    return MEV_OK;
+}
+
 int mev_set_ego_routes(mev_handle* h, const int32_t* routes) {
     if (!h || !routes) return fail(MEV_E_INVALID, "null argument");
     const size_t EN = size_t(h->cfg.num_envs) * size_t(h->cfg.num_agents);
@@ -632,7 +695,7 @@ int mev_set_ego_routes(mev_handle* h, const int32_t* routes) {
 
 int mev_set_traffic_routes(mev_handle* h, const int32_t* routes, int32_t count) {
     if (!h || (count > 0 && !routes)) return fail(MEV_E_INVALID, "null argument");
-    if (count < 0 || count > h->nroutes) return fail(MEV_E_INVALID, "bad traffic route count");
+    if (count < 0 || count > h->P * h->P) return fail(MEV_E_INVALID, "bad traffic route count");
     for (int i = 0; i < count; ++i)
         if (routes[i] < 0 || routes[i] >= h->nroutes) return fail(MEV_E_RANGE, "traffic route id out of range");
     HIP_TRY(hipSetDevice(h->cfg.device));
@@ -1375,7 +1438,8 @@ int mev_get_step_split(const mev_handle* h, int32_t* split) {
 
 int mev_set_reset_routes(mev_handle* h, const int32_t* routes, int32_t count) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
-    if (count < 0 || count > h->nroutes) return fail(MEV_E_INVALID, "count must be in [0, number of routes]");
+    if (count < 0 || count > h->P * h->P)
+        return fail(MEV_E_INVALID, "count must be in [0, number of lane-layout routes]");
     if (count > 0 && !routes) return fail(MEV_E_INVALID, "null routes");
     for (int32_t i = 0; i < count; ++i)
         if (routes[i] < 0 || routes[i] >= h->nroutes) return fail(MEV_E_RANGE, "route id out of range");

@@ -58,8 +58,9 @@ typedef struct orc_env {
     float rc[8];
     int P;               /* 8 * lanes lane points */
     lane_pt* pts;
-    float* paths;        /* [P*P][160][2] */
-    int* intent;         /* [P*P] */
+    float* paths;        /* [nroutes][160][2]: the P*P lane-layout routes, then orc_add_route's */
+    int* intent;         /* [nroutes] */
+    int nroutes;
     float* rel;          /* [rays] */
     uint8_t* line_grid;  /* [750*750] LineMask */
     int* troutes;        /* traffic route ids */
@@ -477,8 +478,9 @@ static void plan_npc(const orc_env* e, int k, float* thr_out, float* st_out) {
 static void spawn_npc(orc_env* e, int troute) {
     if (troute < 0 || troute >= e->ntr) return;
     int rid = e->troutes[troute];
-    int s = rid / e->P;
-    float sx = e->pts[s].x, sy = e->pts[s].y;
+    const float* p = e->paths + (size_t)rid * 2 * PATH_LEN;
+    /* the route's start lane point; a route of the caller's own (orc_add_route) starts at its first point */
+    float sx = rid < e->P * e->P ? e->pts[rid / e->P].x : p[0], sy = rid < e->P * e->P ? e->pts[rid / e->P].y : p[1];
     const float md = CAR_LENGTH * 2.5f, md2 = md * md;
     for (int i = 0; i < e->n; ++i) {
         float dx = e->ego[i].x - sx, dy = e->ego[i].y - sy;
@@ -489,7 +491,6 @@ static void spawn_npc(orc_env* e, int troute) {
         if (dx * dx + dy * dy < md2) return;
     }
     if (e->nnpc >= e->max_npcs) return;
-    const float* p = e->paths + (size_t)rid * 2 * PATH_LEN;
     orc_car c;
     memset(&c, 0, sizeof(c));
     c.x = sx; c.y = sy; c.v = 0.0f;
@@ -599,6 +600,7 @@ orc_env* orc_create(int lanes, int n, int rays, float fov, float maxd, float ste
     e->traffic = traffic; e->density = density < 0.0f ? 0.0f : density; e->max_npcs = max_npcs;
     memcpy(e->rc, rc, sizeof(e->rc));
     build_points(e);
+    e->nroutes = e->P * e->P;
     e->paths = (float*)calloc((size_t)e->P * e->P * 2 * PATH_LEN, sizeof(float));
     e->intent = (int*)calloc((size_t)e->P * e->P, sizeof(int));
     for (int s = 0; s < e->P; ++s)
@@ -635,6 +637,21 @@ int orc_num_points(const orc_env* e) { return e->P; }
 void orc_route_path(const orc_env* e, int r, float* out, int* intent) {
     memcpy(out, e->paths + (size_t)r * 2 * PATH_LEN, sizeof(float) * 2 * PATH_LEN);
     *intent = e->intent[r];
+}
+
+/* A route of the caller's own (the reference's Car.path is a plain read-write
+ * vector, cpp/Car.h:26, cpp/bindings.cpp:29; every function above reads a car's
+ * path through path_of): appended to the table, returns its id. */
+int orc_add_route(orc_env* e, const float* path, int intent) {
+    float* np = (float*)realloc(e->paths, (size_t)(e->nroutes + 1) * 2 * PATH_LEN * sizeof(float));
+    if (!np) return -1;
+    e->paths = np;
+    int* ni = (int*)realloc(e->intent, (size_t)(e->nroutes + 1) * sizeof(int));
+    if (!ni) return -1;
+    e->intent = ni;
+    memcpy(e->paths + (size_t)e->nroutes * 2 * PATH_LEN, path, sizeof(float) * 2 * PATH_LEN);
+    e->intent[e->nroutes] = intent;
+    return e->nroutes++;
 }
 
 void orc_set_traffic_routes(orc_env* e, const int* ids, int m) {

@@ -48,6 +48,7 @@ def lib():
         L.orc_num_points.argtypes = [vp]
         L.orc_route_path.argtypes = [vp, i, vp, vp]
         L.orc_set_traffic_routes.argtypes = [vp, vp, i]
+        L.orc_add_route.argtypes = [vp, vp, i]
         L.orc_reset.argtypes = [vp, vp]
         L.orc_set_state.argtypes = [vp, vp, vp, i, i]
         L.orc_get_state.argtypes = [vp, vp, vp, vp, vp]
@@ -95,6 +96,13 @@ class OracleEnv:
         it = ctypes.c_int()
         lib().orc_route_path(self.h, int(r), out.ctypes.data, ctypes.addressof(it))
         return out, it.value
+
+    def add_route(self, path, intent):
+        a = np.ascontiguousarray(path, np.float32).reshape(160, 2)
+        r = lib().orc_add_route(self.h, a.ctypes.data, int(intent))
+        if r < 0:
+            raise MemoryError("orc_add_route")
+        return r
 
     def set_traffic_routes(self, ids):
         a = np.ascontiguousarray(ids, np.int32)

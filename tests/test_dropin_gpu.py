@@ -248,3 +248,48 @@ def test_cpp_backend_set_state_replays_reference(name):
         info = dict(agents_alive=res.agents_alive, step=res.step, status=res.status, done=res.done)
         _check_step(name, g, t, res.obs, res.rewards, res.terminated, res.truncated, info)
     env.close()
+
+
+def test_cpp_backend_cars_setter_and_written_path():
+    """IntersectionEnv.cars / traffic_cars are read-write and Car.path is a plain
+    read-write vector in the reference (cpp/bindings.cpp:29,66-67): writing the cars
+    back unchanged leaves the run bit-identical to an untouched twin; a bent
+    160-point path becomes a route of the env's own (mev_add_route), is read back
+    as written, survives get_state/set_state into a fresh env and steers the car
+    (its route-following features differ from the twin's from then on)."""
+    g = G.load("n12_r96_policy")
+    envs = [cpp_backend.IntersectionEnv(3) for _ in range(3)]
+    for env in envs:
+        env.reset()
+        for s, t in g["meta"]["ego_routes"][:3]:
+            env.add_car_with_route(s, t)
+        for t in range(10):
+            env.step(g["actions"][t, :3, 0], g["actions"][t, :3, 1])
+    same, bent, twin = envs
+    same.cars = same.cars  # written back unchanged
+    cars = bent.cars
+    p = np.asarray(cars[1].path, np.float64)
+    d = np.gradient(p, axis=0)
+    nrm = np.stack([-d[:, 1], d[:, 0]], 1) / np.maximum(np.hypot(d[:, 0], d[:, 1]), 1e-9)[:, None]
+    new_path = (p + nrm * (8.0 * np.sin(np.pi * np.arange(len(p)) / (len(p) - 1)))[:, None]).astype(np.float32)
+    cars[1].path = [tuple(map(float, q)) for q in new_path]
+    bent.cars = cars
+    assert G.bits_equal(np.asarray(bent.cars[1].path, np.float32), new_path)
+    assert bent.cars[0].path == twin.cars[0].path
+    differs = False
+    for t in range(10, 60):
+        a = g["actions"][t, :3]
+        r0, r1, r2 = (e.step(a[:, 0], a[:, 1]) for e in (same, bent, twin))
+        assert G.bits_equal(r0.obs, r2.obs) and G.bits_equal(r0.rewards, r2.rewards), t
+        differs |= not G.bits_equal(r1.obs[1], r2.obs[1])
+    assert differs
+    snap = bent.get_state()
+    other = cpp_backend.IntersectionEnv(3)
+    other.set_state(snap)
+    assert G.bits_equal(np.asarray(other.cars[1].path, np.float32), new_path)
+    with pytest.raises(ValueError):
+        c = other.cars
+        c[0].path = c[0].path[:100]
+        other.cars = c
+    for env in envs + [other]:
+        env.close()

@@ -32,19 +32,37 @@ CONFIGS = [
     # sequential fallback runs (npc_stats) and is checked here as well
     dict(name="traffic_dense", n=2, rays=32, traffic=True, density=5.0, spawn_p=0.6, npcs=24, npc_gap=30.0,
          expect_seq=True),
+    # routes of the caller's own (a written Car.path, cpp/bindings.cpp:29 -> mev_add_route) beside lane routes,
+    # for egos and NPCs (NPCs spawn on them too: their first point)
+    dict(name="custom_routes_n6", n=6, rays=64, custom=True),
+    dict(name="custom_routes_traffic", n=3, rays=48, traffic=True, density=1.0, spawn_p=0.3, npcs=8, custom=True),
 ]
 
 
-def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0):
+def custom_routes(h):
+    """Four 160-point routes that no lane pair generates: three lane routes bent sideways by up to 9 px
+    (a sine bump along the route's normal) and one straight diagonal across the whole intersection."""
+    out = []
+    for s, t, amp in ((1, 4, 9.0), (3, 12, -6.0), (7, 10, 5.0)):
+        path, intent, _ = h.route_info(h.route_id(s - 1, 12 + t - 1))
+        d = np.gradient(path.astype(np.float64), axis=0)
+        nrm = np.stack([-d[:, 1], d[:, 0]], 1) / np.maximum(np.hypot(d[:, 0], d[:, 1]), 1e-9)[:, None]
+        bump = amp * np.sin(np.pi * np.arange(160) / 159.0)
+        out.append(((path + nrm * bump[:, None]).astype(np.float32), int(intent)))
+    diag = np.stack([np.linspace(120.0, 640.0, 160), np.linspace(610.0, 140.0, 160)], 1).astype(np.float32)
+    out.append((diag, 1))
+    return out
+
+
+def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=()):
     E = h.E
     st = h.get_state()
-    P = 8 * lanes
-    nr = len(routes_table)
+    ids = [h.route_id(s - 1, 4 * lanes + t - 1) for s, t in routes_table] + list(extra)
+    nr = len(ids)
     ego_routes = np.zeros((E, n), np.int32)
     for e in range(E):
         for i in range(n):
-            s, t = routes_table[rng.integers(0, nr)]
-            ego_routes[e, i] = h.route_id(s - 1, 4 * lanes + t - 1)
+            ego_routes[e, i] = ids[rng.integers(0, nr)]
     h.set_ego_routes(ego_routes)
     st["route"][:] = ego_routes
     rw = 42 * lanes
@@ -74,7 +92,7 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0):
             st["path_index"][e, i] = pidx
             st["intention"][e, i] = intent
             st["alive"][e, i] = 0 if rng.uniform() < 0.05 else 1
-    troutes = [h.route_id(s - 1, 4 * lanes + t - 1) for s, t in routes_table]
+    troutes = ids
     for e in range(E):
         k = int(rng.integers(0, npcs + 1)) if npcs else 0
         placed = []
@@ -105,13 +123,15 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0):
     return st, troutes
 
 
-def _oracle_from_state(cfg, st, e, troutes):
+def _oracle_from_state(cfg, st, e, troutes, customs=()):
     n = cfg["n"]
     meta = dict(rays=cfg["rays"], num_lanes=cfg.get("lanes", 3), n_agents=n, use_team=cfg.get("use_team", False),
                 respawn=cfg.get("respawn", True), max_steps=cfg.get("max_steps", 2000),
                 traffic=cfg.get("traffic", False), density=cfg.get("density", 0.5),
                 reward=cfg.get("reward", [10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2]))
     o = R.make_oracle(meta)
+    for path, intent in customs:
+        o.add_route(path, intent)
     o.set_traffic_routes(troutes)
     cars = np.zeros(n, R.O.CAR_DTYPE)
     m = {"x": "x", "y": "y", "v": "v", "h": "heading", "acc": "acc", "steer": "steering", "sx": "spawn_x",
@@ -180,9 +200,16 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0):
             assert h.step_pack() * n * R_ > 512, (h.step_pack(), n, R_)
             pytest.skip("beams of the workgroup's slots exceed one LiDAR pool")
     table = ROUTES2 if lanes == 2 else ROUTES3
-    st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0))
+    customs = custom_routes(h) if cfg.get("custom") else []
+    extra = [h.add_route(path, intent) for path, intent in customs]
+    P = 8 * lanes
+    assert extra == list(range(P * P, P * P + len(customs)))
+    for r, (path, intent) in zip(extra, customs):
+        got = h.route_info(r)
+        assert G.bits_equal(got[0], path) and got[1] == intent and tuple(got[2][:2]) == tuple(path[0])
+    st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0), extra)
     h.set_traffic_routes(troutes)
-    oracles = [_oracle_from_state(cfg, st, e, troutes) for e in range(E)]
+    oracles = [_oracle_from_state(cfg, st, e, troutes, customs) for e in range(E)]
     obs0 = h.observations()
     for e in range(E):
         assert G.bits_equal(obs0[e], oracles[e].observe()), f"env {e}: observation after set_state"
