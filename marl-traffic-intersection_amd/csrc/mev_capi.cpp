@@ -1470,7 +1470,7 @@ struct SnapHeader {
 static_assert(sizeof(SnapHeader) == 64, "snapshot header");
 constexpr uint32_t kSnapMagic = 0x5356454du;  // "MEVS"
 
-std::vector<SnapField> snap_fields(mev_handle* h) {
+static std::vector<SnapField> snap_fields(mev_handle* h) {
     const size_t N = size_t(h->cfg.num_agents), K = size_t(h->cfg.max_npcs), D = size_t(h->D);
     std::vector<SnapField> f;
     auto add = [&](void* live, void* restore, size_t bpe) {

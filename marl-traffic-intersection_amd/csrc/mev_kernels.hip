@@ -1955,11 +1955,14 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             const bool self = js == ii;
             const float dxd = el.tgx[ii] - x, dyd = el.tgy[ii] - y;  // path[min(idx + 10, 159)] (:444-452)
             const float f4 = __builtin_sqrtf(dxd * dxd + dyd * dyd) / float(WIDTH);
-            const float f5 = wrap_angle(atan2f_wave(-dyd, dxd) - h) / PI_F;
+            // one wrap per lane: the own lane's bearing of the look-ahead point, a
+            // neighbour lane's relative heading
+            const float wr = wrap_angle(self ? atan2f_wave(-dyd, dxd) - h : oh - h) / PI_F;
+            const float f5 = wr;
             const float f0 = (self ? x : ox - x) / float(WIDTH);
             const float f1 = (self ? y : oy - y) / float(HEIGHT);
             const float f2 = (self ? v : ov - v) / PHYSICS_MAX_SPEED;
-            const float f3 = (self ? h : wrap_angle(oh - h)) / PI_F;
+            const float f3 = self ? h / PI_F : wr;
             if (act) {
                 float* row = out.obs + (size_t)(e * NE + i) * out.obs_ld;
                 if (!alv) {
@@ -2080,6 +2083,35 @@ __device__ inline float road_safe(float fx, float fy, float dx, float dy, float 
     const float tq = fminf(rx * dx < 0.0f ? -rx * idx : big, ry * dy < 0.0f ? -ry * idy : big);
     const float sc = fmaxf(ax, ay) < sqm ? fminf(tdisc, fminf(tsq, tq)) : 0.0f;
     const float road = fmaxf(fmaxf(sx, sy), sc);
+    const float tx = (dx > 0.0f ? 748.5f - fx : fx - 0.5f) * iadx;
+    const float ty = (dy > 0.0f ? 748.5f - fy : fy - 0.5f) * iady;
+    return fminf(road, fminf(tx, ty));
+}
+
+// road_safe from a point every lane of the wave shares (phase 1: the car centre
+// of the pass's agent): the strip and centre-square terms are wave-uniform
+// branches, so a car outside the centre square does not evaluate the disc root.
+__device__ inline float road_safe_uniform(float fx, float fy, float dx, float dy, float idx, float idy, float iadx,
+                                          float iady, float rwm, float ccen, float crf) {
+    const float big = 1.0e6f;
+    const float rx = fx - 375.0f, ry = fy - 375.0f;
+    const float ax = fabs_f(rx), ay = fabs_f(ry);
+    const float sqm = ccen - 1.55f, rg = crf + 2.0f;
+    float road = 0.0f;
+    if (__builtin_amdgcn_readfirstlane((int)(ax < rwm))) road = fmaxf(road, rwm * iadx - rx * idx);
+    if (__builtin_amdgcn_readfirstlane((int)(ay < rwm))) road = fmaxf(road, rwm * iady - ry * idy);
+    if (__builtin_amdgcn_readfirstlane((int)(fmaxf(ax, ay) < sqm))) {
+        const float qx = rx != 0.0f ? rx : dx, qy = ry != 0.0f ? ry : dy;
+        const float ocx = rx - (qx >= 0.0f ? ccen : -ccen), ocy = ry - (qy >= 0.0f ? ccen : -ccen);
+        const float bq = ocx * dx + ocy * dy;
+        const float cq = ocx * ocx + ocy * ocy - rg * rg;
+        const float disc = bq * bq - cq;
+        const float troot = lidar_keep(-bq - __builtin_amdgcn_sqrtf(disc));
+        const float tdisc = cq <= 0.0f ? 0.0f : ((disc < 0.0f || bq >= 0.0f) ? big : troot);
+        const float tsq = fminf(sqm * iadx - rx * idx, sqm * iady - ry * idy);
+        const float tq = fminf(rx * dx < 0.0f ? -rx * idx : big, ry * dy < 0.0f ? -ry * idy : big);
+        road = fmaxf(road, fminf(tdisc, fminf(tsq, tq)));
+    }
     const float tx = (dx > 0.0f ? 748.5f - fx : fx - 0.5f) * iadx;
     const float ty = (dy > 0.0f ? 748.5f - fy : fy - 0.5f) * iady;
     return fminf(road, fminf(tx, ty));
@@ -2332,7 +2364,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const int px = (int)a.x, py = (int)a.y;
         const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
         const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
-        const float safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
+        const float safe = road_safe_uniform(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
         // probes 1 .. j lie within j*step <= safe of the centre (car centre on screen)
         const int k1 = pmax < (unsigned)WIDTH ? 1 + safe_steps(safe, stp, inv_stp) : 0;
         float fx, fy;
@@ -2568,18 +2600,24 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const float ex0 = box_lo(bx.x), ex1 = box_hi(bx.y);
         const float ey0 = box_lo(bx.z), ey1 = box_hi(bx.w);
         int4 rg;
-        if (R == 1 || (a.x > ex0 && a.x < ex1 && a.y > ey0 && a.y < ey1)) {
+        if (R == 1 || (a.x >= ex0 && a.x <= ex1 && a.y >= ey0 && a.y <= ey1)) {  // (on its edge too)
             rg = make_int4(0 | (R << 16), 0, 0, R);  // inside the widened box: every beam
         } else {
+            // the box's silhouette seen from the agent (outside it): the two corners
+            // that bound its angular span -- the near side's ends when the agent faces
+            // a side, else the corners across the diagonal the agent does not lie on
+            const bool lx = a.x < ex0, hx = a.x > ex1, ly = a.y < ey0, hy = a.y > ey1;
+            const bool mx = !lx && !hx, my = !ly && !hy;
+            const float Xa = my ? (lx ? ex0 : ex1) : (mx ? ex0 : ((lx == ly) ? ex1 : ex0));
+            const float Ya = my ? ey0 : (mx ? (ly ? ey0 : ey1) : ey0);
+            const float Xb = my ? Xa : (mx ? ex1 : ((lx == ly) ? ex0 : ex1));
+            const float Yb = my ? ey1 : (mx ? Ya : ey1);
+            // (relative to the direction of the box centre, as with four corners: both
+            // lie within +-pi/2 of it even when the agent nearly touches the box)
             const float phc = atan2_fast(-(0.5f * (ey0 + ey1) - a.y), 0.5f * (ex0 + ex1) - a.x);
-            float dmin = 0.0f, dmax = 0.0f;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float X = (c & 1) ? ex1 : ex0, Y = (c & 2) ? ey1 : ey0;
-                const float dd = wrap_pi_fast(atan2_fast(-(Y - a.y), X - a.x) - phc);
-                dmin = fminf(dmin, dd);
-                dmax = fmaxf(dmax, dd);
-            }
+            const float da = wrap_pi_fast(atan2_fast(-(Ya - a.y), Xa - a.x) - phc);
+            const float db = wrap_pi_fast(atan2_fast(-(Yb - a.y), Xb - a.x) - phc);
+            const float dmin = fminf(0.0f, fminf(da, db)), dmax = fmaxf(0.0f, fmaxf(da, db));
             float w = phc + dmin - a.z - rel0;
             w -= 6.28318531f * floorf(w * 0.159154943f);  // [0, 2*pi)
             // beams b with rel0 + b*dphi in the span, widened by 2e-4 rad (20x the

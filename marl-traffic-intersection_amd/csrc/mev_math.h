@@ -132,7 +132,8 @@ MEV_HD double reduce_large(uint32_t xi, int* np) {
 // loads.  Returns (sin, cos) before the |y| < 2^-12 shortcut.
 template <bool FMA>
 MEV_HD void sincos_tail(double x, int n, int q, float* so, float* co) {
-    const double xs = ((q + 1) & 2) ? -x : x;
+    // (an exact negation: the sign bit of the high word flipped)
+    const double xs = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, x) ^ ((uint64_t)((q + 1) & 2) << 62));
     const SinCosTab& p = kSinCos[0];
     const double x2 = x * x;
     const double x4 = x2 * x2;
@@ -146,7 +147,7 @@ MEV_HD void sincos_tail(double x, int n, int q, float* so, float* co) {
     const double cp = madd<FMA>(c1, x4, p.c2);
     const float sv = (float)madd<FMA>(sp, x5, s1);
     float cv = (float)madd<FMA>(cp, x6, c2);
-    cv = (q & 2) ? -cv : cv;
+    cv = u2f(f2u(cv) ^ ((uint32_t)(q & 2) << 30));
     *so = (n & 1) ? cv : sv;
     *co = (n & 1) ? sv : cv;
 }
