@@ -2737,6 +2737,15 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         // row) and 8 rows' results are read before any is stored (one LDS wait per 8 rows)
         const int gl = lane < nal ? __float_as_int(ag[lane].w) : 0;
         const bool beam = lane < p.lidar_slots;
+        // (the LiDAR constants read once and pinned in VGPRs by one asm: the compiler cannot
+        // rematerialize an asm result, so it stops re-issuing their scalar loads for every
+        // row -- three dependent scalar-cache round trips per row)
+        float l_max = p.lidar_max, l_step = p.lidar_step, l_inv = p.lidar_inv;
+        asm volatile("" : "+v"(l_max), "+v"(l_step), "+v"(l_inv));
+        auto row_value = [&](int r) {
+            const float dk = TAB ? gmem(p.dist_tab)[r >> 1] : (float)(r >> 1) * l_step;
+            return ((r & 1) ? dk : l_max) * l_inv;
+        };
         for (int j0 = 0; j0 < nal; j0 += 8) {
             int rr[8];
 #pragma unroll
@@ -2745,7 +2754,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             for (int u = 0; u < 8; ++u) {
                 if (j0 + u < nal && beam) {
                     const int g = __builtin_amdgcn_readlane(gl, j0 + u);
-                    out.obs[(size_t)g * out.obs_ld + OBS_HEAD + lane] = lidar_value(rr[u]);
+                    out.obs[(size_t)g * out.obs_ld + OBS_HEAD + lane] = row_value(rr[u]);
                 }
             }
         }
