@@ -1838,7 +1838,15 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
         if (p.use_team && N > 0) {  // sequential sum in agent order, as the reference
             float avg = 0.0f;
             if (PK == 1) {
-                for (int a = 0; a < N; ++a) avg += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), a));
+                if (N <= 8) {  // (unrolled: constant lanes, no scalar loop)
+#pragma unroll
+                    for (int a = 0; a < 8; ++a) {
+                        const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), a));
+                        avg = a < N ? avg + r : avg;
+                    }
+                } else {
+                    for (int a = 0; a < N; ++a) avg += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rew_i), a));
+                }
                 avg /= float(N);
             } else {
                 for (int ps = 0; ps < npk; ++ps) {  // each env's own mean
