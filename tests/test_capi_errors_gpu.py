@@ -63,3 +63,37 @@ def test_large_batch_allocates_and_steps(mev):
         o = h.step(rng.uniform(-1, 1, (E, 8, 2)).astype(np.float32), auto_reset=True)
     assert np.isfinite(o["obs"]).all() and (o["step"] == 3).all()
     h.close()
+
+
+def test_add_route_validates_and_extends_the_id_range(mev):
+    """mev_add_route (a written Car.path): bad paths and intents are refused with
+    nothing added; a good one gets id P*P and becomes a valid ego / traffic / reset
+    route, read back by mev_route_info exactly (spawn = its first point)."""
+    h = mev.Handle(num_envs=2, num_agents=2, lidar_rays=16)
+    P = h.num_points
+    path = h.route_info(h.route_id(0, 13))[0] + np.float32(3.0)
+    bad = path.copy()
+    bad[7, 1] = np.nan
+    with pytest.raises(mev.MevError):
+        h.add_route(bad, 0)
+    with pytest.raises(mev.MevError):
+        h.add_route(path, 3)
+    with pytest.raises(ValueError):
+        h.add_route(path[:100], 0)
+    with pytest.raises(IndexError):
+        h.route_info(P * P)
+    r = h.add_route(path, 1)
+    assert r == P * P
+    got, intent, spawn = h.route_info(r)
+    assert (got.view(np.uint32) == path.view(np.uint32)).all() and intent == 1
+    assert spawn[0] == path[0, 0] and spawn[1] == path[0, 1]
+    h.set_ego_routes(np.full((2, 2), r, np.int32))
+    h.set_traffic_routes([r, h.route_id(1, 14)])
+    h.set_reset_routes([r])
+    h.reset()
+    h.step(np.zeros((2, 2, 2), np.float32))
+    st = h.get_state()
+    assert (st["route"] == r).all() and st["x"][0, 0] == path[0, 0]
+    with pytest.raises(IndexError):
+        h.route_info(r + 1)
+    h.close()
