@@ -249,8 +249,11 @@ def test_several_served_handles_at_once(mev):
     # (sharing one, each launched step would wait for the idle exit behind a resident server)
     assert time.perf_counter() - t0 < 2.0
     d = [h.serve_stats()["steps"] - a for h, a in zip(served, s0)]
-    # two resident servers per process at most: two handles served (almost) throughout
-    assert sorted(d)[-2:] >= [95, 95] and sum(sorted(d)[:-2]) <= 10, d
+    # two resident servers per process at most, serving (almost) throughout: a server that
+    # meets its adaptive idle limit (a host hiccup between two of its handle's steps) exits
+    # and another handle's next step may take the free slot, so the served steps can move
+    # between handles -- but never more than two handles' worth per round (+1 per handoff)
+    assert sum(d) <= 2 * 100 + 5 and sum(sorted(d)[-2:]) >= 170 and sum(d) >= 190, d
     for h in served + launched:
         h.close()
 
