@@ -278,8 +278,9 @@ def test_resident_servers_are_capped(mev):
             _same(hs[i].step(act, auto_reset=True), twins[i].step(act, auto_reset=True), (t, i))
     assert time.perf_counter() - t0 < 2.0
     d = [h.serve_stats()["steps"] - a for h, a in zip(hs, s0)]
-    # kMaxResidentServers: two handles served (almost) throughout, the others launched
-    assert sorted(d)[-2:] >= [95, 95] and sum(sorted(d)[:-2]) <= 10, d
+    # kMaxResidentServers: two handles' worth of served steps per round, the others launched
+    # (a server's idle exit can hand its slot to another handle, as above)
+    assert sum(d) <= 2 * 100 + 5 and sum(sorted(d)[-2:]) >= 170 and sum(d) >= 190, d
     for h in hs + twins:
         h.close()
 
