@@ -34,7 +34,9 @@
 extern "C" {
 #endif
 
-#define MEV_ABI_VERSION 2  /* 2: MEV_GATHER_STATE, MEV_PK_STATE (MEV_PK_FIELDS 7 -> 8), mev_unpack_gathered */
+#define MEV_ABI_VERSION 3  /* 2: MEV_GATHER_STATE, MEV_PK_STATE (MEV_PK_FIELDS 7 -> 8), mev_unpack_gathered;
+                              3: mev_set_car_dims / mev_get_car_dims, mev_set_beam_angles / mev_get_beam_angles,
+                              mev_decode_errors, snapshot format 2 (car sizes, route table check) */
 
 enum {
     MEV_OK = 0,
@@ -159,6 +161,29 @@ int mev_path_len(void);
  * a read-write std::vector member); paths of another length are not
  * supported. */
 int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* route);
+/* Per-car size: reference Car::length / Car::width (cpp/Car.h:19-20), read-write through
+ * cpp/bindings.cpp:24-25 and used by Car::corners (status tests and the SAT car-car
+ * collision, Car.cpp:86-141) and by the LiDAR's box of each car (Lidar.cpp:65-75).
+ * ego_dims [E][N][2] and npc_dims [E][max_npcs][2] hold (length, width) in px; NULL leaves
+ * that array unchanged.  Every car starts at the reference's 54 x 24 px; a reset (and the
+ * MEV_AUTO_RESET of mev_step) gives its egos that size again (new Cars, reference
+ * IntersectionEnv::reset + add_car_with_route), a spawned NPC has it, a respawned ego keeps
+ * its own (Car::respawn, Car.cpp:76-84); NPC sizes move with their NPCs.  Values must be
+ * finite with |value| <= 1e4.  While any car differs from 54 x 24 the steps run the
+ * runtime-layout kernels (k_cars + k_lidar or k_step without the compile-time layouts; no
+ * step server) -- mev_car_dims_active says whether that is the case. */
+int mev_set_car_dims(mev_handle* h, const float* ego_dims, const float* npc_dims);
+int mev_get_car_dims(mev_handle* h, float* ego_dims, float* npc_dims);
+int mev_car_dims_active(const mev_handle* h, int32_t* active);
+/* LiDAR beam offsets (radians, [lidar_rays]): reference Lidar::rel_angles (cpp/Lidar.h:17,
+ * read-write through cpp/bindings.cpp:92), by default the cfg's fov formula
+ * (Lidar.cpp:4-14).  Lidar::update casts beam i along heading + rel_angles[i] for i < rays
+ * (Lidar.cpp:24-25), so a reference Lidar whose rays was lowered casts the first rays
+ * angles of its list: a handle of that many rays with those angles reproduces it.  The
+ * offsets must be evenly spaced (to 1e-5 rad; the car-pair culling models the beams
+ * linearly) and |angle| <= 1000. */
+int mev_set_beam_angles(mev_handle* h, const float* rel);
+int mev_get_beam_angles(mev_handle* h, float* rel);
 /* Ego routes for every (env, agent): route ids [E][N] (reference env.py:104-106,148-151). */
 int mev_set_ego_routes(mev_handle* h, const int32_t* routes);
 /* NPC route list (reference configure_routes / init_traffic_routes, TrafficFlow.cpp:198-238). */
@@ -212,11 +237,18 @@ int mev_set_reset_routes(mev_handle* h, const int32_t* routes, int32_t count);
  * buffer (and env_mask) live on the handle's device and the copies are
  * device-to-device.  mev_restore restores every env (env_mask NULL; also the
  * handle's Philox counter) or only the envs with env_mask[e] != 0; afterwards
- * mev_get_outputs returns the snapshot's outputs. */
+ * mev_get_outputs returns the snapshot's outputs.  The car sizes (mev_set_car_dims)
+ * are part of the state.  A snapshot restores only into a handle of the same shape
+ * whose route table begins with the snapshot handle's routes (mev_add_route, same
+ * paths in the same order); otherwise MEV_E_INVALID and the handle is unchanged. */
 int mev_snapshot_size(mev_handle* h, uint64_t* bytes);
 int mev_snapshot(mev_handle* h, void* dst, uint32_t flags);
 int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_t flags);
 
+/* Diagnostics (cumulative): route ids in state-format gather messages this handle's route
+ * table does not have (mev_unpack_gathered; their rows' look-ahead terms are NaN).
+ * mev_comm_init already refuses ranks whose route tables differ. */
+int mev_decode_errors(mev_handle* h, int64_t* count);
 /* Diagnostics: spawns dropped because max_npcs was full (cumulative). */
 int mev_npc_overflow(mev_handle* h, int64_t* count);
 /* Diagnostics (cumulative): the spawn overflow above, and the NPC turns the

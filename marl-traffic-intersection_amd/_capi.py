@@ -47,7 +47,8 @@ EXPORTED = (
     "mev_set_step_split", "mev_get_step_split", "mev_set_env_deal", "mev_set_serve", "mev_serve_stats",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
     "mev_gather_wait", "mev_output_dlpack", "mev_packed_layout2", "mev_set_gather_format", "mev_lidar_decode_table",
-    "mev_unpack_gathered", "mev_add_route",
+    "mev_unpack_gathered", "mev_add_route", "mev_set_car_dims", "mev_get_car_dims", "mev_car_dims_active",
+    "mev_set_beam_angles", "mev_get_beam_angles", "mev_decode_errors",
 )
 
 
@@ -176,6 +177,12 @@ def load_library(variant: str = None):
     L.mev_unpack_gathered.argtypes = [_vp, _vp, ctypes.c_int32, _vp]
     L.mev_add_route.argtypes = [_vp, f32p, ctypes.c_int32, i32p]
     L.mev_output_dlpack.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(_vp)]
+    L.mev_set_car_dims.argtypes = [_vp, f32p, f32p]
+    L.mev_get_car_dims.argtypes = [_vp, f32p, f32p]
+    L.mev_car_dims_active.argtypes = [_vp, i32p]
+    L.mev_set_beam_angles.argtypes = [_vp, f32p]
+    L.mev_get_beam_angles.argtypes = [_vp, f32p]
+    L.mev_decode_errors.argtypes = [_vp, ctypes.POINTER(ctypes.c_int64)]
     _libs[variant] = L
     return L
 
@@ -652,6 +659,50 @@ class Handle:
         a, b = ctypes.c_int64(), ctypes.c_int64()
         _check(self._lib.mev_npc_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    def decode_errors(self) -> int:
+        """Route ids of state-format gather messages this handle's route table lacks (cumulative)."""
+        v = ctypes.c_int64()
+        _check(self._lib.mev_decode_errors(self._h, ctypes.byref(v)))
+        return v.value
+
+    # -- per-car sizes and beam angles -------------------------------------
+    def set_car_dims(self, ego=None, npc=None):
+        """Car::length / Car::width of every ego ([E][N][2]) and NPC slot ([E][K][2]) in px (mev_set_car_dims);
+        None leaves that array as it is."""
+        f32p = ctypes.POINTER(ctypes.c_float)
+        e = None if ego is None else np.ascontiguousarray(np.broadcast_to(np.asarray(ego, np.float32),
+                                                                          (self.E, self.N, 2)))
+        n = None if npc is None else np.ascontiguousarray(np.broadcast_to(np.asarray(npc, np.float32),
+                                                                          (self.E, self.K, 2)))
+        _check(self._lib.mev_set_car_dims(self._h, None if e is None else e.ctypes.data_as(f32p),
+                                          None if n is None or n.size == 0 else n.ctypes.data_as(f32p)))
+
+    def car_dims(self):
+        """(ego [E][N][2], NPC [E][K][2]) (length, width) of every car."""
+        f32p = ctypes.POINTER(ctypes.c_float)
+        e = np.zeros((self.E, self.N, 2), np.float32)
+        n = np.zeros((self.E, self.K, 2), np.float32)
+        _check(self._lib.mev_get_car_dims(self._h, e.ctypes.data_as(f32p), n.ctypes.data_as(f32p) if n.size else None))
+        return e, n
+
+    def car_dims_active(self) -> bool:
+        """Whether some car differs from the reference's 54 x 24 px (the steps then run the runtime-layout kernels)."""
+        v = ctypes.c_int32()
+        _check(self._lib.mev_car_dims_active(self._h, ctypes.byref(v)))
+        return bool(v.value)
+
+    def set_beam_angles(self, rel):
+        """LiDAR beam offsets [R] in radians (Lidar::rel_angles; evenly spaced)."""
+        a = np.ascontiguousarray(np.asarray(rel, np.float32).reshape(-1))
+        if a.size != self.R:
+            raise ValueError(f"{self.R} beam angles expected, got {a.size}")
+        _check(self._lib.mev_set_beam_angles(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+
+    def beam_angles(self) -> np.ndarray:
+        a = np.zeros(self.R, np.float32)
+        _check(self._lib.mev_get_beam_angles(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+        return a
 
     def npc_overflow(self) -> int:
         v = ctypes.c_int64()

@@ -17,8 +17,9 @@ Deviations from MARLEnv (all outside the hot path):
    160 points, RouteGen.cpp:111-205); a path that is not a lane-layout route is
    appended to the device route table (mev_add_route); other lengths raise
    ValueError;
- * Car.length / Car.width are honoured by Car.check_collision but the
-   environment simulates the reference's fixed 54 x 24 px cars;
+ * Car.length / Car.width (bindings.cpp:24-25) are simulated per car, as in the
+   reference (status corners, SAT collisions, LiDAR boxes; mev_set_car_dims), in
+   |value| <= 1e4 px;
  * observations after set_state() / mid-episode add_car_with_route() carry a
    fresh LiDAR block (max range), exactly as after reset.
 """
@@ -264,9 +265,10 @@ class IntersectionEnv:
             return None
         h = self._h
         if h is None or h.N != n or self._h_lidar != self._lidar:
-            keep = None
+            keep = keep_dims = None
             if h is not None and not self._fresh:
                 keep = h.get_state()  # cars added mid-episode keep the running episode
+                keep_dims = h.car_dims() if h.car_dims_active() else None
             if h is not None:
                 h.close()
             h = self._h = self._create(n, self._lidar)
@@ -277,7 +279,7 @@ class IntersectionEnv:
             h.set_ego_routes(np.asarray(self._routes, np.int32)[None])
             h.reset()  # every car at the spawn of its route
             if keep is not None:
-                self._restore_grown(keep)
+                self._restore_grown(keep, keep_dims)
             self._pending = []
             return h
         if self._reward_dirty:
@@ -290,8 +292,8 @@ class IntersectionEnv:
             self._pending = []
         return h
 
-    def _restore_grown(self, old):
-        """Old cars keep their state; newly added ones start at their spawn (add_car_with_route)."""
+    def _restore_grown(self, old, old_dims=None):
+        """Old cars keep their state (and size); newly added ones start at their spawn (add_car_with_route)."""
         h = self._h
         new = h.get_state()  # after creation == a reset: every car at its spawn
         m = old["x"].shape[1]
@@ -301,6 +303,10 @@ class IntersectionEnv:
             else:
                 new[k][:, :m] = v
         h.set_state(new)
+        if old_dims is not None:
+            ego, npc = h.car_dims()
+            ego[:, :m] = old_dims[0]
+            h.set_car_dims(ego, old_dims[1])
 
     @property
     def step_count(self) -> int:
@@ -354,9 +360,11 @@ class IntersectionEnv:
         return h.observations()[0]
 
     # ----------------------------------------------------------- cars
-    def _cars_from(self, st, ego: bool) -> List[Car]:
+    def _cars_from(self, st, ego: bool, dims=None) -> List[Car]:
         out = []
         h = self._h
+        if dims is None:
+            dims = h.car_dims() if h.car_dims_active() else None
         if ego:
             n = h.N
             get = lambda k, i: st[k][0, i]  # noqa: E731
@@ -376,6 +384,8 @@ class IntersectionEnv:
             if path is None:  # route tables are constant for the env's lane count: built once per route
                 path = self._paths[c._route] = [tuple(map(float, p)) for p in h.route_info(c._route)[0]]
             c.path = list(path)
+            if dims is not None:  # Car::length / Car::width (cpp/Car.h:19-20)
+                c.length, c.width = float(dims[0 if ego else 1][0, i, 0]), float(dims[0 if ego else 1][0, i, 1])
             if ego:
                 c.spawn_state = State(st["spawn_x"][0, i], st["spawn_y"][0, i], st["spawn_v"][0, i],
                                       st["spawn_heading"][0, i])
@@ -433,12 +443,15 @@ class IntersectionEnv:
             return
         if self._h is not None and len(self._routes) == self._h.N:
             st = self._h.get_state()
+            dims = self._h.car_dims() if self._h.car_dims_active() else None
             self._h.close()
             self._h = self._create(len(self._routes), lidar)
             if self._traffic_routes is not None:
                 self._h.set_traffic_routes(self._traffic_routes)
             self._h.set_ego_routes(np.asarray(self._routes, np.int32)[None])
             self._h.set_state(st)
+            if dims is not None:
+                self._h.set_car_dims(*dims)
             self._h_lidar = lidar
         self._lidar = lidar
 
@@ -553,6 +566,14 @@ class IntersectionEnv:
         st["npc_count"][0] = k
         st["step_count"][0] = int(s.step_count)
         self._h.set_state(st)
+        # Car::length / Car::width of every car (the reference copies them with the cars)
+        ego_d = np.array([[[c.length, c.width] for c in s.cars]], np.float32)
+        npc_d = np.empty((1, self._h.K, 2), np.float32)
+        npc_d[...] = (54.0, 24.0)
+        if k:
+            npc_d[0, :k] = [[c.length, c.width] for c in s.traffic_cars]
+        if self._h.car_dims_active() or np.any(ego_d != (54.0, 24.0)) or np.any(npc_d != (54.0, 24.0)):
+            self._h.set_car_dims(ego_d, npc_d)
         self._fresh = False
         self._pending = []
 

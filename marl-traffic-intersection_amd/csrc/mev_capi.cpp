@@ -51,10 +51,27 @@ hipError_t dalloc(T** p, size_t n) {
 struct mev_handle {
     mev_config cfg{};
     int D = 0, lidar_slots = 0, P = 0, nroutes = 0;
+    int route_cap = 0;  // routes the device route tables have room for (mev_add_route)
     std::vector<mev::LanePoint> pts;
     std::vector<float> h_paths, h_spawn;
     std::vector<float> h_pbox;  // [nroutes][3][4] piece bounding boxes (RouteTab::pbox)
     std::vector<int32_t> h_intent;
+    // route_hash[r]: FNV-1a of routes [0, r) (paths and intents), so a snapshot or a gather
+    // peer can tell whether its route ids name the same routes here (routes are only appended)
+    std::vector<uint64_t> route_hash{1469598103934665603ull};
+    void extend_route_hash() {
+        while (route_hash.size() <= size_t(nroutes)) {
+            const size_t r = route_hash.size() - 1;
+            uint64_t x = route_hash.back();
+            auto mix = [&x](const void* p, size_t n) {
+                const uint8_t* b = static_cast<const uint8_t*>(p);
+                for (size_t i = 0; i < n; ++i) x = (x ^ b[i]) * 1099511628211ull;
+            };
+            mix(&h_paths[r * 2 * mev::PATH_LEN], 2 * mev::PATH_LEN * sizeof(float));
+            mix(&h_intent[r], sizeof(int32_t));
+            route_hash.push_back(x);
+        }
+    }
     std::vector<int32_t> h_traffic;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -290,6 +307,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     }
     h->P = 8 * c.num_lanes;
     h->nroutes = h->P * h->P;
+    h->route_cap = h->nroutes;
     h->pts = mev::build_lane_points(c.num_lanes);
     h->h_paths.resize(size_t(h->nroutes) * 2 * mev::PATH_LEN);
     h->h_intent.resize(size_t(h->nroutes));
@@ -330,6 +348,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
         }
     }
     h->h_traffic = mev::default_traffic_routes(c.num_lanes);
+    h->extend_route_hash();
 
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
@@ -365,7 +384,8 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     }
     A(&p.ego.alive, EN);
     A(&p.npc.alive, EK); A(&p.npc.count, size_t(E));
-    A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 2); A(&p.debug, size_t(E) * 8);
+    A(&p.ego_dim, EN * 2); A(&p.npc_dim, EK * 2);  // car sizes (mev_set_car_dims), 54 x 24 until set
+    A(&p.step_count, size_t(E)); A(&p.pending_reset, size_t(E)); A(&p.overflow, 3); A(&p.debug, size_t(E) * 8);
     A(&p.ob_box, size_t(E) * size_t(N + c.max_npcs)); A(&p.ob_cand, EN * 2);
     if (c.traffic_flow) {  // the fused traffic kernel's NPC-aware deal (mev_kernels.h, kDealLists)
         A(&p.deal_cnt, size_t(3) * mev::kDealRingInts);
@@ -401,6 +421,11 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     if (err == hipSuccess)
         err = hipMemcpyAsync(h->d_lidar_table, h->h_lidar_table.data(), 256 * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_traffic, h->h_traffic.data(), h->h_traffic.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
+    // every car of the reference's default size (Car.h:19-20); p.dims stays 0 while they all are
+    std::vector<float> dflt(2 * std::max(EN, EK));
+    for (size_t i = 0; i < dflt.size(); i += 2) { dflt[i] = mev::CAR_LENGTH; dflt[i + 1] = mev::CAR_WIDTH; }
+    if (err == hipSuccess) err = hipMemcpyAsync(p.ego_dim, dflt.data(), EN * 2 * sizeof(float), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(p.npc_dim, dflt.data(), EK * 2 * sizeof(float), hipMemcpyHostToDevice, h->stream);
     // default ego routes: reference env.py:138-145 (mapping routes, cyclic)
     std::vector<int32_t> ego(EN);
     {
@@ -624,6 +649,8 @@ int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* rou
     for (int i = 0; i < 2 * mev::PATH_LEN; ++i)
         if (!(fabsf(path[i]) < 1.0e6f)) return fail(MEV_E_INVALID, "path points must be finite (|coordinate| < 1e6)");
     if (h->nroutes >= 32767) return fail(MEV_E_INVALID, "too many routes (the state gather format ships i16 ids)");
+    if (h->comm && h->gather_fmt == MEV_GATHER_STATE)  // every rank's route ids are decoded with the root's table
+        return fail(MEV_E_INVALID, "routes cannot be added while a state-format gather communicator exists");
     HIP_TRY(hipSetDevice(h->cfg.device));
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -644,15 +671,36 @@ int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* rou
             h->h_pbox.push_back(x0); h->h_pbox.push_back(x1); h->h_pbox.push_back(y0); h->h_pbox.push_back(y1);
         }
     }
-    // the four route tables, reallocated one route larger and uploaded whole
+    // the four route tables: the new route's rows go into spare capacity; a full table is
+    // reallocated at twice the routes (so n added routes cost O(log n) reallocations, each a
+    // hipFree that waits for the device) and uploaded whole
+    const size_t per[4] = {2 * mev::PATH_LEN * sizeof(float), sizeof(int32_t), 3 * sizeof(float), 12 * sizeof(float)};
+    const void* src[4] = {h->h_paths.data(), h->h_intent.data(), h->h_spawn.data(), h->h_pbox.data()};
+    if (r < h->route_cap) {
+        void* cur[4] = {h->d_paths, h->d_intent, h->d_spawn_tab, h->d_pbox};
+        hipError_t e = hipSuccess;
+        for (int k = 0; k < 4 && e == hipSuccess; ++k)
+            e = hipMemcpy(static_cast<uint8_t*>(cur[k]) + size_t(r) * per[k],
+                          static_cast<const uint8_t*>(src[k]) + size_t(r) * per[k], per[k], hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            h->h_paths.resize(h->h_paths.size() - 2 * mev::PATH_LEN);
+            h->h_intent.pop_back();
+            h->h_spawn.resize(h->h_spawn.size() - 3);
+            h->h_pbox.resize(h->h_pbox.size() - 12);
+            return fail(MEV_E_HIP, std::string("route table: ") + hipGetErrorString(e));
+        }
+        h->nroutes = r + 1;
+        h->extend_route_hash();
+        h->sp.rt.nroutes = h->nroutes;
+        *route = r;
+        return MEV_OK;
+    }
+    const int cap = std::min(32767, std::max(2 * h->route_cap, r + 1));
     hipError_t e = hipSuccess;
     void* np[4] = {nullptr, nullptr, nullptr, nullptr};
-    const size_t bytes[4] = {h->h_paths.size() * sizeof(float), h->h_intent.size() * sizeof(int32_t),
-                             h->h_spawn.size() * sizeof(float), h->h_pbox.size() * sizeof(float)};
-    const void* src[4] = {h->h_paths.data(), h->h_intent.data(), h->h_spawn.data(), h->h_pbox.data()};
     for (int k = 0; k < 4 && e == hipSuccess; ++k) {
-        e = hipMalloc(&np[k], bytes[k]);
-        if (e == hipSuccess) e = hipMemcpy(np[k], src[k], bytes[k], hipMemcpyHostToDevice);
+        e = hipMalloc(&np[k], size_t(cap) * per[k]);
+        if (e == hipSuccess) e = hipMemcpy(np[k], src[k], size_t(r + 1) * per[k], hipMemcpyHostToDevice);
     }
     if (e != hipSuccess) {
         for (void* q : np) if (q) (void)hipFree(q);
@@ -671,13 +719,103 @@ int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* rou
     h->d_intent = static_cast<int32_t*>(np[1]);
     h->d_spawn_tab = static_cast<float*>(np[2]);
     h->d_pbox = static_cast<float*>(np[3]);
+    h->route_cap = cap;
     h->nroutes = r + 1;
+    h->extend_route_hash();
     h->sp.rt.path = h->d_paths;
     h->sp.rt.intent = h->d_intent;
     h->sp.rt.spawn = h->d_spawn_tab;
     h->sp.rt.pbox = reinterpret_cast<const float4*>(h->d_pbox);
     h->sp.rt.nroutes = h->nroutes;  // (the next launch refreshes the device copy of the parameters)
     *route = r;
+    return MEV_OK;
+}
+
+// ---- per-car sizes (reference Car::length / Car::width, cpp/Car.h:19-20, read-write
+// through cpp/bindings.cpp:24-25): the SAT corners, the status corners and the LiDAR
+// boxes of each car.  The device arrays always hold every car's size (54 x 24 until
+// set); SimParams::dims says whether any differs, and only then do the steps run the
+// runtime-layout kernels that read them (mev_kernels.hip, DIMS).
+static bool all_default_dims(const float* d, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (d[2 * i] != mev::CAR_LENGTH || d[2 * i + 1] != mev::CAR_WIDTH) return false;
+    return true;
+}
+
+int mev_set_car_dims(mev_handle* h, const float* ego_dims, const float* npc_dims) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    const size_t EN = size_t(h->cfg.num_envs) * size_t(h->cfg.num_agents);
+    const size_t EK = size_t(h->cfg.num_envs) * size_t(h->cfg.max_npcs);
+    for (int w = 0; w < 2; ++w) {
+        const float* d = w ? npc_dims : ego_dims;
+        const size_t n = 2 * (w ? EK : EN);
+        if (d)
+            for (size_t i = 0; i < n; ++i)
+                if (!(fabsf(d[i]) <= 1.0e4f)) return fail(MEV_E_INVALID, "car length / width must be finite, |value| <= 1e4 px");
+    }
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
+    if (ego_dims) HIP_TRY(hipMemcpyAsync(h->sp.ego_dim, ego_dims, EN * 2 * sizeof(float), hipMemcpyHostToDevice, h->stream));
+    if (npc_dims && EK) HIP_TRY(hipMemcpyAsync(h->sp.npc_dim, npc_dims, EK * 2 * sizeof(float), hipMemcpyHostToDevice, h->stream));
+    // whether any car differs from 54 x 24: the arrays given, and the device's for the other
+    std::vector<float> e(ego_dims ? 0 : EN * 2), k(npc_dims ? 0 : EK * 2);
+    if (!e.empty()) HIP_TRY(hipMemcpyAsync(e.data(), h->sp.ego_dim, e.size() * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    if (!k.empty()) HIP_TRY(hipMemcpyAsync(k.data(), h->sp.npc_dim, k.size() * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    const bool dflt = all_default_dims(ego_dims ? ego_dims : e.data(), EN) && all_default_dims(npc_dims ? npc_dims : k.data(), EK);
+    h->sp.dims = dflt ? 0 : 1;  // (the next step refreshes the device copy of the parameters)
+    h->deal_valid = false;      // (a dims handle runs another kernel: the deal restarts)
+    return MEV_OK;
+}
+
+int mev_get_car_dims(mev_handle* h, float* ego_dims, float* npc_dims) {
+    if (!h) return fail(MEV_E_INVALID, "null handle");
+    const size_t EN = size_t(h->cfg.num_envs) * size_t(h->cfg.num_agents);
+    const size_t EK = size_t(h->cfg.num_envs) * size_t(h->cfg.max_npcs);
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
+    if (ego_dims) HIP_TRY(hipMemcpyAsync(ego_dims, h->sp.ego_dim, EN * 2 * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    if (npc_dims && EK) HIP_TRY(hipMemcpyAsync(npc_dims, h->sp.npc_dim, EK * 2 * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MEV_OK;
+}
+
+int mev_car_dims_active(const mev_handle* h, int32_t* active) {
+    if (!h || !active) return fail(MEV_E_INVALID, "null argument");
+    *active = h->sp.dims;
+    return MEV_OK;
+}
+
+// ---- LiDAR beam offsets (reference Lidar::rel_angles, cpp/Lidar.h:17, read-write through
+// cpp/bindings.cpp:92): e.g. the first R angles of a longer beam list, which is what a
+// reference Lidar whose `rays` was lowered casts (Lidar.cpp:24-25 indexes rel_angles up to
+// rays).  The step's car-pair culling models the beams as rel[0] + b * (rel[R-1] - rel[0]) /
+// (R - 1) with 2e-4 rad of margin (mev_kernels.hip phase 3b), so the offsets must be evenly
+// spaced to 1e-5 rad; any other list is refused.
+int mev_set_beam_angles(mev_handle* h, const float* rel) {
+    if (!h || !rel) return fail(MEV_E_INVALID, "null argument");
+    const int R = h->cfg.lidar_rays;
+    for (int b = 0; b < R; ++b)
+        if (!(fabsf(rel[b]) <= 1.0e3f)) return fail(MEV_E_INVALID, "beam angles must be finite, |angle| <= 1000 rad");
+    if (R > 2) {
+        const double d = (double(rel[R - 1]) - double(rel[0])) / double(R - 1);
+        for (int b = 1; b < R - 1; ++b)
+            if (fabs(double(rel[b]) - (double(rel[0]) + b * d)) > 1.0e-5)
+                return fail(MEV_E_INVALID, "beam angles must be evenly spaced (to 1e-5 rad)");
+    }
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(h->d_rel, rel, size_t(R) * sizeof(float), hipMemcpyHostToDevice));
+    return MEV_OK;
+}
+
+int mev_get_beam_angles(mev_handle* h, float* rel) {
+    if (!h || !rel) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(rel, h->d_rel, size_t(h->cfg.lidar_rays) * sizeof(float), hipMemcpyDeviceToHost));
     return MEV_OK;
 }
 
@@ -1465,8 +1603,11 @@ struct SnapHeader {
     uint32_t magic, version;
     int32_t E, N, K, D, R, nfields;
     uint64_t rng_counter, total_bytes;
-    uint8_t pad[16];
+    int32_t dims;     // SimParams::dims of the snapshot's handle (some car not 54 x 24)
+    int32_t nroutes;  // its route table's size (route ids must name the same routes on restore)
+    uint64_t route_hash;  // mev_handle::route_hash[nroutes]
 };
+constexpr uint32_t kSnapVersion = 2;  // 2: car sizes, dims flag and route count
 static_assert(sizeof(SnapHeader) == 64, "snapshot header");
 constexpr uint32_t kSnapMagic = 0x5356454du;  // "MEVS"
 
@@ -1480,6 +1621,8 @@ static std::vector<SnapField> snap_fields(mev_handle* h) {
     STATE_FIELDS(SNAP)
 #undef SNAP
     add(h->sp.pending_reset, h->sp.pending_reset, 1);
+    add(h->sp.ego_dim, h->sp.ego_dim, N * 2 * sizeof(float));  // car sizes (mev_set_car_dims)
+    add(h->sp.npc_dim, h->sp.npc_dim, K * 2 * sizeof(float));
     const mev::Outputs& L = h->last;
     const mev::Outputs& I = h->internal;
     add(L.obs ? L.obs : I.obs, I.obs, N * D * sizeof(float));
@@ -1523,7 +1666,8 @@ int mev_snapshot(mev_handle* h, void* dst, uint32_t flags) {
     std::vector<size_t> off;
     const size_t total = snap_offsets(f, E, &off);
     SnapHeader hd{};
-    hd.magic = kSnapMagic; hd.version = 1;
+    hd.magic = kSnapMagic; hd.version = kSnapVersion;
+    hd.dims = h->sp.dims; hd.nroutes = h->nroutes; hd.route_hash = h->route_hash[size_t(h->nroutes)];
     hd.E = h->cfg.num_envs; hd.N = h->cfg.num_agents; hd.K = h->cfg.max_npcs; hd.D = h->D; hd.R = h->cfg.lidar_rays;
     hd.nfields = int32_t(f.size()); hd.rng_counter = h->rng_counter; hd.total_bytes = total;
     uint8_t* d = static_cast<uint8_t*>(dst);
@@ -1555,9 +1699,13 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
         const std::vector<SnapField> f0 = snap_fields(h);
         h->last = save_last;
         const size_t total0 = snap_offsets(f0, E, nullptr);
-        if (hd.magic != kSnapMagic || hd.version != 1 || hd.E != h->cfg.num_envs || hd.N != h->cfg.num_agents ||
+        if (hd.magic != kSnapMagic || hd.version != kSnapVersion || hd.E != h->cfg.num_envs || hd.N != h->cfg.num_agents ||
             hd.K != h->cfg.max_npcs || hd.D != h->D || hd.nfields != int32_t(f0.size()) || hd.total_bytes != total0)
             return fail(MEV_E_INVALID, "snapshot does not match this handle");
+        // the snapshot's route ids index its handle's route table (lane-layout routes, then
+        // mev_add_route's): a handle with fewer routes would read past the end of its tables
+        if (hd.nroutes < 0 || hd.nroutes > h->nroutes || hd.route_hash != h->route_hash[size_t(hd.nroutes)])
+            return fail(MEV_E_INVALID, "snapshot's routes differ from this handle's (mev_add_route)");
         if (env_mask && f0.size() > size_t(mev::kMaxRestoreFields)) return fail(MEV_E_INVALID, "too many snapshot fields");
     }
     // the live outputs are restored into the handle's own buffers; envs a masked
@@ -1575,6 +1723,7 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
         const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
         for (size_t i = 0; i < f.size(); ++i) HIP_TRY(hipMemcpyAsync(f[i].restore, s + off[i], f[i].bpe * E, kind, h->stream));
         h->rng_counter = hd.rng_counter;
+        h->sp.dims = hd.dims;
     } else {
         const uint8_t* dsrc = s;
         const uint8_t* dmask = env_mask;
@@ -1602,6 +1751,7 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
             tab.bpe[i] = int32_t(f[i].bpe);
         }
         HIP_TRY(mev::launch_restore(tab, dsrc, dmask, h->cfg.num_envs, h->stream));
+        h->sp.dims = h->sp.dims || hd.dims;  // (the sizes arrays hold valid entries either way)
     }
     if (!dev) HIP_TRY(hipStreamSynchronize(h->stream));
     return MEV_OK;
@@ -1695,6 +1845,32 @@ int mev_comm_init(mev_handle* h, const uint8_t* id, int32_t world, int32_t rank,
     h->comm = comm;
     h->world = world; h->rank = rank; h->root = root; h->slots = slots; h->gathers = 0;
     hipError_t e = hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking);
+    if (e == hipSuccess && h->gather_fmt == MEV_GATHER_STATE && world > 1) {
+        // the root rebuilds every rank's observation heads from route ids with ITS route
+        // table: every rank must hold the same routes (mev_add_route, in the same order)
+        uint64_t* d = nullptr;
+        e = hipMalloc(reinterpret_cast<void**>(&d), size_t(world + 1) * 2 * sizeof(uint64_t));
+        const uint64_t mine[2] = {uint64_t(h->nroutes), h->route_hash[size_t(h->nroutes)]};
+        std::vector<uint64_t> all(size_t(world) * 2);
+        if (e == hipSuccess) e = hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice);
+        ncclResult_t ar = ncclSuccess;
+        if (e == hipSuccess) ar = ncclAllGather(d, d + 2, 2, ncclUint64, comm, h->comm_stream);
+        if (e == hipSuccess && ar == ncclSuccess) e = hipStreamSynchronize(h->comm_stream);
+        if (e == hipSuccess && ar == ncclSuccess)
+            e = hipMemcpy(all.data(), d + 2, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+        if (d) (void)hipFree(d);
+        if (ar != ncclSuccess) {
+            h->free_comm();
+            return fail(MEV_E_HIP, std::string("RCCL route table check: ") + ncclGetErrorString(ar));
+        }
+        if (e == hipSuccess)
+            for (int r = 0; r < world; ++r)
+                if (all[size_t(2 * r)] != mine[0] || all[size_t(2 * r + 1)] != mine[1]) {
+                    h->free_comm();
+                    return fail(MEV_E_INVALID, "the ranks' route tables differ (mev_add_route): the state gather "
+                                               "format decodes every rank's route ids with the root's table");
+                }
+    }
     const size_t per = (rank == root) ? size_t(world) * h->pk_bytes : h->pk_bytes;
     for (int b = 0; b < 2 && e == hipSuccess; ++b) {
         e = hipMalloc(reinterpret_cast<void**>(&h->pk_buf[b]), per);
@@ -1738,7 +1914,7 @@ int mev_gather_result(mev_handle* h, void** stacked, uint64_t* bytes_per_rank, i
 int mev_unpack_gathered(mev_handle* h, const void* stacked, int32_t world, float* obs) {
     if (!h || !stacked || !obs) return fail(MEV_E_INVALID, "null argument");
     if (!h->comm) return fail(MEV_E_INVALID, "no communicator (mev_comm_init): the layout is the handle's");
-    if (world < 1) return fail(MEV_E_INVALID, "world must be >= 1");
+    if (world < 1 || world > h->world) return fail(MEV_E_INVALID, "world must be in [1, the communicator's world]");
     HIP_TRY(hipSetDevice(h->cfg.device));
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     const uint8_t* sb = static_cast<const uint8_t*>(stacked);
@@ -1879,6 +2055,17 @@ int mev_npc_stats(mev_handle* h, int64_t* overflow, int64_t* sequential_turns) {
     HIP_TRY(hipStreamSynchronize(h->stream));
     *overflow = int64_t(v[0]);
     *sequential_turns = int64_t(v[1]);
+    return MEV_OK;
+}
+
+int mev_decode_errors(mev_handle* h, int64_t* count) {
+    if (!h || !count) return fail(MEV_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->cfg.device));
+    if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
+    unsigned long long v[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(v, h->sp.overflow, sizeof(v), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    *count = int64_t(v[2]);
     return MEV_OK;
 }
 

@@ -114,7 +114,7 @@ struct SimParams {
     int32_t n_traffic_routes;
     int32_t* step_count;      // [E]
     uint8_t* pending_reset;   // [E]
-    unsigned long long* overflow;  // [2]: dropped spawns, sequential NPC turns (npc_phase)
+    unsigned long long* overflow;  // [3]: dropped spawns, sequential NPC turns (npc_phase), undecodable route ids (k_decode_state)
     unsigned long long* debug;     // diagnostic builds only (MEV_STAMPS): [E*8]
     // LiDAR hand-off k_cars -> k_lidar (L2-resident, rewritten every step)
     int4* ob_box;                  // [E][ob_stride] integer pixel AABB (x0, x1, y0, y1)
@@ -133,6 +133,15 @@ struct SimParams {
     // class) counters, each on its own 128-B line, and per (ring, list, class) env orders
     int32_t* deal_cnt;    // [3][kDealLists][kDealClasses][kDealPad]
     int32_t* deal_order;  // [3][kDealLists][kDealClasses][E]: rings like the counters
+    // Car sizes (Car::length / Car::width, cpp/Car.h:19-20), (length, width) per car: ego
+    // [E*N][2], NPC [E*K][2] (moved with the NPCs).  Always valid: every entry is 54, 24 until
+    // mev_set_car_dims.  The kernels that can run a handle with other sizes (k_cars, k_reset,
+    // k_step<NM = 0>) read and keep them; dims: some car differs from 54 x 24, so the steps
+    // run those kernels (the compile-time layouts assume the reference's size).  Last in the
+    // struct: the other fields keep their offsets.
+    float* ego_dim;
+    float* npc_dim;
+    int32_t dims;
 };
 
 // The fused traffic k_step deals envs to workgroups by their NPC count: every env

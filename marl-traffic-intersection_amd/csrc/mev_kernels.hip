@@ -318,9 +318,10 @@ struct EgoLDS {
 
 // capacity KM NPC slots (k_cars / k_reset: MAXK; the fused k_step: the smallest
 // of 32 / 64 that holds the handle's max_npcs, so that the NPC arrays leave room
-// in the wave's LDS for a LiDAR pool)
-template <int KM>
+// in the wave's LDS for a LiDAR pool).  DIMS: with each NPC's length / width (last).
+template <int KM, bool DIMS = false>
 struct NpcLDST {
+    static constexpr bool kDims = DIMS;
     static constexpr int kCap = KM;
     float x[KM], y[KM], v[KM], h[KM], c[KM], s[KM], acc[KM], steer[KM];
     int32_t pidx[KM], route[KM], intent[KM];
@@ -347,8 +348,25 @@ struct NpcLDST {
     float nsteer[KM], ntan[KM];  // Car::update's new steering angle and its tangent
     float accb[KM], mdc[KM];  // cruise throttle, distance to the centre
     float endx[KM], endy[KM];  // the route's last point (arrival test)
+    // Per-NPC length / width (Car::length / Car::width), after every other array: only in
+    // the kernels that can run a handle with per-car sizes (k_cars, k_reset, k_step<NM =
+    // 0>); zero-length elsewhere, so the compile-time layouts keep their size
+    float len[DIMS ? KM : 0], wid[DIMS ? KM : 0];
 };
-using NpcLDS = NpcLDST<MAXK>;
+using NpcLDS = NpcLDST<MAXK, true>;
+
+// the size of NPC k (the reference's constant 54 x 24 px unless the handle has cars of
+// other sizes: dims)
+template <class NL>
+__device__ __forceinline__ float npc_len(const NL& nl, int k, bool dims) {
+    if constexpr (NL::kDims) return dims ? nl.len[k] : CAR_LENGTH;
+    else return CAR_LENGTH;
+}
+template <class NL>
+__device__ __forceinline__ float npc_wid(const NL& nl, int k, bool dims) {
+    if constexpr (NL::kDims) return dims ? nl.wid[k] : CAR_WIDTH;
+    else return CAR_WIDTH;
+}
 
 // One NPC slot's state in the registers of lane = slot, loaded together with the
 // ego state (one round of loads) and handed to npc_phase.
@@ -356,13 +374,15 @@ struct NpcRegs {
     float x, y, v, h, acc, steer;
     int32_t pidx, route, intent;
     uint8_t alive;
+    float len, wid;  // (dims handles only)
 };
 
 
 // --------------------------------------------------- NPC traffic phase ---
 // update_traffic_flow, cpp/TrafficFlow.cpp:317-367, for env e.  Egos (positions
 // in LDS) are read for spawn blocking but not moved.  On return NpcLDS holds the compacted NPCs.
-__device__ inline NpcRegs npc_load(const SimParams& p, int e, int lane) {
+template <bool DIMS>
+__device__ __forceinline__ NpcRegs npc_load(const SimParams& p, int e, int lane) {
     NpcRegs r{};
     if (lane < p.K) {
         const int g = e * p.K + lane;
@@ -370,6 +390,10 @@ __device__ inline NpcRegs npc_load(const SimParams& p, int e, int lane) {
         r.acc = npcf(p, NF_ACC)[g]; r.steer = npcf(p, NF_STEER)[g];
         r.pidx = npci(p, NF_PIDX)[g]; r.route = npci(p, NF_ROUTE)[g]; r.intent = npci(p, NF_INTENT)[g];
         r.alive = gmem(p.npc.alive)[g];
+        if constexpr (DIMS) {
+            r.len = gmem(p.npc_dim)[2 * g];
+            r.wid = gmem(p.npc_dim)[2 * g + 1];
+        }
     }
     return r;
 }
@@ -550,6 +574,10 @@ __device__ __forceinline__ void npc_writeback(const SimParams& p, int e, const N
         npcf(p, NF_X)[g] = nl.x[lane]; npcf(p, NF_Y)[g] = nl.y[lane]; npcf(p, NF_V)[g] = nl.v[lane]; npcf(p, NF_H)[g] = nl.h[lane];
         npcf(p, NF_ACC)[g] = nl.acc[lane]; npcf(p, NF_STEER)[g] = nl.steer[lane]; npci(p, NF_PIDX)[g] = nl.pidx[lane];
         npci(p, NF_ROUTE)[g] = nl.route[lane]; npci(p, NF_INTENT)[g] = nl.intent[lane]; gmem(p.npc.alive)[g] = 1;
+        if constexpr (NL::kDims) {
+            gmem(p.npc_dim)[2 * g] = nl.len[lane];
+            gmem(p.npc_dim)[2 * g + 1] = nl.wid[lane];
+        }
     }
     if (lane == 0) gmem(p.npc.count)[e] = newcnt;
 }
@@ -560,6 +588,9 @@ template <class NL>
 __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cnt, NL& nl, int lane,
                           const float* ego_x, const float* ego_y, const NpcRegs& nr) {
     const int K = p.K;
+    // per-NPC sizes (Car::length / width in the SAT and the LiDAR boxes): kernels that can
+    // run a handle with cars of other sizes keep them (every entry is 54 x 24 unless p.dims)
+    constexpr bool dims = NL::kDims;
 #ifdef MEV_STAMPS_N
     unsigned long long nt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long nt_prev = __builtin_amdgcn_s_memtime();
@@ -569,6 +600,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         nl.x[lane] = nr.x; nl.y[lane] = nr.y; nl.v[lane] = nr.v; nl.h[lane] = nr.h;
         nl.acc[lane] = nr.acc; nl.steer[lane] = nr.steer;
         nl.pidx[lane] = nr.pidx; nl.route[lane] = nr.route; nl.intent[lane] = nr.intent; nl.alive[lane] = nr.alive;
+        if constexpr (NL::kDims) { nl.len[lane] = nr.len; nl.wid[lane] = nr.wid; }
     }
     // -- spawn (TrafficFlow.cpp:320-329, try_spawn_traffic_car :275-315)
     int r = -1;
@@ -621,6 +653,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
                     nl.route[cnt] = rid;
                     nl.intent[cnt] = gmem(p.rt.intent)[rid];
                     nl.alive[cnt] = 1;
+                    if constexpr (NL::kDims) { nl.len[cnt] = CAR_LENGTH; nl.wid[cnt] = CAR_WIDTH; }  // a new Car
                 }
                 ++cnt;
             } else if (lane == 0) {
@@ -1059,7 +1092,8 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     NT(3);  // sequential turns (with the moves)
     // -- NPC-NPC collision: greedy i<j, both removed (:347-356)
     if (lane < cnt) {
-        car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
+        car_corners_d(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], npc_len(nl, lane, dims),
+                      npc_wid(nl, lane, dims), nl.cx[lane], nl.cy[lane]);
         nl.col[lane] = 0ull;
     }
     wave_lds_sync();
@@ -1071,7 +1105,8 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const int a = cnt <= 8 ? (lane >> 3) : pi / cnt, b = cnt <= 8 ? (lane & 7) : pi % cnt;
             const int aa = a < cnt ? a : 0, bb = b < cnt ? b : 0;
             const float cdx = nl.x[aa] - nl.x[bb], cdy = nl.y[aa] - nl.y[bb];
-            const bool close = !(cdx * cdx + cdy * cdy > 3600.0f);  // circumcircles (cars_pre)
+            // circumcircles (cars_pre); cars of other sizes: every pair runs the SAT
+            const bool close = !(cdx * cdx + cdy * cdy > 3600.0f) || (dims && p.dims);
             if ((cnt <= 8 ? (a < cnt && b < cnt) : pi < cnt * cnt) && a < b && close &&
                 sat_collide(nl.cx[a], nl.cy[a], nl.c[a], nl.s[a], nl.cx[b], nl.cy[b], nl.c[b], nl.s[b]))
                 atomicOr(&nl.col[a], 1ull << b);
@@ -1102,22 +1137,26 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // (most steps erase nothing: the survivors already are the prefix 0 .. cnt - 1)
     if (keep_m != (cnt >= 64 ? ~0ull : ((1ull << cnt) - 1ull))) {
         const int dst = __builtin_popcountll(keep_m & ((1ull << lane) - 1ull));
-        float kx = 0, ky = 0, kv = 0, kh = 0, ka = 0, ks = 0, kc = 0, ksn = 0;
+        float kx = 0, ky = 0, kv = 0, kh = 0, ka = 0, ks = 0, kc = 0, ksn = 0, kl = 0, kw = 0;
         int kp = 0, kr = 0, ki = 0;
         if (keep) {
             kx = nl.x[lane]; ky = nl.y[lane]; kv = nl.v[lane]; kh = nl.h[lane]; ka = nl.acc[lane]; ks = nl.steer[lane];
             kc = nl.c[lane]; ksn = nl.s[lane]; kp = nl.pidx[lane]; kr = nl.route[lane]; ki = nl.intent[lane];
+            kl = npc_len(nl, lane, dims); kw = npc_wid(nl, lane, dims);
         }
         wave_lds_sync();
         if (keep) {
             nl.x[dst] = kx; nl.y[dst] = ky; nl.v[dst] = kv; nl.h[dst] = kh; nl.acc[dst] = ka; nl.steer[dst] = ks;
             nl.c[dst] = kc; nl.s[dst] = ksn; nl.pidx[dst] = kp; nl.route[dst] = kr; nl.intent[dst] = ki; nl.alive[dst] = 1;
+            if constexpr (NL::kDims) { nl.len[dst] = kl; nl.wid[dst] = kw; }
         }
         wave_lds_sync();
     }
     // store back + corners of the survivors (for ego-NPC SAT)
     npc_writeback(p, e, nl, newcnt, lane);
-    if (lane < newcnt) car_corners(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], nl.cx[lane], nl.cy[lane]);
+    if (lane < newcnt)
+        car_corners_d(nl.x[lane], nl.y[lane], nl.c[lane], nl.s[lane], npc_len(nl, lane, dims),
+                      npc_wid(nl, lane, dims), nl.cx[lane], nl.cy[lane]);
     wave_lds_sync();
 #ifdef MEV_STAMPS_N
     NT(7);  // collisions, erase, store
@@ -1228,6 +1267,8 @@ struct CarsLDS {
     // k_step without traffic (null otherwise): 5 KB for the LDS path windows of the car
     // part's first pass, inside the LiDAR pool's region (free until the LiDAR runs)
     float4* win;
+    // dims handles only (null otherwise): each ego's length / width (Car::length / width)
+    float *len, *wid;
 };
 
 __host__ __device__ constexpr size_t lds_al(size_t b) { return (b + 15) & ~size_t(15); }
@@ -1235,13 +1276,14 @@ __host__ __device__ constexpr size_t lds_al(size_t b) { return (b + 15) & ~size_
 // NPC slots that need obstacle entries in k_cars' LDS (none without traffic)
 __host__ __device__ inline int cars_k(const SimParams& p) { return p.traffic ? p.K : 0; }
 
-__host__ __device__ constexpr size_t cars_lds_bytes(int N, int K) {
+// dims: the handle has cars of other sizes (two more per-ego arrays at the end)
+__host__ __device__ constexpr size_t cars_lds_bytes(int N, int K, bool dims = false) {
     const size_t n = (size_t)N, ob = (size_t)(N + K);
     return 22 * lds_al(n * 4) + 2 * lds_al(n * 16) + 3 * lds_al(n * 4) + 4 * lds_al(n) + lds_al(n * 8) +
-           lds_al(ob * 16) + 3 * lds_al(ob * 4) + lds_al(n * 16);
+           lds_al(ob * 16) + 3 * lds_al(ob * 4) + lds_al(n * 16) + (dims ? 2 * lds_al(n * 4) : 0);
 }
 
-__device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
+__device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K, bool dims = false) {
     const size_t n = (size_t)N, ob = (size_t)(N + K);
     CarsLDS L;
     unsigned char* q = base;
@@ -1265,6 +1307,12 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
     L.py = reinterpret_cast<float*>(take(ob * 4));
     L.ph = reinterpret_cast<float*>(take(ob * 4));
     L.cand = reinterpret_cast<unsigned long long*>(take(n * 16));
+    L.len = nullptr;
+    L.wid = nullptr;
+    if (dims) {
+        L.len = reinterpret_cast<float*>(take(n * 4));
+        L.wid = reinterpret_cast<float*>(take(n * 4));
+    }
     L.head = nullptr;
     L.rel = nullptr;
     L.envw = nullptr;
@@ -1277,7 +1325,7 @@ __device__ inline CarsLDS carve_cars_lds(unsigned char* base, int N, int K) {
 // slot i is global agent e * NE + i); spawn poses, intent, alive and route only
 // for envs reset this step (do_reset: the lane's env)
 __device__ __forceinline__ void ego_writeback(const SimParams& p, int e, int NE, int N, const CarsLDS& el,
-                                              bool do_reset, int tid) {
+                                              bool do_reset, int tid, bool dims = false) {
     for (int i = tid; i < N; i += WAVE) {
         const int g = e * NE + i;
         egof(p, EF_X)[g] = el.x[i]; egof(p, EF_Y)[g] = el.y[i]; egof(p, EF_V)[g] = el.v[i]; egof(p, EF_H)[g] = el.h[i];
@@ -1286,6 +1334,10 @@ __device__ __forceinline__ void ego_writeback(const SimParams& p, int e, int NE,
         if (do_reset) {
             egof(p, EF_SX)[g] = el.sx[i]; egof(p, EF_SY)[g] = el.sy[i]; egof(p, EF_SV)[g] = el.sv[i]; egof(p, EF_SH)[g] = el.sh[i];
             egoi(p, EF_INTENT)[g] = el.intent[i]; gmem(p.ego.alive)[g] = el.alive[i]; egoi(p, EF_ROUTE)[g] = el.route[i];
+            if (dims) {  // reset + add_car_with_route: new Cars of the default size (Car.h:19-20)
+                gmem(p.ego_dim)[2 * g] = CAR_LENGTH;
+                gmem(p.ego_dim)[2 * g + 1] = CAR_WIDTH;
+            }
         }
     }
 }
@@ -1313,11 +1365,20 @@ struct CarsCtx {
 // the respawned egos (el.envw[6]) at the end and passes workgroup barrier B.
 // EARLY: phase 1's first path windows come by LDS DMA from group-layout route /
 // index registers loaded in the state round (k_step without traffic).
-template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false>
+// DIMS: the kernel can run a handle whose cars have other sizes than 54 x 24 px
+// (k_cars, k_step<NM = 0>); p.dims then says whether this one does, and the car
+// corners, the SAT pre-test and the LiDAR boxes take each car's length / width.
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false, bool DIMS = false>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
                                             const CarsLDS& el, NL* nl) {
     static_assert(!ESPLIT || (FUSED && !TRAFFIC), "early split: k_step without traffic");
     static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
+    static_assert(!DIMS || (PK == 1 && !EARLY && !ESPLIT), "per-car sizes: the runtime-layout kernels");
+    static_assert(!TRAFFIC || NL::kDims == DIMS, "NPC sizes in LDS exactly when the kernel handles them");
+    // (a DIMS kernel keeps every car's size: all 54 x 24 unless p.dims; p.dims alone turns
+    // off the SAT's circumcircle pre-test, which assumes that size)
+    constexpr bool dims = DIMS;
+    const bool all_pairs = DIMS && p.dims;
     // One wave per env: the order-dependent per-env logic (NPCs, kinematics,
     // status, collisions, respawn, observation head); the LiDAR block of the
     // observation is filled by the LiDAR body right after.  Per-agent phases run on
@@ -1362,6 +1423,11 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     const float sh0 = ldu(egof(p, EF_SH), ug);
     const int pidx_l = ldu(egoi(p, EF_PIDX), ug), intent_l = ldu(egoi(p, EF_INTENT), ug);
     const uint8_t alive_l = ldu(gmem(p.ego.alive), ug);
+    float len_l = CAR_LENGTH, wid_l = CAR_WIDTH;
+    if constexpr (DIMS) {
+        len_l = ldu(gmem(p.ego_dim), 2 * ug);
+        wid_l = ldu(gmem(p.ego_dim), 2 * ug + 1);
+    }
     // phase 1's first pass in group layout (lane (grp, sub): agent grp), without
     // traffic (there the NPC phase runs in between, and the window registers would
     // stay live through it): the agent's route, path index and env reset flag
@@ -1399,7 +1465,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         rl1 = ldu(gmem(p.rel_angles), (uint32_t)(tid + WAVE < rmax ? tid + WAVE : rmax));
     }
     NpcRegs nreg{};
-    if constexpr (TRAFFIC) nreg = npc_load(p, e, tid);  // in flight with the ego loads
+    if constexpr (TRAFFIC) nreg = npc_load<DIMS>(p, e, tid);  // in flight with the ego loads
     // every load above is issued before any of their values is used (a use scheduled
     // between them would put a wait for the first loads in front of the rest)
     __builtin_amdgcn_sched_barrier(0);
@@ -1417,6 +1483,10 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         el.pa0[il] = pa00; el.pa1[il] = pa10;
         el.sx[il] = sx0; el.sy[il] = sy0; el.sv[il] = sv0; el.sh[il] = sh0;
         el.pidx[il] = pidx_l; el.intent[il] = intent_l; el.alive[il] = alive_l;
+    }
+    if (DIMS && lane_on) {  // an env being reset gets new Cars of the default size (Car.h:19-20)
+        el.len[il] = do_reset ? CAR_LENGTH : len_l;
+        el.wid[il] = do_reset ? CAR_WIDTH : wid_l;
     }
     if constexpr (FUSED && !ESPLIT) {
         if (p.R <= 2 * WAVE) {
@@ -1484,6 +1554,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     STAMP(0);
     int ncnt = 0;
     if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg);
+
     if (TRAFFIC && FUSED) {
         // the envs with many NPCs set the kernel's end: the rest of their step goes first
         // (3 or more NPCs: level 2, 6 or more: 3; config 4 +1.4 % over a fixed level)
@@ -1588,7 +1659,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         float rew = 0.0f, cur = 0.0f, an = 0.0f, sn = 0.0f;
         bool succ = false;
         float ccx[4], ccy[4];
-        car_corners(k.x, k.y, cH, sH, ccx, ccy);
+        car_corners_d(k.x, k.y, cH, sH, (dims ? el.len[ii] : CAR_LENGTH), (dims ? el.wid[ii] : CAR_WIDTH), ccx, ccy);
         {  // (branch-free: every lane evaluates the terms, a dead agent's are zeroed)
             // compute_progress / compute_stuck / compute_smooth (:15-46)
             cur = hypotf(k.x - pend.x, k.y - pend.y);
@@ -1682,7 +1753,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             // (2 x 29.55 px; 60 px with margin for the rounding of the corners) cannot
             // overlap: the SAT runs only for lanes (and waves) with a close pair
             const float cdx = el.x[a] - el.x[b], cdy = el.y[a] - el.y[b];
-            const bool close = !(cdx * cdx + cdy * cdy > 3600.0f);
+            const bool close = !(cdx * cdx + cdy * cdy > 3600.0f) || all_pairs;  // (other sizes: every pair)
             if (a < b && (PK == 1 || a / NE == b / NE) && el.alive[a] && el.alive[b] && close &&
                 sat_collide(reinterpret_cast<const float*>(&el.cx[a]), reinterpret_cast<const float*>(&el.cy[a]),
                             el.c[a], el.s[a], reinterpret_cast<const float*>(&el.cx[b]),
@@ -1696,7 +1767,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             if (pi < N * ncnt) {
                 const int a = pi / ncnt, b = pi % ncnt;
                 const float cdx = el.x[a] - nl->x[b], cdy = el.y[a] - nl->y[b];
-                const bool close = !(cdx * cdx + cdy * cdy > 3600.0f);  // as for the ego pairs
+                const bool close = !(cdx * cdx + cdy * cdy > 3600.0f) || all_pairs;  // as for the ego pairs
                 if (el.alive[a] && close && sat_collide(reinterpret_cast<const float*>(&el.cx[a]),
                                                reinterpret_cast<const float*>(&el.cy[a]), el.c[a], el.s[a],
                                                nl->cx[b], nl->cy[b], nl->c[b], nl->s[b]))
@@ -1762,10 +1833,16 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     const int nob = lone ? 0 : N + ncnt;  // lone egos: no obstacle anyone could see
     const int OB = p.ob_stride;
     for (int o = tid; o < nob; o += WAVE) {
-        float x, y, h, c, s;
-        if (o < N) { x = el.x[o]; y = el.y[o]; h = el.h[o]; c = el.c[o]; s = el.s[o]; }
-        else { const int k = o - N; x = nl->x[k]; y = nl->y[k]; h = nl->h[k]; c = nl->c[k]; s = nl->s[k]; }
-        const PxBox bx = aabb_px(x, y, c, s);
+        float x, y, h, c, s, bl = CAR_LENGTH, bw = CAR_WIDTH;
+        if (!TRAFFIC || o < N) {  // (no NPC branch without traffic: nl is null there)
+            x = el.x[o]; y = el.y[o]; h = el.h[o]; c = el.c[o]; s = el.s[o];
+            if (dims) { bl = el.len[o]; bw = el.wid[o]; }
+        } else {
+            const int k = o - N;
+            x = nl->x[k]; y = nl->y[k]; h = nl->h[k]; c = nl->c[k]; s = nl->s[k];
+            if constexpr (TRAFFIC && DIMS) { bl = nl->len[k]; bw = nl->wid[k]; }
+        }
+        const PxBox bx = aabb_px_d(x, y, c, s, bl, bw);
         const int4 b4 = make_int4(bx.x0, bx.x1, bx.y0, bx.y1);
         el.box[o] = b4;
         el.px[o] = x; el.py[o] = y; el.ph[o] = h;
@@ -1812,7 +1889,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
 // k_cars): bonuses, team mix and env flags (:320-370), the reward / done /
 // status outputs and the state write-back, the observation head (:418-520).
 // Reads only the car LDS (the LiDAR never writes it).
-template <bool TRAFFIC, bool FUSED, class NL, int PK = 1>
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool DIMS = false>
 __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out, const int e, const CarsLDS& el,
                                           const NL* nl, CarsCtx& cx) {
     const int tid = threadIdx.x & (WAVE - 1);
@@ -1894,7 +1971,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
         }
     }
     // ---- the final ego state back to HBM (lane = agent)
-    ego_writeback(p, e, NE, N, el, do_reset, tid);
+    ego_writeback(p, e, NE, N, el, do_reset, tid, DIMS);
     if (out.state) {
         // the state gather format: the post-step state the root rebuilds the head from
         // (launch_decode_state), instead of the head itself
@@ -2013,13 +2090,13 @@ __global__ __launch_bounds__(WAVE) void k_cars(SimParams p, StepInputs in, Outpu
 #if defined(MEV_STAMPS_R)
     STAMP_RAW(0);
 #endif
-    const CarsLDS el = carve_cars_lds(cars_lds, p.N, cars_k(p));
+    const CarsLDS el = carve_cars_lds(cars_lds, p.N, cars_k(p), true);
     __shared__ typename std::conditional<TRAFFIC, NpcLDS, char>::type nl_storage;
     NpcLDS* nl = nullptr;
     if constexpr (TRAFFIC) nl = &nl_storage;
-    CarsCtx cx = cars_pre<TRAFFIC, false>(p, in, out, e, el, nl);
+    CarsCtx cx = cars_pre<TRAFFIC, false, NpcLDS, 1, false, false, true>(p, in, out, e, el, nl);
     wave_lds_sync();
-    cars_post<TRAFFIC, false>(p, out, e, el, nl, cx);
+    cars_post<TRAFFIC, false, NpcLDS, 1, true>(p, out, e, el, nl, cx);
 }
 
 // ------------------------------------------------------------- LiDAR ---
@@ -2805,7 +2882,7 @@ struct StepLayout {
 };
 __host__ __device__ inline StepLayout step_layout(const SimParams& p) {
     StepLayout L;
-    int off = (int)lds_al(cars_lds_bytes(p.N, cars_k(p)));
+    int off = (int)lds_al(cars_lds_bytes(p.N, cars_k(p), true));  // (k_step<NM = 0> keeps the car sizes)
     L.head = off;  // (no staged heads: the car part writes its rows' heads itself)
     L.rel = off; off += (int)lds_al((size_t)p.R * 4);
     L.envw = off; off += 32;
@@ -2846,7 +2923,8 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
     // R <= 128 puts every pool (step_pool agents) within the layout's beams
     const bool npcs = KM == 0 ? !p.traffic : (p.traffic && p.K <= KM);
     const size_t npc_lds = KM == 0 ? 0 : sizeof(NpcLDST<(KM ? KM : 1)>);
-    return p.N <= NM && p.R <= kFixedRays && npcs &&
+    // (a handle with cars of other sizes runs the runtime layout, NM = 0)
+    return p.N <= NM && p.R <= kFixedRays && npcs && !p.dims &&
            (size_t)FixedLayout<NM, KM>::bytes + npc_lds <= 10 * 1024;
 }
 
@@ -3026,6 +3104,8 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
             egof(p, EF_ACC)[g] = 0.0f; egof(p, EF_STEER)[g] = 0.0f; egof(p, EF_PREV_DIST)[g] = 0.0f;
             egof(p, EF_PA0)[g] = 0.0f; egof(p, EF_PA1)[g] = 0.0f; egoi(p, EF_PIDX)[g] = 0;
             egoi(p, EF_INTENT)[g] = gmem(p.rt.intent)[rid]; gmem(p.ego.alive)[g] = 1;
+            gmem(p.ego_dim)[2 * g] = CAR_LENGTH;  // reset + add_car_with_route: new Cars of the
+            gmem(p.ego_dim)[2 * g + 1] = CAR_WIDTH;  // default size (Car.h:19-20)
         }
         el.x[i] = egof(p, EF_X)[g]; el.y[i] = egof(p, EF_Y)[g]; el.v[i] = egof(p, EF_V)[g]; el.h[i] = egof(p, EF_H)[g];
         el.alive[i] = gmem(p.ego.alive)[g]; el.intent[i] = egoi(p, EF_INTENT)[g]; el.pidx[i] = egoi(p, EF_PIDX)[g];
@@ -3064,7 +3144,7 @@ static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Ou
     // k_cars then k_lidar over the envs [e0, e1)
     if (e1 <= e0) return hipSuccess;
     if (ev) (void)hipEventRecord(ev[0], s);
-    const unsigned cars_lds = (unsigned)cars_lds_bytes(p.N, cars_k(p));
+    const unsigned cars_lds = (unsigned)cars_lds_bytes(p.N, cars_k(p), true);
     if (p.traffic) hipLaunchKernelGGL(k_cars<true>, dim3(e1 - e0), dim3(WAVE), cars_lds, s, p, in, out, e0);
     else hipLaunchKernelGGL(k_cars<false>, dim3(e1 - e0), dim3(WAVE), cars_lds, s, p, in, out, e0);
     hipError_t e = hipGetLastError();
@@ -3100,7 +3180,8 @@ static int fused_npc_cap(const SimParams& p) { return p.K <= 32 ? 32 : 64; }
 // step_pool(p) agents) plus, with traffic, the static NPC arrays
 static size_t fused_lds_bytes(const SimParams& p) {
     size_t b = (size_t)step_layout(p).bytes;
-    if (p.traffic) b += fused_npc_cap(p) == 32 ? sizeof(NpcLDST<32>) : sizeof(NpcLDST<64>);
+    // (the runtime-layout traffic kernels hold the NPC sizes too: NpcLDST<KM, true>)
+    if (p.traffic) b += fused_npc_cap(p) == 32 ? sizeof(NpcLDST<32, true>) : sizeof(NpcLDST<64, true>);
     return b;
 }
 
@@ -3239,7 +3320,7 @@ hipError_t launch_step(const SimParams& p, const SimParams* dp, const StepInputs
 // one ego with <= 32 NPC slots -- and, for more NPC slots (env.py's 64), the
 // dynamic traffic layout, which at one env may take more than a wave's 10 KB share
 bool serve_fits(const SimParams& p) {
-    if (step_kernel_for(p) == 0 || p.step_kernel == 1) return false;
+    if (step_kernel_for(p) == 0 || p.step_kernel == 1 || p.dims) return false;
     if (p.E > kServeMaxWG) return false;
     if (p.traffic) return fixed_fits<1, 32>(p) || (p.K > 32 && fused_fits(p));
     return fixed_fits<8, 0>(p) && step_pack(p) == 1 && !step_esplit(p) && p.step_split != 1;
@@ -3340,10 +3421,17 @@ __global__ __launch_bounds__(WAVE) void k_decode_state(SimParams p, const uint8_
             for (int q = 0; q < OBS_HEAD; ++q) row[q] = 0.0f;
             continue;
         }
-        const int rt = route < 0 ? 0 : (route >= p.rt.nroutes ? p.rt.nroutes - 1 : route);
+        // a route id this table does not have (a peer's mev_add_route; mev_comm_init checks
+        // the tables, so only a corrupt message gets here): counted (overflow[2]) and the
+        // look-ahead terms NaN, never a clamped route's point
+        const bool bad = route < 0 || route >= p.rt.nroutes;
+        if (bad) atomicAdd(p.overflow + 2, 1ull);
+        const int rt = bad ? 0 : route;
         const int ti = pidx + 10 < PATH_LEN - 1 ? (pidx + 10 < 0 ? 0 : pidx + 10) : PATH_LEN - 1;
         const float* path = p.rt.path + (size_t)rt * (2 * PATH_LEN);
-        write_obs_head_tg<false>(p, i, el, (const NpcLDS*)nullptr, 0, path[2 * ti], path[2 * ti + 1], row, false);
+        const float nan = __builtin_nanf("");
+        write_obs_head_tg<false>(p, i, el, (const NpcLDST<MAXK>*)nullptr, 0, bad ? nan : path[2 * ti],
+                                 bad ? nan : path[2 * ti + 1], row, false);
     }
     // LiDAR block and padding, every lane: (agent, column) pairs
     const int tail = D - OBS_HEAD;

@@ -101,10 +101,11 @@ MEV_HD bool is_line_px(int x, int y, int stop) {
     return (xband && yout) || (yband && xout);
 }
 
-// Car::corners, cpp/Car.cpp:86-103 (y-up rotation kept: SURVEY §7.3 quirk 6).
-MEV_HD void car_corners(float x, float y, float cosA, float sinA, float* cx, float* cy) {
-    const float hx = CAR_WIDTH * 0.5f;
-    const float hy = CAR_LENGTH * 0.5f;
+// Car::corners, cpp/Car.cpp:86-103 (y-up rotation kept: SURVEY §7.3 quirk 6), for a
+// car of length len and width wid (Car::length / Car::width, cpp/Car.h:19-20).
+MEV_HD void car_corners_d(float x, float y, float cosA, float sinA, float len, float wid, float* cx, float* cy) {
+    const float hx = wid * 0.5f;
+    const float hy = len * 0.5f;
     const float lx[4] = {hy, hy, -hy, -hy};
     const float ly[4] = {hx, -hx, -hx, hx};
 #pragma unroll
@@ -112,6 +113,10 @@ MEV_HD void car_corners(float x, float y, float cosA, float sinA, float* cx, flo
         cx[k] = x + lx[k] * cosA - ly[k] * sinA;
         cy[k] = y + lx[k] * sinA + ly[k] * cosA;
     }
+}
+// the reference's default 54 x 24 px car (constant-folded)
+MEV_HD void car_corners(float x, float y, float cosA, float sinA, float* cx, float* cy) {
+    car_corners_d(x, y, cosA, sinA, CAR_LENGTH, CAR_WIDTH, cx, cy);
 }
 
 // project + Car::check_collision, cpp/Car.cpp:105-141 (SAT on 4 axes).
@@ -230,9 +235,10 @@ MEV_HD void car_update_steered(Kin& k, float throttle, float new_steer, float ta
 struct PxBox {
     int x0, x1, y0, y1;
 };
-MEV_HD PxBox aabb_px(float x, float y, float cosA, float sinA) {
-    const float hl = CAR_LENGTH * 0.5f;
-    const float hw = CAR_WIDTH * 0.5f;
+// (len, wid: the car's Car::length / Car::width, Lidar.cpp:67-68)
+MEV_HD PxBox aabb_px_d(float x, float y, float cosA, float sinA, float len, float wid) {
+    const float hl = len * 0.5f;
+    const float hw = wid * 0.5f;
     const float ex = fabs_f(cosA) * hl + fabs_f(sinA) * hw;
     const float ey = fabs_f(sinA) * hl + fabs_f(cosA) * hw;
     PxBox b;
@@ -244,6 +250,9 @@ MEV_HD PxBox aabb_px(float x, float y, float cosA, float sinA) {
     b.y0 = (int)__builtin_ceilf(cl(ly));
     b.y1 = (int)__builtin_floorf(cl(hy_));
     return b;
+}
+MEV_HD PxBox aabb_px(float x, float y, float cosA, float sinA) {
+    return aabb_px_d(x, y, cosA, sinA, CAR_LENGTH, CAR_WIDTH);
 }
 
 }  // namespace mev

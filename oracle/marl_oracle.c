@@ -45,6 +45,7 @@ enum { ST_ALIVE = 0, ST_DEAD = 1, ST_SUCCESS = 2, ST_CRASH_WALL = 3, ST_CRASH_LI
 typedef struct {
     float x, y, v, h, acc, steer, sx, sy, sv, sh, prev_dist, pa0, pa1;
     int32_t path_index, route, intention, alive;
+    float len, wid; /* Car::length / Car::width, cpp/Car.h:19-20 (default 54 x 24) */
 } orc_car;
 
 typedef struct {
@@ -288,9 +289,9 @@ static void respawn(orc_car* c) {
     c->acc = 0.0f; c->steer = 0.0f;
 }
 
-/* Car::corners, cpp/Car.cpp:86-103 */
+/* Car::corners, cpp/Car.cpp:86-103 (the car's own width / length) */
 static void corners(const orc_car* c, float* px, float* py) {
-    const float hx = CAR_WIDTH * 0.5f, hy = CAR_LENGTH * 0.5f;
+    const float hx = c->wid * 0.5f, hy = c->len * 0.5f;
     const float ca = cosf(c->h), sa = sinf(c->h);
     const float lx[4] = {hy, hy, -hy, -hy}, ly[4] = {hx, -hx, -hx, hx};
     for (int k = 0; k < 4; ++k) {
@@ -344,7 +345,7 @@ static void lidar_update(const orc_env* e, const orc_car* self, int self_idx, co
                     if (j == self_idx) continue;
                     if (fabsf(c->x - cx) < 1e-3f && fabsf(c->y - cy) < 1e-3f && fabsf(c->h - hd) < 1e-3f) continue;
                     float ca = cosf(c->h), sa = sinf(c->h);
-                    float hl = CAR_LENGTH * 0.5f, hw = CAR_WIDTH * 0.5f;
+                    float hl = c->len * 0.5f, hw = c->wid * 0.5f; /* Lidar.cpp:67-68 */
                     float ex = fabsf(ca) * hl + fabsf(sa) * hw;
                     float ey = fabsf(sa) * hl + fabsf(ca) * hw;
                     if ((float)px >= c->x - ex && (float)px <= c->x + ex && (float)py >= c->y - ey && (float)py <= c->y + ey) {
@@ -497,6 +498,7 @@ static void spawn_npc(orc_env* e, int troute) {
     c.h = atan2f(-(p[3] - p[1]), p[2] - p[0]);
     c.sx = c.x; c.sy = c.y; c.sv = 0.0f; c.sh = c.h;
     c.alive = 1; c.intention = e->intent[rid]; c.route = rid; c.path_index = 0;
+    c.len = CAR_LENGTH; c.wid = CAR_WIDTH; /* a new Car, cpp/Car.h:19-20 */
     e->npc[e->nnpc++] = c;
 }
 
@@ -671,6 +673,7 @@ void orc_reset(orc_env* e, const int* routes) {
         c->h = atan2f(-(p[3] - p[1]), p[2] - p[0]);
         c->sx = c->x; c->sy = c->y; c->sv = 0.0f; c->sh = c->h;
         c->alive = 1; c->intention = e->intent[r];
+        c->len = CAR_LENGTH; c->wid = CAR_WIDTH; /* a new Car, cpp/Car.h:19-20 */
         for (int b = 0; b < e->rays; ++b) e->lidar[i * e->rays + b] = e->maxd;
     }
     e->nnpc = 0;

@@ -18,7 +18,15 @@ LIB = os.path.join(HERE, "_build", "libmarl_oracle.so")
 
 CAR_DTYPE = np.dtype([(n, np.float32) for n in ("x", "y", "v", "h", "acc", "steer", "sx", "sy", "sv", "sh",
                                                  "prev_dist", "pa0", "pa1")] +
-                     [(n, np.int32) for n in ("path_index", "route", "intention", "alive")])
+                     [(n, np.int32) for n in ("path_index", "route", "intention", "alive")] +
+                     [(n, np.float32) for n in ("len", "wid")])  # Car::length / width (Car.h:19-20)
+
+
+def new_cars(n: int) -> np.ndarray:
+    """n zeroed car records of the reference's default size (54 x 24 px, Car.h:19-20)."""
+    c = np.zeros(n, CAR_DTYPE)
+    c["len"], c["wid"] = 54.0, 24.0
+    return c
 
 _lib = None
 

@@ -45,6 +45,9 @@ struct Harness {
     // Route bookkeeping so the harness can name the route of every car.
     std::vector<std::vector<std::pair<float, float>>> npc_route_paths;  // index = traffic_routes idx
     std::vector<int> ego_route_of;  // per ego car, caller-provided tag
+    // paths of the caller's own, written into Car.path (cpp/bindings.cpp:29: a plain
+    // read-write member, assigned without Car::set_path, so path_index stays)
+    std::vector<std::vector<std::pair<float, float>>> custom_paths;
     int lidar_rays{96};
     float lidar_fov{360.0f}, lidar_max{250.0f}, lidar_step{4.0f};
     explicit Harness(int lanes) : env(lanes) {}
@@ -60,9 +63,12 @@ struct Harness {
             }
         }
     }
+    // the traffic-route index of an NPC's path, 1000 + k for custom path k, or -1
     int npc_route_index(const Car& c) const {
         for (size_t i = 0; i < npc_route_paths.size(); ++i)
             if (npc_route_paths[i] == c.path) return int(i);
+        for (size_t i = 0; i < custom_paths.size(); ++i)
+            if (custom_paths[i] == c.path) return 1000 + int(i);
         return -1;
     }
     // Same LiDAR construction as cpp/IntersectionEnv.cpp:111-128, with R rays.
@@ -221,6 +227,26 @@ int rh_add_npc(void* p, int route, const float* f, const int32_t* i) {
     rec_to_car(f, i, c);
     h->env.traffic_cars.push_back(std::move(c));
     h->env.traffic_lidars.emplace_back();
+    return 0;
+}
+
+// A path of the caller's own (n points, xy interleaved); returns its index.
+int rh_add_custom_path(void* p, const float* xy, int n) {
+    auto* h = static_cast<Harness*>(p);
+    std::vector<std::pair<float, float>> path;
+    for (int k = 0; k < n; ++k) path.emplace_back(xy[2 * k], xy[2 * k + 1]);
+    h->custom_paths.push_back(std::move(path));
+    return int(h->custom_paths.size()) - 1;
+}
+
+// Car.path = custom path `custom` of ego k (which 0) or NPC k (which 1): the member
+// assignment pybind's def_readwrite performs (cpp/bindings.cpp:29), nothing else changes.
+int rh_set_car_path(void* p, int which, int k, int custom) {
+    auto* h = static_cast<Harness*>(p);
+    if (custom < 0 || size_t(custom) >= h->custom_paths.size()) return 1;
+    auto& v = which == 0 ? h->env.cars : h->env.traffic_cars;
+    if (k < 0 || size_t(k) >= v.size()) return 1;
+    v[size_t(k)].path = h->custom_paths[size_t(custom)];
     return 0;
 }
 

@@ -58,6 +58,8 @@ def lib():
         L.rh_add_npc.argtypes = [vp, i, fp, ip]
         L.rh_get_lidar.argtypes = [vp, fp]
         L.rh_route_path.argtypes = [vp, i, fp]
+        L.rh_add_custom_path.argtypes = [vp, fp, i]
+        L.rh_set_car_path.argtypes = [vp, i, i, i]
         L.rh_geometry_grid.argtypes = [i, ctypes.POINTER(ctypes.c_uint8)]
         L.rh_is_on_road.argtypes = [i, f, f]
         L.rh_hits_yellow_line.argtypes = [i, f, f]
@@ -145,6 +147,16 @@ class RefEnv:
         f = np.ascontiguousarray(f, np.float32)
         i = np.ascontiguousarray(i, np.int32)
         return lib().rh_add_npc(self.h, int(route), _f(f), _i(i))
+
+    def add_custom_path(self, path: np.ndarray) -> int:
+        """A path of the caller's own (n x 2); returns its index (NPCs on it report route 1000 + index)."""
+        a = np.ascontiguousarray(path, np.float32).reshape(-1, 2)
+        return lib().rh_add_custom_path(self.h, _f(a), len(a))
+
+    def set_car_path(self, which: int, k: int, custom: int):
+        """Car.path = custom path `custom` (ego k: which 0, NPC k: which 1), as pybind's setter does."""
+        if lib().rh_set_car_path(self.h, int(which), int(k), int(custom)) != 0:
+            raise IndexError("bad car or custom path index")
 
     def route_path(self, route: int) -> np.ndarray:
         out = np.zeros((512, 2), np.float32)

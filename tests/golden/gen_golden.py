@@ -6,6 +6,10 @@ unmodified reference simulator + our harness).  The .npz files it writes are
 committed; the GPU box never needs the reference.
 
     python tests/golden/gen_golden.py            # (re)writes every scenario
+    python tests/golden/gen_golden.py --check    # regenerates the deterministic scenarios into a
+                                                 # temporary directory and compares them with the
+                                                 # committed files, array by array, byte for byte
+    python tests/golden/gen_golden.py NAME ...   # (re)writes the named scenarios only
 
 Each scenario file holds the configuration (``meta`` JSON), the initial state
 the device path is loaded with, the per-step inputs (actions, and for traffic
@@ -30,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import refharness as R  # noqa: E402
 
 OUT = os.path.dirname(os.path.abspath(__file__))
+HERE = OUT
 
 ROUTES3 = [("IN_1", "OUT_4"), ("IN_2", "OUT_8"), ("IN_3", "OUT_12"), ("IN_4", "OUT_7"),
            ("IN_5", "OUT_11"), ("IN_6", "OUT_3"), ("IN_7", "OUT_10"), ("IN_8", "OUT_2"),
@@ -55,7 +60,10 @@ def policy(obs: np.ndarray, rng: np.random.Generator, target_v=3.5, noise=0.05) 
 def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_steps=2000,
         traffic=False, density=0.5, lanes=3, ego_routes=None, reward=None, steps=200,
         act="random", seed=0, dt=1.0 / 60.0, act_scale=1.0, zero_throttle_p=0.0,
-        inject=None, notes="", warmup=0, roundtrip=False):
+        inject=None, notes="", warmup=0, roundtrip=False, custom_paths=None, ego_paths=None):
+    """custom_paths: [C][160][2] paths of the caller's own (Car.path writes); ego_paths: per ego
+    the custom path written into its Car.path, or -1 (NPCs on custom path k, injected by
+    `inject`, record route 1000 + k)."""
     routes = ROUTES3 if lanes == 3 else ROUTES2
     if ego_routes is None:
         ego_routes = [routes[i % len(routes)] for i in range(n_agents)]
@@ -65,6 +73,13 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
     env.reset()
     for i, (s, e) in enumerate(ego_routes):
         assert env.add_car(s, e, tag=routes.index((s, e)) if (s, e) in routes else -1) == 0
+    cps = [] if custom_paths is None else [np.asarray(c, np.float32) for c in custom_paths]
+    for c in cps:
+        env.add_custom_path(c)
+    for i, k in enumerate(ego_paths or []):
+        if k >= 0:
+            env.set_car_path(0, i, k)  # Car.path = ... (cpp/bindings.cpp:29)
+    env.custom_paths = cps
     rng = np.random.default_rng(seed)
     if inject is not None:
         inject(env, rng)
@@ -121,6 +136,8 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
                 respawn=respawn, max_steps=max_steps, traffic=traffic, density=density,
                 reward=reward, ego_routes=ego_routes, traffic_routes=routes, dt=dt, steps=steps,
                 act=act, seed=seed, notes=notes, init_step=init_step, warmup=warmup, set_state=bool(roundtrip))
+    if cps:
+        meta["ego_paths"] = [int(k) for k in ego_paths or [-1] * n]
     arrays = dict(
         meta=np.array(json.dumps(meta)),
         init_ego_f=ef, init_ego_i=ei, init_npc_f=nf.reshape(-1, R.NF), init_npc_i=ni.reshape(-1, R.NI),
@@ -131,6 +148,8 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
     )
     if rays > 96:
         arrays["lidar"] = np.asarray(LD, np.float32)
+    if cps:
+        arrays["custom_paths"] = np.stack(cps).astype(np.float32)
     path = os.path.join(OUT, f"{name}.npz")
     np.savez_compressed(path, **arrays)
     env.close()
@@ -170,7 +189,9 @@ def inject_dead(env: R.RefEnv, rng: np.random.Generator):
             env.set_car(k, f[k], i[k])
 
 
-def inject_npcs(kcount: int):
+def inject_npcs(kcount: int, dims=None, custom=None):
+    """dims: (length, width) per injected NPC, cycled (default 54 x 24); custom: inject
+    NPC j on custom path custom[j] (>= 0) instead of a random traffic route."""
     def _inj(env: R.RefEnv, rng: np.random.Generator):
         """Place NPCs on points of random traffic routes (on their own path,
         path-aligned heading), at least 70 px apart and away from the ego."""
@@ -179,8 +200,10 @@ def inject_npcs(kcount: int):
         tries = 0
         while len(placed) < kcount + 1 and tries < 1000:
             tries += 1
+            j = len(placed) - 1
+            cj = custom[j] if custom is not None and j < len(custom) else -1
             route = int(rng.integers(0, 12))
-            path = env.route_path(route)
+            path = env.route_path(route) if cj < 0 else env.custom_paths[cj]
             idx = int(rng.integers(0, 150))
             x, y = float(path[idx, 0]), float(path[idx, 1])
             if min((x - px) ** 2 + (y - py) ** 2 for px, py in placed) < 70.0 ** 2:
@@ -191,11 +214,45 @@ def inject_npcs(kcount: int):
             f[2] = rng.uniform(0, 5)
             f[3] = math.atan2(-dy, dx) + rng.normal(0, 0.05)
             f[6], f[7], f[9] = path[0, 0], path[0, 1], math.atan2(-(path[1, 1] - path[0, 1]), path[1, 0] - path[0, 0])
-            f[13], f[14] = 54.0, 24.0
+            f[13], f[14] = (54.0, 24.0) if dims is None else dims[j % len(dims)]
             i = np.array([1, 0, max(0, idx - 2), route], np.int32)
             assert env.add_npc(route, f, i) == 0
+            if cj >= 0:  # Car.path = custom path cj (intention stays the route's, as a plain write)
+                env.set_car_path(1, env.k - 1, cj)
             placed.append((x, y))
     return _inj
+
+
+EGO_DIMS = [(80.0, 30.0), (40.0, 18.0), (54.0, 24.0), (70.0, 36.0), (30.0, 12.0), (110.0, 22.0), (60.0, 60.0),
+            (20.0, 40.0)]
+NPC_DIMS = [(90.0, 34.0), (36.0, 16.0), (54.0, 24.0), (66.0, 44.0), (120.0, 20.0)]
+
+
+def with_ego_dims(inject=None, dims=EGO_DIMS):
+    """Write Car.length / Car.width of every ego (cpp/bindings.cpp:24-25), after `inject`."""
+    def _inj(env: R.RefEnv, rng: np.random.Generator):
+        if inject is not None:
+            inject(env, rng)
+        f, i = env.cars(0)
+        for k in range(len(f)):
+            f[k, 13], f[k, 14] = dims[k % len(dims)]
+            env.set_car(k, f[k], i[k])
+    return _inj
+
+
+def bent_path(env: R.RefEnv, route: int, amp: float, waves: float = 1.5) -> np.ndarray:
+    """Traffic route `route`'s 160 points with a lateral sine offset (zero at both ends)."""
+    p = env.route_path(route).astype(np.float64)
+    t = np.linspace(0.0, 1.0, len(p))
+    d = np.gradient(p, axis=0)
+    nrm = np.stack([-d[:, 1], d[:, 0]], 1) / np.maximum(np.hypot(d[:, 0], d[:, 1]), 1e-9)[:, None]
+    off = amp * np.sin(np.pi * t) * np.sin(2.0 * np.pi * waves * t)
+    return (p + nrm * off[:, None]).astype(np.float32)
+
+
+def diag_path(x0, y0, x1, y1, n=160) -> np.ndarray:
+    t = np.linspace(0.0, 1.0, n, dtype=np.float64)
+    return np.stack([x0 + (x1 - x0) * t, y0 + (y1 - y0) * t], 1).astype(np.float32)
 
 
 def gen_static(lanes: int):
@@ -232,10 +289,56 @@ def gen_set_state():
     run("set_state_72_n3", n_agents=3, rays=96, steps=60, act="random", seed=21, warmup=40, roundtrip=True)
 
 
-def main():
-    if len(sys.argv) > 1 and sys.argv[1] == "--set-state":  # only the set_state scenarios
-        gen_set_state()
-        return
+def gen_dims():
+    """Per-car sizes (Car::length / Car::width, cpp/Car.h:19-20, read-write through
+    bindings.cpp:24-25): the status corners, the SAT and the LiDAR boxes of every car."""
+    for c in range(4):
+        run(f"dims_inject_egos_c{c}", n_agents=8, rays=64, steps=4, act="random", seed=400 + c,
+            inject=with_ego_dims(inject_random_egos))
+    run("dims_cfg3_policy", n_agents=8, rays=64, use_team=True, steps=300, act="policy", seed=410,
+        inject=with_ego_dims())
+    run("dims_respawn_off", n_agents=6, rays=96, respawn=False, steps=200, act="policy", seed=411,
+        inject=with_ego_dims(dims=EGO_DIMS[::-1]))
+    run("dims_npc_k7", n_agents=1, rays=64, traffic=True, density=0.0, steps=200, act="policy", seed=412,
+        inject=with_ego_dims(inject_npcs(7, dims=NPC_DIMS), dims=[(90.0, 30.0)]))
+
+
+def gen_dims_traffic():
+    """Sized egos and NPCs with the reference's (unseeded) spawns: recorded and replayed."""
+    run("dims_traffic_d5", n_agents=1, rays=64, traffic=True, density=5.0, steps=400, act="policy", seed=413,
+        inject=with_ego_dims(inject_npcs(4, dims=NPC_DIMS), dims=[(70.0, 30.0)]))
+
+
+def gen_paths():
+    """Written Car.path (cpp/bindings.cpp:29; every function reads a car's path through it)."""
+    env = R.RefEnv(num_lanes=3, traffic=True, density=0.0, routes=ROUTES3)
+    bent = [bent_path(env, 0, 14.0), bent_path(env, 4, 10.0, 2.0), bent_path(env, 7, 12.0, 1.0)]
+    env.close()
+    run("path_bent_egos", n_agents=4, rays=64, use_team=True, steps=200, act="policy", seed=420,
+        custom_paths=bent, ego_paths=[0, -1, 1, 2])
+    # a diagonal route across the box for the ego (from its own spawn: the path is written after
+    # add_car_with_route, so the car stays where that put it), an NPC on a bent traffic route
+    env = R.RefEnv(num_lanes=3, traffic=True, density=0.0, routes=ROUTES3)
+    p0 = env.route_path(5)
+    diag = diag_path(float(p0[0, 0]), float(p0[0, 1]), 520.0, 520.0)
+    bent_npc = bent_path(env, 9, 12.0)
+    env.close()
+    run("path_diag_npc", n_agents=1, rays=64, traffic=True, density=0.0, steps=200, act="policy", seed=421,
+        ego_routes=[ROUTES3[5]], custom_paths=[diag, bent_npc], ego_paths=[0],
+        inject=inject_npcs(3, custom=[1, -1, 1]))
+
+
+def gen_paths_traffic():
+    env = R.RefEnv(num_lanes=3, traffic=True, density=0.0, routes=ROUTES3)
+    bent_npc = bent_path(env, 2, 10.0, 2.0)
+    env.close()
+    run("path_npc_d2", n_agents=1, rays=64, traffic=True, density=2.0, steps=300, act="policy", seed=422,
+        custom_paths=[bent_npc], ego_paths=[-1], inject=inject_npcs(2, custom=[0, 0]))
+
+
+# (name prefix or scenario name, generator, deterministic).  Traffic with density > 0 draws
+# its spawns from the reference's unseeded RNG (TrafficFlow.cpp:278,324): not reproducible.
+def _core():
     gen_static(3)
     gen_static(2)
     # Config 1 shape: 1 env x 1 agent, 16 beams.
@@ -263,11 +366,6 @@ def main():
         dt=1.0 / 30.0, reward=[5.0, 2.0, -0.05, -7.0, -3.0, 4.0, -0.1, 0.5])
     # 2-lane layout.
     run("lanes2_policy", n_agents=7, rays=64, lanes=2, steps=300, act="policy", seed=11)
-    # Traffic mode (config 4 shape) with recorded spawns.
-    run("traffic_d05", n_agents=1, rays=64, traffic=True, density=0.5, steps=1500, act="policy", seed=12)
-    run("traffic_d5", n_agents=1, rays=64, traffic=True, density=5.0, steps=800, act="policy", seed=13)
-    run("traffic_d20", n_agents=1, rays=64, traffic=True, density=20.0, steps=500, act="policy", seed=14)
-    run("traffic_d20_random", n_agents=1, rays=64, traffic=True, density=20.0, steps=400, act="random", seed=15)
     # State injection.
     for c in range(6):
         run(f"inject_egos_c{c}", n_agents=8, rays=64, steps=3, act="random", seed=100 + c, inject=inject_random_egos)
@@ -276,6 +374,64 @@ def main():
         run(f"inject_npc_k{k}", n_agents=1, rays=64, traffic=True, density=0.0, steps=150, act="policy",
             seed=300 + k, inject=inject_npcs(k))
     gen_set_state()
+
+
+def _traffic():
+    # Traffic mode (config 4 shape) with recorded spawns.
+    run("traffic_d05", n_agents=1, rays=64, traffic=True, density=0.5, steps=1500, act="policy", seed=12)
+    run("traffic_d5", n_agents=1, rays=64, traffic=True, density=5.0, steps=800, act="policy", seed=13)
+    run("traffic_d20", n_agents=1, rays=64, traffic=True, density=20.0, steps=500, act="policy", seed=14)
+    run("traffic_d20_random", n_agents=1, rays=64, traffic=True, density=20.0, steps=400, act="random", seed=15)
+
+
+GROUPS = [("core", _core, True), ("dims", gen_dims, True), ("paths", gen_paths, True),
+          ("traffic", _traffic, False), ("dims_traffic", gen_dims_traffic, False),
+          ("paths_traffic", gen_paths_traffic, False)]
+
+
+def check() -> int:
+    """Regenerate every deterministic scenario into a temporary directory and compare each
+    array of each file with the committed one, byte for byte.  Returns the mismatch count."""
+    import tempfile
+    global OUT
+    bad = 0
+    with tempfile.TemporaryDirectory() as tmp:
+        OUT = tmp
+        for _, gen, det in GROUPS:
+            if det:
+                gen()
+        OUT = HERE
+        for fn in sorted(os.listdir(tmp)):
+            a = np.load(os.path.join(tmp, fn), allow_pickle=False)
+            path = os.path.join(HERE, fn)
+            if not os.path.exists(path):
+                print(f"MISSING {fn}")
+                bad += 1
+                continue
+            b = np.load(path, allow_pickle=False)
+            diff = sorted(set(a.files) ^ set(b.files))
+            diff += [k for k in sorted(set(a.files) & set(b.files))
+                     if a[k].dtype != b[k].dtype or a[k].shape != b[k].shape or a[k].tobytes() != b[k].tobytes()]
+            if diff:
+                print(f"DIFFERS {fn}: {diff}")
+                bad += 1
+    print(f"gen_golden --check: {bad} file(s) differ")
+    return bad
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--check":
+        sys.exit(1 if check() else 0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--set-state":  # only the set_state scenarios
+        gen_set_state()
+        return
+    if len(sys.argv) > 1:  # groups by name
+        for name, gen, _ in GROUPS:
+            if name in sys.argv[1:]:
+                gen()
+        return
+    for _, gen, _ in GROUPS:
+        gen()
 
 
 if __name__ == "__main__":

@@ -69,6 +69,52 @@ class Report:
             self.mismatches.append(msg)
 
 
+DEFAULT_DIMS = (54.0, 24.0)  # Car::length / Car::width defaults (cpp/Car.h:19-20)
+
+
+def custom_route_ids(h, d):
+    """Register scenario d's paths of the caller's own (Car.path writes) on handle / oracle h
+    (add_route); their ids, in the scenario's order."""
+    if "custom_paths" not in d:
+        return []
+    return [h.add_route(cp, 0) for cp in d["custom_paths"]]
+
+
+def ego_route_ids(h, d, L, cids):
+    """Each ego's route id: its lane route, or the custom path written into its Car.path."""
+    eps = d["meta"].get("ego_paths") or [-1] * int(d["meta"]["n_agents"])
+    return [cids[k] if k >= 0 else h.route_id(point_index(s, L), point_index(e, L))
+            for (s, e), k in zip(d["meta"]["ego_routes"], eps)]
+
+
+def npc_route_ids(rec_routes, troutes, cids):
+    """NPC route ids from the recorded route indexes (traffic route, or 1000 + custom path)."""
+    return [cids[r - 1000] if r >= 1000 else troutes[r] for r in rec_routes]
+
+
+def has_dims(d) -> bool:
+    """Whether scenario d writes Car::length / Car::width (record columns 13, 14)."""
+    f = [d["init_ego_f"], d["ego_f"].reshape(-1, d["ego_f"].shape[-1])]
+    if len(d["init_npc_f"]):
+        f.append(d["init_npc_f"])
+    return any(a.shape[-1] >= 15 and (np.any(a[:, 13] != DEFAULT_DIMS[0]) or np.any(a[:, 14] != DEFAULT_DIMS[1]))
+               for a in f)
+
+
+def set_dims(h, data):
+    """The scenarios' initial car sizes on envs 0..B-1 of handle h (mev_set_car_dims)."""
+    ego = np.empty((h.E, h.N, 2), np.float32)
+    npc = np.empty((h.E, h.K, 2), np.float32)
+    ego[...] = DEFAULT_DIMS
+    npc[...] = DEFAULT_DIMS
+    for b, d in enumerate(data):
+        ego[b] = d["init_ego_f"][:, 13:15]
+        k = len(d["init_npc_f"])
+        if k:
+            npc[b, :k] = d["init_npc_f"][:, 13:15]
+    h.set_car_dims(ego, npc)
+
+
 def make_handle(mod, meta, num_envs: int, device: int = 0):
     R = int(meta["rays"])
     return mod.Handle(num_envs=num_envs, num_agents=int(meta["n_agents"]), num_lanes=int(meta["num_lanes"]),
@@ -84,10 +130,10 @@ def single_env_handle(mod, d):
     meta = d["meta"]
     L = int(meta["num_lanes"])
     h = make_handle(mod, meta, 1)
+    cids = custom_route_ids(h, d)
     troutes = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["traffic_routes"]]
     h.set_traffic_routes(troutes)
-    ego_routes = np.array([[h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["ego_routes"]]],
-                          np.int32)
+    ego_routes = np.array([ego_route_ids(h, d, L, cids)], np.int32)
     h.set_ego_routes(ego_routes)
     st = h.get_state()
     f, i = d["init_ego_f"], d["init_ego_i"]
@@ -101,9 +147,11 @@ def single_env_handle(mod, d):
         for j, key in enumerate(NPC_F):
             st[key][0, :k] = nf[:, j]
         st["npc_alive"][0, :k], st["npc_intention"][0, :k], st["npc_path_index"][0, :k] = ni[:, 0], ni[:, 1], ni[:, 2]
-        st["npc_route"][0, :k] = [troutes[r] for r in ni[:, 3]]
+        st["npc_route"][0, :k] = npc_route_ids(ni[:, 3], troutes, cids)
     st["step_count"][0] = int(meta.get("init_step", 0))
     h.set_state(st)
+    if has_dims(d):
+        set_dims(h, [d])
     spawn_of = (lambda t: np.array([d["spawned"][t]], np.int32)) if meta["traffic"] else (lambda t: None)
     return h, spawn_of
 
@@ -134,12 +182,14 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
         h.set_step_pack(pack)  # envs per fused wave (scheduling only)
     if split:
         h.set_step_split(split)  # two waves per fused workgroup: 1 off, 2 on (scheduling only)
+    # paths of the caller's own: each scenario's, registered in turn (ids per scenario)
+    cids = [custom_route_ids(h, d) for d in data]
     troutes = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["traffic_routes"]]
     h.set_traffic_routes(troutes)
     n = int(meta["n_agents"])
     ego_routes = np.zeros((B, n), np.int32)
     for b, d in enumerate(data):
-        ego_routes[b] = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in d["meta"]["ego_routes"]]
+        ego_routes[b] = ego_route_ids(h, d, L, cids[b])
     h.set_ego_routes(ego_routes)
     # initial state
     st = h.get_state()
@@ -160,9 +210,12 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
             st["npc_alive"][b, :k] = ni[:, 0]
             st["npc_intention"][b, :k] = ni[:, 1]
             st["npc_path_index"][b, :k] = ni[:, 2]
-            st["npc_route"][b, :k] = [troutes[r] for r in ni[:, 3]]
+            st["npc_route"][b, :k] = npc_route_ids(ni[:, 3], troutes, cids[b])
         st["step_count"][b] = int(d["meta"].get("init_step", 0))  # set_state scenarios start mid-episode
     h.set_state(st)
+    dims = any(has_dims(d) for d in data)
+    if dims:
+        set_dims(h, data)
     reports = [Report(nm) for nm in names]
     obs0 = h.observations()
     for b, d in enumerate(data):
@@ -177,6 +230,7 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
             spawn = np.array([d["spawned"][t] for d in data], np.int32)
         h.step(acts, float(meta["dt"]), out=out, spawn_route=spawn)
         st = h.get_state()
+        cd = h.car_dims() if dims else None
         for b, d in enumerate(data):
             rep = reports[b]
             if not rep.ok and stop_at_first:
@@ -220,8 +274,12 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
                         rep.add(f"step {t + 1}: {key} {st[key][b, :kc]} vs {nf[:, j]}")
                 if not bits_equal(st["npc_path_index"][b, :kc], ni[:, 2]):
                     rep.add(f"step {t + 1}: npc path_index differ")
-                if not bits_equal(st["npc_route"][b, :kc], np.array([troutes[r] for r in ni[:, 3]], np.int32)):
+                if not bits_equal(st["npc_route"][b, :kc], np.array(npc_route_ids(ni[:, 3], troutes, cids[b]), np.int32)):
                     rep.add(f"step {t + 1}: npc route differ")
+                if cd is not None and not bits_equal(cd[1][b, :kc], nf[:, 13:15]):
+                    rep.add(f"step {t + 1}: npc length / width differ")
+            if cd is not None and not bits_equal(cd[0][b], ef[:, 13:15]):
+                rep.add(f"step {t + 1}: ego length / width differ")
         if stop_at_first and all(not r.ok for r in reports):
             break
     seq = h.npc_stats()[1]

@@ -11,7 +11,7 @@ import oracle as O  # noqa: E402
 
 
 def state_from_records(f, i, routes):
-    cars = np.zeros(len(f), O.CAR_DTYPE)
+    cars = O.new_cars(len(f))
     names = ["x", "y", "v", "h", "acc", "steer", "sx", "sy", "sv", "sh", "prev_dist", "pa0", "pa1"]
     for j, nm in enumerate(names):
         cars[nm] = f[:, j]
@@ -19,6 +19,8 @@ def state_from_records(f, i, routes):
     cars["intention"] = i[:, 1]
     cars["path_index"] = i[:, 2]
     cars["route"] = routes
+    if f.shape[1] >= 15:  # the recorded Car::length / Car::width (ref_harness.cpp car_to_rec)
+        cars["len"], cars["wid"] = f[:, 13], f[:, 14]
     return cars
 
 
@@ -35,12 +37,14 @@ def replay(name):
     meta = d["meta"]
     L = int(meta["num_lanes"])
     env = make_oracle(meta)
+    cids = G.custom_route_ids(env, d)
     tr = [env.route_id(G.point_index(s, L), G.point_index(e, L)) for s, e in meta["traffic_routes"]]
     env.set_traffic_routes(tr)
-    ego_routes = [env.route_id(G.point_index(s, L), G.point_index(e, L)) for s, e in meta["ego_routes"]]
+    ego_routes = G.ego_route_ids(env, d, L, cids)
     egos = state_from_records(d["init_ego_f"], d["init_ego_i"], ego_routes)
     k = len(d["init_npc_f"])
-    npcs = state_from_records(d["init_npc_f"], d["init_npc_i"], [tr[r] for r in d["init_npc_i"][:, 3]]) if k else []
+    npcs = state_from_records(d["init_npc_f"], d["init_npc_i"], G.npc_route_ids(d["init_npc_i"][:, 3], tr, cids)) \
+        if k else []
     env.set_state(egos, npcs, int(meta.get("init_step", 0)))
     errs = []
     if not G.bits_equal(env.observe()[:, :127], d["init_obs"]):
@@ -64,6 +68,13 @@ def replay(name):
                 errs.append(f"step {t + 1}: ego {nm}")
         if len(npcs) != int(d["npc_count"][t]):
             errs.append(f"step {t + 1}: npc count")
+        elif ef.shape[1] >= 15:  # car sizes move with their cars (NPC erase, resets)
+            if not (G.bits_equal(egos["len"], ef[:, 13]) and G.bits_equal(egos["wid"], ef[:, 14])):
+                errs.append(f"step {t + 1}: ego length / width")
+            kc = int(d["npc_count"][t])
+            if kc and not (G.bits_equal(npcs["len"], d["npc_f"][t, :kc, 13]) and
+                           G.bits_equal(npcs["wid"], d["npc_f"][t, :kc, 14])):
+                errs.append(f"step {t + 1}: npc length / width")
         if errs:
             break
     env.close()
@@ -79,7 +90,7 @@ NPC_FIELDS = {"x": "npc_x", "y": "npc_y", "v": "npc_v", "h": "npc_heading", "acc
               "intention": "npc_intention", "alive": "npc_alive"}
 
 
-def oracle_from_device_state(meta, st, e, traffic_routes=None):
+def oracle_from_device_state(meta, st, e, traffic_routes=None, dims=None):
     """An oracle env holding env e of a device handle's state (mev_get_state arrays, every hidden
     Car field included): the reference's IntersectionEnv with its cars / traffic_cars / step_count
     set to the same values (cpp/IntersectionEnv.cpp:394-416, set_state)."""
@@ -87,13 +98,16 @@ def oracle_from_device_state(meta, st, e, traffic_routes=None):
     if traffic_routes is not None:
         o.set_traffic_routes([int(r) for r in traffic_routes])
     n = int(meta["n_agents"])
-    cars = np.zeros(n, O.CAR_DTYPE)
+    cars = O.new_cars(n)
     for a, b in EGO_FIELDS.items():
         cars[a] = st[b][e]
     k = int(st["npc_count"][e])
-    npcs = np.zeros(k, O.CAR_DTYPE)
+    npcs = O.new_cars(k)
     for a, b in NPC_FIELDS.items():
         npcs[a] = st[b][e, :k]
+    if dims is not None:  # (ego [E][N][2], npc [E][K][2]) from Handle.car_dims()
+        cars["len"], cars["wid"] = dims[0][e, :, 0], dims[0][e, :, 1]
+        npcs["len"], npcs["wid"] = dims[1][e, :k, 0], dims[1][e, :k, 1]
     o.set_state(cars, npcs, int(st["step_count"][e]))
     return o
 
@@ -107,9 +121,16 @@ def check_step(tag, out, e, r):
     assert got == [r["terminated"], r["truncated"], r["agents_alive"], r["step"]], tag + ": flags"
 
 
-def check_state(tag, gst, e, o):
-    """The full ego / NPC state of env e (mev_get_state arrays) equals the oracle's, bit for bit."""
+def check_state(tag, gst, e, o, dims=None):
+    """The full ego / NPC state of env e (mev_get_state arrays) equals the oracle's, bit for bit
+    (and the car sizes, dims = Handle.car_dims(), when given)."""
     egos, npcs, sc = o.get_state()
+    if dims is not None:
+        assert G.bits_equal(dims[0][e, :, 0], egos["len"]) and G.bits_equal(dims[0][e, :, 1], egos["wid"]), \
+            f"{tag}: ego length / width"
+        k_ = len(npcs)
+        assert G.bits_equal(dims[1][e, :k_, 0], npcs["len"]) and G.bits_equal(dims[1][e, :k_, 1], npcs["wid"]), \
+            f"{tag}: npc length / width"
     for a, b in EGO_FIELDS.items():
         if a in egos.dtype.names:
             assert G.bits_equal(gst[b][e], egos[a]), f"{tag}: ego {a}"

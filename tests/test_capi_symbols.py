@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol(mev):
 
 def test_abi_and_defaults_without_gpu(mev):
     lib = mev.load_library()
-    assert lib.mev_abi_version() == 2  # 2: the state gather format
+    assert lib.mev_abi_version() == 3  # 3: per-car sizes, beam angles, snapshot format 2
     assert lib.mev_path_len() == 160
     cfg = mev._capi.default_config()
     # reference defaults: 96 beams (IntersectionEnv.cpp:113), RewardConfig (Reward.h:5-14), max_steps 2000

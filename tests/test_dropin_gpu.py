@@ -293,3 +293,41 @@ def test_cpp_backend_cars_setter_and_written_path():
         other.cars = c
     for env in envs + [other]:
         env.close()
+
+
+@pytest.mark.parametrize("name", ["dims_cfg3_policy", "dims_respawn_off", "path_bent_egos"])
+def test_cpp_backend_written_cars_replay_reference(name):
+    """MARLEnv-style writes through the read-write cars vector (cpp/bindings.cpp:24-25,29,66):
+    Car.length / Car.width and Car.path set on the cars add_car_with_route made, then the
+    recorded steps -- every output bit-exact against the reference, which recorded the same
+    writes (tests/golden/gen_golden.py gen_dims / gen_paths)."""
+    g = G.load(name)
+    meta = g["meta"]
+    env = cpp_backend.IntersectionEnv(meta["num_lanes"])
+    env.configure(meta["use_team"], meta["respawn"], meta["max_steps"])
+    env.reset()
+    for s, t in meta["ego_routes"]:
+        env.add_car_with_route(s, t)
+    env.lidars = [cpp_backend.Lidar(meta["rays"]) for _ in meta["ego_routes"]]
+    cars = env.cars
+    f = g["init_ego_f"]
+    eps = meta.get("ego_paths") or [-1] * len(cars)
+    for k, c in enumerate(cars):
+        c.length, c.width = float(f[k, 13]), float(f[k, 14])
+        if eps[k] >= 0:
+            c.path = [tuple(map(float, q)) for q in g["custom_paths"][eps[k]]]
+    env.cars = cars
+    back = env.cars
+    assert [(c.length, c.width) for c in back] == [(float(x), float(y)) for x, y in f[:, 13:15]]
+    assert G.bits_equal(env.get_observations(), g["init_obs"])
+    for t in range(len(g["actions"])):
+        a = g["actions"][t]
+        res = env.step(a[:, 0].tolist(), a[:, 1].tolist(), meta["dt"])
+        info = dict(agents_alive=res.agents_alive, step=res.step, status=res.status, done=res.done)
+        _check_step(name, g, t, res.obs, res.rewards, res.terminated, res.truncated, info)
+    # the sizes survive get_state / set_state into a fresh env (EnvState copies the Cars)
+    other = cpp_backend.IntersectionEnv(meta["num_lanes"])
+    other.set_state(env.get_state())
+    assert [(c.length, c.width) for c in other.cars] == [(c.length, c.width) for c in env.cars]
+    env.close()
+    other.close()

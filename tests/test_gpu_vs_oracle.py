@@ -36,7 +36,22 @@ CONFIGS = [
     # for egos and NPCs (NPCs spawn on them too: their first point)
     dict(name="custom_routes_n6", n=6, rays=64, custom=True),
     dict(name="custom_routes_traffic", n=3, rays=48, traffic=True, density=1.0, spawn_p=0.3, npcs=8, custom=True),
+    # per-car sizes (Car::length / Car::width, cpp/Car.h:19-20; mev_set_car_dims): egos and injected NPCs of
+    # random sizes, spawned NPCs of the default one; the runtime-layout kernels run these handles
+    dict(name="dims_n8_r64_team", n=8, rays=64, use_team=True, dims=True),
+    dict(name="dims_n2_r16", n=2, rays=16, dims=True),
+    dict(name="dims_traffic_n3", n=3, rays=48, traffic=True, density=2.0, spawn_p=0.3, npcs=9, dims=True),
+    dict(name="dims_traffic_n1", n=1, rays=64, traffic=True, density=0.5, spawn_p=0.2, npcs=12, npc_gap=45.0,
+         dims=True),
 ]
+
+
+def random_dims(rng, h):
+    """Random (length, width) per ego and NPC slot: 12..130 x 8..70 px, some at the default 54 x 24."""
+    ego = np.stack([rng.uniform(12, 130, (h.E, h.N)), rng.uniform(8, 70, (h.E, h.N))], -1).astype(np.float32)
+    npc = np.stack([rng.uniform(12, 130, (h.E, h.K)), rng.uniform(8, 70, (h.E, h.K))], -1).astype(np.float32)
+    ego[rng.uniform(size=(h.E, h.N)) < 0.25] = (54.0, 24.0)
+    return ego, npc
 
 
 def custom_routes(h):
@@ -123,7 +138,7 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=()):
     return st, troutes
 
 
-def _oracle_from_state(cfg, st, e, troutes, customs=()):
+def _oracle_from_state(cfg, st, e, troutes, customs=(), dims=None):
     n = cfg["n"]
     meta = dict(rays=cfg["rays"], num_lanes=cfg.get("lanes", 3), n_agents=n, use_team=cfg.get("use_team", False),
                 respawn=cfg.get("respawn", True), max_steps=cfg.get("max_steps", 2000),
@@ -133,18 +148,21 @@ def _oracle_from_state(cfg, st, e, troutes, customs=()):
     for path, intent in customs:
         o.add_route(path, intent)
     o.set_traffic_routes(troutes)
-    cars = np.zeros(n, R.O.CAR_DTYPE)
+    cars = R.O.new_cars(n)
     m = {"x": "x", "y": "y", "v": "v", "h": "heading", "acc": "acc", "steer": "steering", "sx": "spawn_x",
          "sy": "spawn_y", "sv": "spawn_v", "sh": "spawn_heading", "prev_dist": "prev_dist", "pa0": "prev_a0",
          "pa1": "prev_a1", "path_index": "path_index", "route": "route", "intention": "intention", "alive": "alive"}
     for a, b in m.items():
         cars[a] = st[b][e]
     k = int(st["npc_count"][e])
-    npcs = np.zeros(k, R.O.CAR_DTYPE)
+    npcs = R.O.new_cars(k)
     mn = {"x": "npc_x", "y": "npc_y", "v": "npc_v", "h": "npc_heading", "acc": "npc_acc", "steer": "npc_steering",
           "path_index": "npc_path_index", "route": "npc_route", "intention": "npc_intention", "alive": "npc_alive"}
     for a, b in mn.items():
         npcs[a] = st[b][e, :k]
+    if dims is not None:
+        cars["len"], cars["wid"] = dims[0][e, :, 0], dims[0][e, :, 1]
+        npcs["len"], npcs["wid"] = dims[1][e, :k, 0], dims[1][e, :k, 1]
     o.set_state(cars, npcs, int(st["step_count"][e]))
     return o
 
@@ -155,7 +173,7 @@ def test_random_states_match_oracle(mev, cfg, kernel):
     _random_states_vs_oracle(mev, cfg, kernel)
 
 
-PACKED = [c for c in CONFIGS if c["n"] <= 4 and not c.get("traffic")]
+PACKED = [c for c in CONFIGS if c["n"] <= 4 and not c.get("traffic") and not c.get("dims")]
 
 
 @pytest.mark.parametrize("pack", [2, 4, 8])
@@ -167,8 +185,8 @@ def test_random_states_match_oracle_packed_waves(mev, cfg, pack):
 
 
 @pytest.mark.parametrize("pack", [1, 2, 4])
-@pytest.mark.parametrize("cfg", [c for c in CONFIGS if not c.get("traffic")],
-                         ids=[c["name"] for c in CONFIGS if not c.get("traffic")])
+@pytest.mark.parametrize("cfg", [c for c in CONFIGS if not c.get("traffic") and not c.get("dims")],
+                         ids=[c["name"] for c in CONFIGS if not c.get("traffic") and not c.get("dims")])
 def test_random_states_match_oracle_early_split(mev, cfg, pack):
     """The early split (mev_set_step_split(3): the LiDAR wave computes the poses
     after Car::update itself and marches the road beside the car part), `pack`
@@ -209,7 +227,13 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0):
         assert G.bits_equal(got[0], path) and got[1] == intent and tuple(got[2][:2]) == tuple(path[0])
     st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0), extra)
     h.set_traffic_routes(troutes)
-    oracles = [_oracle_from_state(cfg, st, e, troutes, customs) for e in range(E)]
+    dims = None
+    if cfg.get("dims"):
+        dims = random_dims(rng, h)
+        h.set_car_dims(*dims)
+        assert h.car_dims_active()
+        assert all(G.bits_equal(a, b) for a, b in zip(h.car_dims(), dims))
+    oracles = [_oracle_from_state(cfg, st, e, troutes, customs, dims) for e in range(E)]
     obs0 = h.observations()
     for e in range(E):
         assert G.bits_equal(obs0[e], oracles[e].observe()), f"env {e}: observation after set_state"
@@ -224,6 +248,7 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0):
             spawn = np.where(rng.uniform(size=E) < cfg["spawn_p"], rng.integers(0, len(troutes), E), -1).astype(np.int32)
         h.step(acts, dt, out=out, spawn_route=spawn)
         gst = h.get_state()
+        cd = h.car_dims() if dims is not None else None
         for e in range(E):
             r = oracles[e].step(acts[e], dt, int(spawn[e]) if spawn is not None else -1)
             tag = f"{cfg['name']} env {e} step {t + 1}"
@@ -239,6 +264,9 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0):
             k = len(npcs)
             if k:
                 assert G.bits_equal(gst["npc_x"][e, :k], npcs["x"]) and G.bits_equal(gst["npc_v"][e, :k], npcs["v"]), tag
+            if cd is not None:  # sizes move with their cars (NPC erase, spawns of the default size)
+                assert G.bits_equal(cd[0][e, :, 0], egos["len"]) and G.bits_equal(cd[0][e, :, 1], egos["wid"]), tag
+                assert G.bits_equal(cd[1][e, :k, 0], npcs["len"]) and G.bits_equal(cd[1][e, :k, 1], npcs["wid"]), tag
     if cfg.get("expect_seq"):
         assert h.npc_stats()[1] > 0, "the controller's sequential fallback never ran"
     h.close()

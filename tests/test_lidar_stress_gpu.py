@@ -76,13 +76,13 @@ def _oracle_obs(case, st, e, D):
     n = case["n"]
     o = OracleEnv(num_lanes=case.get("lanes", 3), n_agents=n, rays=case["rays"], fov=case["fov"],
                   max_dist=case["maxd"], step=case["step"], obs_dim=D, respawn=False)
-    cars = np.zeros(n, CAR_DTYPE)
+    cars = ORP.O.new_cars(n)
     for a, b in {"x": "x", "y": "y", "v": "v", "h": "heading", "acc": "acc", "steer": "steering",
                  "sx": "spawn_x", "sy": "spawn_y", "sv": "spawn_v", "sh": "spawn_heading", "prev_dist": "prev_dist",
                  "pa0": "prev_a0", "pa1": "prev_a1", "path_index": "path_index", "route": "route",
                  "intention": "intention", "alive": "alive"}.items():
         cars[a] = st[b][e]
-    o.set_state(cars, np.zeros(0, CAR_DTYPE), int(st["step_count"][e]))
+    o.set_state(cars, ORP.O.new_cars(0), int(st["step_count"][e]))
     r = o.step(np.zeros((n, 2), np.float32))
     o.close()
     return r["obs"]

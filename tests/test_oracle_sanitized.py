@@ -53,7 +53,7 @@ def _write_input(path, name):
     egos = R.state_from_records(d["init_ego_f"], d["init_ego_i"], ego_routes)
     k = len(d["init_npc_f"])
     npcs = R.state_from_records(d["init_npc_f"], d["init_npc_i"], [tr[r] for r in d["init_npc_i"][:, 3]]) if k \
-        else np.zeros(0, R.O.CAR_DTYPE)
+        else R.O.new_cars(0)
     steps = int(meta["steps"])
     hdr = np.array([L, n, rays, obs_dim, int(bool(meta["use_team"])), int(bool(meta["respawn"])),
                     int(meta["max_steps"]), int(bool(meta["traffic"])), 64, steps, len(tr), k,
