@@ -53,8 +53,21 @@ constexpr int WAVE = 64;
 #else
 #define STAMP(k) STAMP_RAW(k)
 #endif
+#elif defined(MEV_STAMPS_Q)
+// -DMEV_STAMPS_Q: s_memtime at eight points of the fused step kept in LDS (no global store,
+// no wave barrier; lane 0 of single-wave workgroups), written to SimParams::debug[e*8 + k]
+// at the end of the kernel: 0 entry, 1 loads consumed, 2 NPC phase done, 3 phase 1 done,
+// 4 cars_pre done, 5 cars_post before the observation head, 6 cars_post done, 7 kernel end
+// (tools/qstamp_profile.py)
+__shared__ unsigned long long mev_qst[8];
+#define QSTAMP(k) do { if ((threadIdx.x & 63) == 0) mev_qst[(k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define STAMP(k) do { if ((k) == 0) QSTAMP(1); if ((k) == 1) QSTAMP(2); if ((k) == 2) QSTAMP(3); \
+                      if ((k) == 5) QSTAMP(4); if ((k) == 6) QSTAMP(6); } while (0)
 #else
 #define STAMP(k) do {} while (0)
+#endif
+#ifndef QSTAMP
+#define QSTAMP(k) do {} while (0)
 #endif
 constexpr int MAXN = 64;
 constexpr int MAXK = 64;
@@ -1991,6 +2004,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
         return;
     }
     // ---- observation head (:418-520)
+    QSTAMP(5);
     const int C = PK > 1 ? NE : N + (TRAFFIC ? ncnt : 0);  // neighbour candidates per agent (+ itself)
     if (C <= 8) {
         // lane (grp, sub): agent i0 + grp, neighbour candidate sub; rank = position
