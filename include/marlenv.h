@@ -316,7 +316,12 @@ int mev_set_env_deal(mev_handle* h, int32_t on);
  * handle stops it first.  Only on the handle's own stream (not after
  * mev_set_stream); the kernel itself runs on a non-blocking highest-priority
  * stream of its own; at most 2 servers are resident per process (other handles
- * step launched).  While it is resident, every device-wide wait of the process
+ * step launched).  A server slot belongs to the handle that took it -- across its
+ * server's idle exits and paused stretches -- until the handle is closed, turns
+ * serving off, moves to another stream, or has made no host-mode step for 50 ms
+ * when another handle asks for a slot; so a round-robin over more small handles
+ * than slots serves the first two to step, whatever the timing of idle exits.
+ * While it is resident, every device-wide wait of the process
  * (hipDeviceSynchronize, torch.cuda.synchronize(), frees that wait for the
  * device) waits for its idle exit, so the idle limit is adaptive: 8 x the
  * moving average of the host's time between an answer and the next post,

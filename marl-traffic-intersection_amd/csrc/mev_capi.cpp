@@ -198,6 +198,9 @@ struct mev_handle {
     uint64_t serve_pause = 0;
     uint64_t serve_misses_total = 0;
     std::chrono::steady_clock::time_point serve_t_answer{};
+    // steady-clock ns of the handle's last host-mode step (serve_slot: a slot's owner
+    // that has made no host step for kServeStaleMs may lose it to another handle)
+    std::atomic<int64_t> serve_last_ns{0};
     // the server's own stream: non-blocking, at the highest priority, whose hardware
     // queues are not the ones normal-priority streams share (GPU_MAX_HW_QUEUES of them):
     // a resident kernel holds back whatever another stream queues behind it on its queue
@@ -519,6 +522,7 @@ int mev_set_stream(mev_handle* h, void* stream) {
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));  // order the switch after outstanding work
     h->stream = static_cast<hipStream_t>(stream);  // NULL = the legacy default stream
+    if (h->stream != h->own_stream) serve_unlist(h);  // (no server on a caller's stream: its slot goes)
     return MEV_OK;
 }
 
@@ -1004,10 +1008,20 @@ int serve_launch(mev_handle* h) {
 
 // Resident servers per process are capped: their high-priority hardware queues are
 // few, and a server launched behind another one's on a shared queue would wait for its
-// idle exit.  Handles beyond the cap step launched (same results).
+// idle exit.  Handles beyond the cap step launched (same results).  A slot belongs to
+// the handle that took it -- across its server's idle exits and paused stretches --
+// until the handle is closed, or has made no host step for kServeStaleMs when another
+// handle asks for a slot: which handles are served does not depend on the timing of
+// idle exits (a round-robin over more handles than slots serves the first ones).
 constexpr int kMaxResidentServers = 2;
+constexpr int64_t kServeStaleMs = 50;
 std::mutex g_serve_mu;
-std::vector<mev_handle*> g_serving;  // handles whose server may be resident
+std::vector<mev_handle*> g_serving;  // the slots' owners (<= kMaxResidentServers)
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 // whether h's server is still resident (some workgroup has not yet left)
 bool serve_resident(const mev_handle* h) {
@@ -1018,16 +1032,24 @@ bool serve_resident(const mev_handle* h) {
     return false;
 }
 
-// h may keep or start a resident server
+// h may keep or start a resident server: it owns a slot, or takes a free one (or
+// one whose owner has stepped no host step for kServeStaleMs and has no server left)
 bool serve_slot(mev_handle* h) {
     std::lock_guard<std::mutex> lk(g_serve_mu);
-    if (serve_resident(h)) return true;  // (one that left idle competes for a slot again)
-    int n = 0;
-    for (const mev_handle* x : g_serving) n += (x != h && serve_resident(x)) ? 1 : 0;
-    if (n >= kMaxResidentServers) return false;
-    bool listed = false;
-    for (const mev_handle* x : g_serving) listed |= x == h;
-    if (!listed) g_serving.push_back(h);
+    for (const mev_handle* x : g_serving)
+        if (x == h) return true;
+    if ((int)g_serving.size() >= kMaxResidentServers) {
+        const int64_t t = now_ns();
+        for (size_t i = 0; i < g_serving.size(); ++i) {
+            const mev_handle* x = g_serving[i];
+            if (!serve_resident(x) && t - x->serve_last_ns.load(std::memory_order_relaxed) > kServeStaleMs * 1000000) {
+                g_serving.erase(g_serving.begin() + long(i));
+                break;
+            }
+        }
+    }
+    if ((int)g_serving.size() >= kMaxResidentServers) return false;
+    g_serving.push_back(h);
     return true;
 }
 
@@ -1162,6 +1184,7 @@ int mev_set_serve(mev_handle* h, int32_t mode) {
     HIP_TRY(hipSetDevice(h->cfg.device));
     if (int r = serve_stop(h)) return r;
     h->serve_mode = mode;
+    if (mode == 0) serve_unlist(h);  // (its slot, if it owns one, goes to the next handle that asks)
     return MEV_OK;
 }
 
@@ -1190,6 +1213,7 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     in.auto_reset = (a->flags & MEV_AUTO_RESET) ? 1 : 0;
     in.rng_counter = h->rng_counter++;
     const bool pinned = !dev && !gather && pin_ready(h);  // zero-copy host mode (small handles)
+    if (pinned) h->serve_last_ns.store(now_ns(), std::memory_order_relaxed);  // (a slot owner keeps stepping)
     const bool serve = pinned && serve_wanted(h) && serve_slot(h);  // ... answered by the resident step server
     if (!serve)
         if (int r = serve_stop(h)) return r;
@@ -1556,6 +1580,7 @@ int mev_set_step_split(mev_handle* h, int32_t mode) {
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->sp.step_split = mode;
+    h->deal_valid = false;  // (the traffic early split deals 4 envs per workgroup: restart the rings)
     return MEV_OK;
 }
 

@@ -59,8 +59,8 @@ constexpr int WAVE = 64;
 // at the end of the kernel: 0 entry, 1 loads consumed, 2 NPC phase done, 3 phase 1 done,
 // 4 cars_pre done, 5 cars_post before the observation head, 6 cars_post done, 7 kernel end
 // (tools/qstamp_profile.py)
-__shared__ unsigned long long mev_qst[8];
-#define QSTAMP(k) do { if ((threadIdx.x & 63) == 0) mev_qst[(k)] = __builtin_amdgcn_s_memtime(); } while (0)
+__shared__ unsigned long long mev_qst[8 * 8];  // (per wave of the workgroup)
+#define QSTAMP(k) do { if ((threadIdx.x & 63) == 0) mev_qst[(threadIdx.x >> 6) * 8 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #define STAMP(k) do { if ((k) == 0) QSTAMP(1); if ((k) == 1) QSTAMP(2); if ((k) == 2) QSTAMP(3); \
                       if ((k) == 5) QSTAMP(4); if ((k) == 6) QSTAMP(6); } while (0)
 #else
@@ -300,9 +300,12 @@ __device__ inline int xcd_env(int b, int E) {
 // The env of workgroup b under the NPC-aware deal (kDealLists in mev_kernels.h):
 // list x = b % 8 (the XCD the dispatcher sends b to), rank i = b / 8 in that list's
 // descending NPC-class order, from the counts and orders step t - 1 built.
-__device__ inline int deal_env(const SimParams& p, int ring, int b) {
+// (k = 4 envs per workgroup, the traffic early split: workgroup b takes ranks
+// 4 (b / 8) + j, j < 4, of its list; every list holds E / 8 envs whichever kernel
+// built it, so any E divisible by 32 keeps the deal a bijection)
+__device__ inline int deal_env(const SimParams& p, int ring, int b, int k = 1, int j = 0) {
     const int x = b & (kDealLists - 1);
-    int i = b >> 3;
+    int i = (b >> 3) * k + j;
     const __attribute__((address_space(1))) int32_t* cnt =
         gmem(p.deal_cnt) + (size_t)ring * kDealRingInts + x * kDealClasses * kDealPad;
     int n[kDealClasses];
@@ -1384,7 +1387,7 @@ struct CarsCtx {
 template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false, bool DIMS = false>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
                                             const CarsLDS& el, NL* nl) {
-    static_assert(!ESPLIT || (FUSED && !TRAFFIC), "early split: k_step without traffic");
+    static_assert(!ESPLIT || FUSED, "early split: k_step");
     static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
     static_assert(!DIMS || (PK == 1 && !EARLY && !ESPLIT), "per-car sizes: the runtime-layout kernels");
     static_assert(!TRAFFIC || NL::kDims == DIMS, "NPC sizes in LDS exactly when the kernel handles them");
@@ -2341,6 +2344,39 @@ struct LidarSrcLds {
     }
     __device__ int4 box(int, int o) const { return el.box[o]; }
 };
+// The LiDAR wave of the traffic early split: ENVS envs of one ego each, env j's
+// car LDS (carved at base + j * reg bytes, the obstacle table of that env) and
+// one beam-offset array; an agent's env is found from its global index (N = 1:
+// the env index), so the phase-3 pairs of different envs share the 64 lanes.
+template <int ENVS>
+struct LidarSrcLdsEnvs {
+    static constexpr bool kBoxLds = true;  // the obstacle tables are in this workgroup's LDS
+    const CarsLDS& el0;  // env 0's arrays
+    int reg;             // bytes between two envs' car LDS
+    const float* relp;
+    const int* env;      // [ENVS] the workgroup's envs (wave-uniform)
+    __device__ int off(int g) const {
+        int j = 0;
+#pragma unroll
+        for (int u = 1; u < ENVS; ++u) j = g == env[u] ? u : j;
+        return j * reg;
+    }
+    template <class T>
+    __device__ const T* at(const T* p0, int g) const {
+        return reinterpret_cast<const T*>(reinterpret_cast<const unsigned char*>(p0) + off(g));
+    }
+    __device__ float rel(int b) const { return relp[b]; }
+    __device__ bool alive(int g) const { return at(el0.alive, g)[0] != 0; }
+    __device__ float4 pose(int g) const {
+        return make_float4(at(el0.x, g)[0], at(el0.y, g)[0], at(el0.h, g)[0], __int_as_float(g));
+    }
+    __device__ void cand(int g, unsigned long long& c0, unsigned long long& c1) const {
+        const unsigned long long* c = at(el0.cand, g);
+        c0 = c[0];
+        c1 = c[1];
+    }
+    __device__ int4 box(int g, int o) const { return at(el0.box, g)[o]; }
+};
 
 // Lidar::update (Lidar.cpp:16-90) + Lidar::normalized for the agents
 // [a0, a0 + na) (na <= G) of one wave; base/lay: the wave's LDS.  Phase 1
@@ -2769,7 +2805,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 const int j = seg_jo[m] >> 8;
                 const float4 a = ag[j];
                 const int4 rg = seg_rg[m];
-                const int4 bx = Src::kBoxLds ? src.box(0, seg_jo[m] & 255) : seg_bx[m];
+                const int4 bx = Src::kBoxLds ? src.box(__float_as_int(a.w), seg_jo[m] & 255) : seg_bx[m];
                 const int cA = rg.x >> 16, cB = rg.y >> 16;
                 const int b = r < cA ? (rg.x & 0xffff) + r
                                      : (r < cA + cB ? (rg.y & 0xffff) + r - cA : (rg.z & 0xffff) + r - cA - cB);
@@ -3006,11 +3042,24 @@ __device__ __forceinline__ void deal_append(const SimParams& p, const StepInputs
 // workgroup).
 constexpr int kSplitWpe = 4;
 constexpr int kEsplitWpe = 8;
+// the traffic early split: kTsplitEnvs envs (car waves) + one LiDAR wave per workgroup,
+// kTsplitWpe waves per SIMD (config 4: 4096 envs -> 5120 waves on 1024 SIMDs)
+#ifndef MEV_TS_ENVS
+#define MEV_TS_ENVS 4
+#endif
+constexpr int kTsplitEnvs = MEV_TS_ENVS;
+#ifndef MEV_TS_BEAMS
+#define MEV_TS_BEAMS kFixedRays
+#endif
+constexpr int kTsplitRays = MEV_TS_BEAMS;  // LiDAR pool beams per env
+constexpr int kTsplitWpe = MEV_TS_ENVS == 4 ? 5 : (MEV_TS_ENVS == 2 ? 6 : 4);
 constexpr int kPrioEsplitRoad = 3;
 constexpr int kPrioEsplitCars = 2;
 constexpr int kPrioEsplitCarPhase = 1;
 template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
-__global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, (ESPLIT && PK == 1) ? kEsplitWpe : (SPLIT ? kSplitWpe : 4)) void k_step(
+__global__ __launch_bounds__((TRAFFIC && ESPLIT) ? (PK + 1) * WAVE : (SPLIT ? 2 * WAVE : WAVE),
+                             (TRAFFIC && ESPLIT) ? kTsplitWpe
+                                                 : ((ESPLIT && PK == 1) ? kEsplitWpe : (SPLIT ? kSplitWpe : 4))) void k_step(
     const SimParams* __restrict__ pp, StepInputs in, Outputs out) {
 #include "mev_step_body.inc"
 }
@@ -3249,7 +3298,11 @@ constexpr int kSplitMaxWg = 2048;
 // 4096 x 1 x 64 beams (config 2) 13.3 -> 11.6 us per step at 4 envs, 4096 x 4 x 64
 // 24.1 -> 22.0 at 2, 2048 x 1 x 64 12.4 -> 10.0 at 2, 4096 x 1 x 128 15.5 -> 14.4 at 2.
 int esplit_pack(const SimParams& p) {
-    if (p.traffic || !fixed_fits<8, 0>(p) || p.N > 8) return 0;
+    // traffic: kTsplitEnvs one-ego envs per workgroup (every workgroup full, and the
+    // NPC-aware deal's lists of E / 8 envs split into whole workgroups)
+    if (p.traffic)
+        return fixed_fits<1, 32>(p) && p.R <= kTsplitRays && p.E % (8 * kTsplitEnvs) == 0 && p.step_split == 3 ? kTsplitEnvs : 0;
+    if (!fixed_fits<8, 0>(p) || p.N > 8) return 0;
     const int nr = p.N * p.R;
     int pk = p.step_pack;
     if (pk == 1 || pk == 2 || pk == 4 || pk == 8) {
@@ -3280,6 +3333,13 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
     if (p.traffic) {
         if (fixed_fits<1, 32>(p)) {  // compile-time LDS layout (config 4: one ego, <= 32 NPC slots)
             const unsigned lds = (unsigned)FixedLayout<1, 32>::bytes;  // + the static NpcLDST
+            if (step_esplit(p)) {  // the traffic early split: kTsplitEnvs car waves + a LiDAR wave
+                constexpr int P = kTsplitEnvs;
+                const unsigned tl = (unsigned)(P * FixedLayout<1, 32>::lidar + lidar_layout_beams(P, P * kTsplitRays, 32, false).bytes);
+                hipLaunchKernelGGL((k_step<true, TAB, 1, 32, P, true, true>), dim3(p.E / P), dim3((P + 1) * WAVE), tl, s,
+                                   dp, in, out);
+                return;
+            }
             hipLaunchKernelGGL((k_step<true, TAB, 1, 32>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
             return;
         }

@@ -64,6 +64,16 @@ class PackedOutputs:
             raise ValueError("the compact gather format needs the decode table (Handle.lidar_decode_table())")
         if self.fmt == _capi.MEV_GATHER_STATE and handle is None:
             raise ValueError("the state gather format is decoded by the library: pass the root's Handle")
+        if handle is not None:
+            # the library decodes with the handle's own layout (mev_unpack_gathered): a buffer
+            # packed in another layout would be read out of bounds on the device
+            comm = getattr(handle, "comm", None)
+            got = (getattr(handle, "gather_format", 0), comm["slots"] if comm else None, handle.N, handle.D,
+                   handle.lidar_slots())
+            want = (self.fmt, self.C, self.N, self.D, self.L if self.fmt else handle.lidar_slots())
+            if got != want:
+                raise ValueError(f"the handle's gather layout (format, slots, agents, obs_dim, lidar_slots) {got} "
+                                 f"differs from this layout's {want}")
         self.table = table
         self.handle = handle
         self.offsets, self.nbytes = _capi.packed_layout(self.C, self.N, self.D, self.fmt, self.L)

@@ -197,16 +197,28 @@ def test_random_states_match_oracle_early_split(mev, cfg, pack):
     _random_states_vs_oracle(mev, cfg, 2, pack, split=3)
 
 
-def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0):
+TRAFFIC_ONE_EGO = [c for c in CONFIGS if c.get("traffic") and c["n"] == 1 and not c.get("dims")]
+
+
+@pytest.mark.parametrize("cfg", TRAFFIC_ONE_EGO, ids=[c["name"] for c in TRAFFIC_ONE_EGO])
+def test_random_states_match_oracle_traffic_early_split(mev, cfg):
+    """The traffic early split (mev_set_step_split(3), one ego and <= 32 NPC slots per
+    env, E divisible by 32: four car waves -- NPC phase and car part of one env each
+    -- and one LiDAR wave for their four egos per workgroup), 32 envs from random
+    states: every output and the state after every step bit-exact."""
+    _random_states_vs_oracle(mev, cfg, 2, 0, split=3, max_npcs=32, E=32)
+
+
+def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0, max_npcs=64, E=24):
     rng = np.random.default_rng(zlib.crc32(cfg["name"].encode()))
-    E, T = 24, 50
+    T = 50
     n, lanes = cfg["n"], cfg.get("lanes", 3)
     R_ = cfg["rays"]
     D = 127 if R_ <= 96 else 31 + R_
     h = mev.Handle(num_envs=E, num_agents=n, num_lanes=lanes, lidar_rays=R_, obs_dim=D,
                    traffic_flow=int(cfg.get("traffic", False)), traffic_density=cfg.get("density", 0.5),
                    use_team_reward=int(cfg.get("use_team", False)), respawn_enabled=int(cfg.get("respawn", True)),
-                   max_steps=cfg.get("max_steps", 2000), max_npcs=64,
+                   max_steps=cfg.get("max_steps", 2000), max_npcs=max_npcs,
                    reward=cfg.get("reward", [10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2]))
     use_step_kernel(mev, h, kernel)
     if pack:
@@ -214,7 +226,9 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0):
         assert h.step_pack() == (pack if pack * n <= 8 else max(1, 8 // n)), h.step_pack()
     if split:
         h.set_step_split(split)
-        if h.step_split() != 2:  # the early split needs the slots' beams in one 512-beam pool
+        if cfg.get("traffic"):
+            assert h.step_split() == 2, "traffic early split not selected"
+        elif h.step_split() != 2:  # the early split needs the slots' beams in one 512-beam pool
             assert h.step_pack() * n * R_ > 512, (h.step_pack(), n, R_)
             pytest.skip("beams of the workgroup's slots exceed one LiDAR pool")
     table = ROUTES2 if lanes == 2 else ROUTES3

@@ -148,24 +148,30 @@ def test_fused_and_two_kernel_paths_agree_traffic_full_size(mev):
     the Philox spawn stream, 32 NPC slots): the fused k_step (NPC phase, car
     part and LiDAR in one wave) and k_cars + k_lidar agree bit for bit, step
     after step, with auto-reset on; the NPC fleets (counts and every NPC
-    field) too."""
+    field) too.  A third handle runs the traffic early split (four car waves and
+    one LiDAR wave per workgroup, the NPC-aware deal over 4-env workgroups)."""
     cfg = dict(num_envs=E, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32,
                max_steps=300, seed=11)
-    hs = [mev.Handle(**cfg) for _ in range(2)]
-    for h, kernel in zip(hs, (1, 2)):
+    hs = [mev.Handle(**cfg) for _ in range(3)]
+    for h, kernel in zip(hs, (1, 2, 2)):
         h.set_step_kernel(kernel)
+    hs[2].set_step_split(3)
+    assert hs[2].step_split() == 2 and hs[1].step_split() == 0
     rng = np.random.default_rng(12)
     most = 0
     for t in range(400):
         a = rng.uniform(-1, 1, (E, 1, 2)).astype(np.float32)
         o1 = hs[0].step(a, auto_reset=True)
         o2 = hs[1].step(a, auto_reset=True)
+        o3 = hs[2].step(a, auto_reset=True)
         for k in o1:
             assert np.array_equal(o1[k], o2[k]), (t, k)
+            assert np.array_equal(o1[k], o3[k]), (t, k, "split")
         if t % 50 == 49 or t == 399:
-            s1, s2 = hs[0].get_state(), hs[1].get_state()
+            s1, s2, s3 = hs[0].get_state(), hs[1].get_state(), hs[2].get_state()
             for k in s1:
                 assert np.array_equal(s1[k], s2[k]), (t, k)
+                assert np.array_equal(s1[k], s3[k]), (t, k, "split")
             most = max(most, int(s1["npc_count"].max()))
     assert most >= 4  # busy intersections were exercised
     for h in hs:
@@ -178,26 +184,34 @@ def test_env_deal_exact_beyond_residency(mev):
     while earlier ones of the same step have already appended to the next
     step's orders) the deal and the identity order agree bit for bit, every
     output each step and the whole state (NPC fleets included) every 25 steps,
-    with auto-resets and busy intersections."""
+    with auto-resets and busy intersections.  A third handle deals 4-env
+    workgroups of the traffic early split (switched on after 40 steps of the
+    one-env kernel; the deal then restarts from the identity order)."""
     E4 = 16384
     cfg = dict(num_envs=E4, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=2.0, max_npcs=32,
                max_steps=90, seed=21)
-    hs = [mev.Handle(**cfg) for _ in range(2)]
+    hs = [mev.Handle(**cfg) for _ in range(3)]
     hs[1].set_env_deal(False)
     for h in hs:
         assert h.step_kernel() == 2
     rng = np.random.default_rng(22)
     most = 0
     for t in range(150):
+        if t == 40:
+            hs[2].set_step_split(3)
+            assert hs[2].step_split() == 2
         a = rng.uniform(-1, 1, (E4, 1, 2)).astype(np.float32)
         o1 = hs[0].step(a, auto_reset=True)
         o2 = hs[1].step(a, auto_reset=True)
+        o3 = hs[2].step(a, auto_reset=True)
         for k in o1:
             assert np.array_equal(o1[k], o2[k]), (t, k)
+            assert np.array_equal(o1[k], o3[k]), (t, k, "split")
         if t % 25 == 24:
-            s1, s2 = hs[0].get_state(), hs[1].get_state()
+            s1, s2, s3 = hs[0].get_state(), hs[1].get_state(), hs[2].get_state()
             for k in s1:
                 assert np.array_equal(s1[k], s2[k]), (t, k)
+                assert np.array_equal(s1[k], s3[k]), (t, k, "split")
             most = max(most, int(s1["npc_count"].max()))
     assert most >= 5  # the deal sorted envs over several NPC classes
     for h in hs:

@@ -249,11 +249,9 @@ def test_several_served_handles_at_once(mev):
     # (sharing one, each launched step would wait for the idle exit behind a resident server)
     assert time.perf_counter() - t0 < 2.0
     d = [h.serve_stats()["steps"] - a for h, a in zip(served, s0)]
-    # two resident servers per process at most, serving (almost) throughout: a server that
-    # meets its adaptive idle limit (a host hiccup between two of its handle's steps) exits
-    # and another handle's next step may take the free slot, so the served steps can move
-    # between handles -- but never more than two handles' worth per round (+1 per handoff)
-    assert sum(d) <= 2 * 100 + 5 and sum(sorted(d)[-2:]) >= 170 and sum(d) >= 190, d
+    # two resident servers per process at most: the two handles that stepped first keep
+    # their slots (across idle exits) and are served (almost) throughout
+    assert d[0] >= 95 and d[1] >= 95 and sum(d[2:]) == 0, d
     for h in served + launched:
         h.close()
 
@@ -278,9 +276,9 @@ def test_resident_servers_are_capped(mev):
             _same(hs[i].step(act, auto_reset=True), twins[i].step(act, auto_reset=True), (t, i))
     assert time.perf_counter() - t0 < 2.0
     d = [h.serve_stats()["steps"] - a for h, a in zip(hs, s0)]
-    # kMaxResidentServers: two handles' worth of served steps per round, the others launched
-    # (a server's idle exit can hand its slot to another handle, as above)
-    assert sum(d) <= 2 * 100 + 5 and sum(sorted(d)[-2:]) >= 170 and sum(d) >= 190, d
+    # kMaxResidentServers: handles 0 and 1 (the first to step) served throughout, the
+    # others launched -- slot ownership does not move with idle exits
+    assert d[0] >= 95 and d[1] >= 95 and sum(d[2:]) == 0, d
     for h in hs + twins:
         h.close()
 

@@ -113,6 +113,34 @@ def test_packed_layout_offsets():
     assert lay.nbytes % 256 == 0 and lay.nbytes >= lay.used
 
 
+def test_packed_layout_checks_the_decoding_handle():
+    """The state format is decoded by the library with the HANDLE's layout: a
+    PackedOutputs whose format, slots, agents, obs_dim or LiDAR slots differ from the
+    handle's is refused up front (the decode kernel would read out of bounds)."""
+
+    class FakeHandle:  # the attributes PackedOutputs reads (no device)
+        N, D, gather_format = 8, 127, 2
+        comm = {"slots": 64}
+
+        def lidar_slots(self):
+            return 64
+
+    h = FakeHandle()
+    sharding.PackedOutputs(64, 8, 127, fmt=2, lidar_slots=64, handle=h)  # matches
+    for kw in (dict(slots=63), dict(agents=4), dict(obs_dim=95), dict(lidar_slots=32)):
+        a = dict(slots=64, agents=8, obs_dim=127, lidar_slots=64)
+        a.update(kw)
+        with pytest.raises(ValueError, match="gather layout"):
+            sharding.PackedOutputs(a["slots"], a["agents"], a["obs_dim"], fmt=2, lidar_slots=a["lidar_slots"],
+                                   handle=h)
+    h.gather_format = 1
+    with pytest.raises(ValueError, match="gather layout"):
+        sharding.PackedOutputs(64, 8, 127, fmt=2, lidar_slots=64, handle=h)
+    h.comm = None  # no communicator: no layout at all
+    with pytest.raises(ValueError, match="gather layout"):
+        sharding.PackedOutputs(64, 8, 127, fmt=2, lidar_slots=64, handle=h)
+
+
 @pytest.mark.parametrize("total_envs", [6, 5])
 def test_gather_matches_single_process(total_envs):
     world = 2

@@ -24,11 +24,15 @@ def main():
     ap.add_argument("--traffic", type=float, default=0.5)
     ap.add_argument("--warmup", type=int, default=600)
     ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--split", type=int, default=0, help="mev_set_step_split mode (3: the traffic early split; "
+                    "its car waves' last part is the deal append, not the LiDAR)")
     a = ap.parse_args()
     mev = pkgload.load()
     h = mev.Handle(num_envs=a.envs, num_agents=a.agents, lidar_rays=a.rays, use_team_reward=int(a.agents > 1),
                    traffic_flow=int(a.traffic > 0), traffic_density=a.traffic, max_npcs=32)
     h.set_step_kernel(2)
+    if a.split:
+        h.set_step_split(a.split)
     rng = np.random.default_rng(0)
     for t in range(a.warmup):
         h.step(rng.uniform(-1, 1, (a.envs, a.agents, 2)).astype(np.float32), auto_reset=True)

@@ -27,6 +27,12 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                # timing-only: k_step stopped after the car part / LiDAR phase 1 / 2 / 3 (instruction budgets)
                "stop1": ["-DMEV_EXP_STOP=1"], "stop2": ["-DMEV_EXP_STOP=2"], "stop3": ["-DMEV_EXP_STOP=3"],
                "stop4": ["-DMEV_EXP_STOP=4"], "stop0": ["-DMEV_EXP_STOP=0"],
+               # the traffic early split (mev_set_step_split(3)): timing-only cuts -- the LiDAR wave
+               # without its work after barrier B / without any work, the car waves without cars_post
+               # -- and the LiDAR wave's phase 1 at two agents per pass (exact)
+               "ts1": ["-DMEV_EXP_TS=1"], "ts2": ["-DMEV_EXP_TS=2"], "ts3": ["-DMEV_EXP_TS=3"],
+               "tsilp2": ["-DMEV_TS_ILP=2"], "ts2env": ["-DMEV_TS_ENVS=2"],
+               "tsb64": ["-DMEV_TS_BEAMS=64"], "ts2b64": ["-DMEV_TS_BEAMS=64", "-DMEV_EXP_TS=2"],
                # compiler options (exact): SLP vectorization back on, no loop vectorization, the max-ilp
                # scheduler, kernel-argument preloading, AMDGPU register-pressure trackers, no unclustered
                # high-pressure reschedule stage, latency over occupancy, relaxed occupancy
