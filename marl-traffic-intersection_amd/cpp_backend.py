@@ -11,8 +11,14 @@ creating the environment raises.
 Deviations from MARLEnv (all outside the hot path):
  * configure_routes validates lane names immediately (MARLEnv fails later,
    inside step, on an unknown end lane; an unknown start lane never spawns);
- * all cars share one LiDAR configuration (MARLEnv keeps one Lidar per car);
-   assigning `lidars` reconfigures every car;
+ * per-car LiDAR objects (IntersectionEnv.lidars, bindings.cpp:68,85-92) are simulated
+   as in the reference, each car's rays / max_dist / step_size / rel_angles; cars of
+   different configurations are stepped by one device handle per configuration, all
+   fed the same calls (identical states and spawn streams), each car's observation row
+   taken from the handle of its own configuration.  rel_angles must be evenly spaced
+   (every list Lidar() or add_car_with_route makes, and any prefix of one, is), with at
+   least `rays` entries and rays >= 1 (the reference reads past the end otherwise);
+   `lidars` must hold one Lidar per car, or one configuration for all of them;
  * Car.path may be any 160-point path (every path MARLEnv itself generates has
    160 points, RouteGen.cpp:111-205); a path that is not a lane-layout route is
    appended to the device route table (mev_add_route); other lengths raise
@@ -160,6 +166,69 @@ class Lidar:
         return (np.asarray(self.distances, np.float32) * inv).tolist()
 
 
+def _lidar_key(l_: "Lidar") -> tuple:
+    """A car's LiDAR as the simulation sees it: (rays, fov_deg, max_dist, step_size, rel_angles);
+    rel_angles as float32 values, every entry (the reference keeps the whole list)."""
+    rays = int(l_.rays)
+    rel = tuple(np.asarray(l_.rel_angles, np.float32).reshape(-1).tolist())
+    if rays < 1 or len(rel) < rays:
+        raise ValueError(f"Lidar with {rays} rays and {len(rel)} rel_angles: need rays >= 1 and at least rays "
+                         "offsets (the reference reads past the end of rel_angles otherwise)")
+    return (rays, float(l_.fov_deg), float(l_.max_dist), float(l_.step_size), rel)
+
+
+def _default_key(lidar) -> tuple:
+    """The per-car key of a uniform (rays, fov, max, step) configuration."""
+    return (int(lidar[0]), float(lidar[1]), float(lidar[2]), float(lidar[3]),
+            tuple(np.asarray(_rel_angles(int(lidar[0]), float(lidar[1])), np.float32).tolist()))
+
+
+class _LidarGroup:
+    """One env as several device handles that differ only in their LiDAR (one per distinct
+    per-car configuration, cpp_backend's per-car `lidars`): every call that changes the env
+    goes to all of them in the same order, so their states -- and their spawn streams --
+    stay identical; reads come from the first; car i's observation row from handle
+    row_of[i]."""
+
+    _ALL = ("set_state", "set_car_dims", "set_traffic_routes", "set_ego_routes", "reset", "configure",
+            "configure_traffic", "set_reward", "add_route")
+
+    def __init__(self, handles, row_of):
+        self._hs = list(handles)
+        self._row_of = np.asarray(row_of)
+        self._outs = None
+
+    def __getattr__(self, name):
+        if name in _LidarGroup._ALL:
+            def call(*a, **k):
+                r = [getattr(h, name)(*a, **k) for h in self._hs]
+                return r[0]
+            return call
+        return getattr(self._hs[0], name)
+
+    def _stitch(self, obs0, others):
+        for g, o in enumerate(others, start=1):
+            m = self._row_of == g
+            obs0[0, m] = o[0, m]
+        return obs0
+
+    def step(self, actions, dt=1.0 / 60.0, out=None):
+        if self._outs is None:
+            self._outs = [h.alloc_outputs() for h in self._hs[1:]]
+        r = self._hs[0].step(actions, dt, out=out)
+        for h, o in zip(self._hs[1:], self._outs):
+            h.step(actions, dt, out=o)
+        self._stitch(r["obs"], [o["obs"] for o in self._outs])
+        return r
+
+    def observations(self):
+        return self._stitch(self._hs[0].observations().copy(), [h.observations() for h in self._hs[1:]])
+
+    def close(self):
+        for h in self._hs:
+            h.close()
+
+
 def _rel_angles(rays: int, fov: float) -> List[float]:
     """Beam offsets in float32 exactly as cpp/Lidar.cpp:4-14."""
     f32 = np.float32
@@ -243,12 +312,21 @@ class IntersectionEnv:
         if ei < 0:
             raise IndexError(f"unknown lane id {end_id!r}")  # std::out_of_range from .at() (RouteGen.cpp:120)
         r = si * 8 * self.num_lanes + ei
+        if self._lidar[0] == "per_car":  # the new car's own Lidar: 96 rays (IntersectionEnv.cpp:111-128)
+            self._lidar = ("per_car", tuple(self._lidar[1]) + (_default_key(DEFAULT_LIDAR),))
         self._routes.append(r)
         self._pending.append(r)
         self._agent_ids.append(self._next_id)
         self._next_id += 1
 
     def _create(self, n: int, lidar):
+        """A device handle for n cars of one LiDAR configuration `lidar` ((rays, fov, max, step)),
+        or, per car (("per_car", keys), see _lidar_key), one handle per distinct key."""
+        if lidar[0] == "per_car":
+            keys = self._car_keys(lidar, n)
+            uniq = list(dict.fromkeys(keys))
+            return _LidarGroup([self._create(n, k[:4]) if k == _default_key(k[:4]) else self._create_rel(n, k)
+                                for k in uniq], [uniq.index(k) for k in keys])
         h = _capi.Handle(num_envs=1, num_agents=n, num_lanes=self.num_lanes, lidar_rays=lidar[0],
                          lidar_fov_deg=lidar[1], lidar_max_dist=lidar[2], lidar_step=lidar[3], obs_dim=OBS_W,
                          traffic_flow=int(self._traffic), traffic_density=self._density,
@@ -258,6 +336,21 @@ class IntersectionEnv:
         for path, intent in self._custom:  # the caller's own routes keep their ids on a new handle
             h.add_route(path, intent)
         return h
+
+    def _create_rel(self, n: int, key):
+        h = self._create(n, key[:4])
+        try:
+            h.set_beam_angles(np.asarray(key[4][: key[0]], np.float32))  # Lidar::rel_angles[0 .. rays)
+        except _capi.MevError as e:
+            h.close()
+            raise ValueError(f"Lidar.rel_angles: {e} (this backend needs evenly spaced offsets)") from None
+        return h
+
+    @staticmethod
+    def _car_keys(lidar, n: int) -> List[tuple]:
+        """Per-car keys for n cars: cars beyond the list got add_car_with_route's 96-ray Lidar."""
+        keys = list(lidar[1][:n])
+        return keys + [_default_key(DEFAULT_LIDAR)] * (n - len(keys))
 
     def _sync(self) -> Optional[_capi.Handle]:
         n = len(self._routes)
@@ -414,12 +507,15 @@ class IntersectionEnv:
         h = self._sync()
         if h is None:
             return []
-        rays, fov, maxd, stp = self._lidar
-        obs = h.observations()[0][:, 31:31 + min(rays, OBS_W - 31)]
+        n = h.N
+        keys = self._car_keys(self._lidar, n) if self._lidar[0] == "per_car" else [_default_key(self._lidar)] * n
+        obs = h.observations()[0]
         out = []
-        inv = np.float32(1.0) / np.float32(maxd)
-        for row in obs:
+        for row_all, (rays, fov, maxd, stp, rel) in zip(obs, keys):
+            row = row_all[31:31 + min(rays, OBS_W - 31)]
+            inv = np.float32(1.0) / np.float32(maxd)
             l_ = Lidar(rays, fov, maxd, stp)
+            l_.rel_angles = list(rel)
             k = np.rint(row.astype(np.float64) * maxd / stp)
             cand = (k * stp).astype(np.float32)
             ok = (cand * inv) == row
@@ -432,13 +528,18 @@ class IntersectionEnv:
     def lidars(self, lidars: Sequence[Lidar]):
         if not lidars:
             return
-        cfg = {(l_.rays, l_.fov_deg, l_.max_dist, l_.step_size) for l_ in lidars}
-        if len(cfg) != 1:
-            raise ValueError("all cars must share one LiDAR configuration")
-        self._set_lidar(cfg.pop())
+        keys = [_lidar_key(l_) for l_ in lidars]
+        if len(set(keys)) == 1 and keys[0] == _default_key(keys[0][:4]):
+            self._set_lidar(keys[0][:4])  # one configuration with its own offsets: one handle
+            return
+        n = len(self._routes)
+        if len(set(keys)) > 1 and len(keys) != n:
+            raise ValueError(f"{len(keys)} Lidars for {n} cars: one per car (or one configuration for all)")
+        self._set_lidar(("per_car", tuple(keys * n if len(keys) == 1 else keys)))
 
     def _set_lidar(self, lidar):
-        lidar = (int(lidar[0]), float(lidar[1]), float(lidar[2]), float(lidar[3]))
+        if lidar[0] != "per_car":
+            lidar = (int(lidar[0]), float(lidar[1]), float(lidar[2]), float(lidar[3]))
         if lidar == self._lidar:
             return
         if self._h is not None and len(self._routes) == self._h.N:

@@ -656,6 +656,10 @@ int orc_add_route(orc_env* e, const float* path, int intent) {
     return e->nroutes++;
 }
 
+/* Lidar::rel_angles written by the caller (read-write, cpp/bindings.cpp:91): the
+ * first `rays` offsets are the beams' (Lidar.cpp:25). */
+void orc_set_rel_angles(orc_env* e, const float* rel) { memcpy(e->rel, rel, sizeof(float) * (size_t)e->rays); }
+
 void orc_set_traffic_routes(orc_env* e, const int* ids, int m) {
     e->ntr = m;
     memcpy(e->troutes, ids, sizeof(int) * (size_t)m);

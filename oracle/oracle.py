@@ -56,6 +56,7 @@ def lib():
         L.orc_num_points.argtypes = [vp]
         L.orc_route_path.argtypes = [vp, i, vp, vp]
         L.orc_set_traffic_routes.argtypes = [vp, vp, i]
+        L.orc_set_rel_angles.argtypes = [vp, vp]
         L.orc_add_route.argtypes = [vp, vp, i]
         L.orc_reset.argtypes = [vp, vp]
         L.orc_set_state.argtypes = [vp, vp, vp, i, i]
@@ -81,6 +82,7 @@ class OracleEnv:
         if not self.h:
             raise ValueError("bad oracle configuration")
         self.n = n_agents
+        self.rays = rays
         self.D = obs_dim if obs_dim > 0 else 31 + rays
         self.max_npcs = max_npcs
         self.P = L.orc_num_points(self.h)
@@ -111,6 +113,12 @@ class OracleEnv:
         if r < 0:
             raise MemoryError("orc_add_route")
         return r
+
+    def set_rel_angles(self, rel):
+        """Lidar::rel_angles[0 .. rays) (cpp/bindings.cpp:91)."""
+        a = np.ascontiguousarray(np.asarray(rel, np.float32)[: self.rays])
+        assert a.size == self.rays
+        lib().orc_set_rel_angles(self.h, a.ctypes.data)
 
     def set_traffic_routes(self, ids):
         a = np.ascontiguousarray(ids, np.int32)

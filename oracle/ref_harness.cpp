@@ -164,6 +164,20 @@ void rh_set_lidar(void* p, int rays, float fov, float maxd, float step) {
     for (auto& l : h->env.lidars) l = h->make_lidar();
 }
 
+// IntersectionEnv.lidars[i] = a Lidar whose fields the caller wrote (cpp/bindings.cpp:68,
+// 85-92: Lidar() then rays / fov_deg / max_dist / step_size / rel_angles assigned as
+// plain members; distances stay as Lidar() made them -- update() resizes them).
+void rh_set_car_lidar(void* p, int i, int rays, float fov, float maxd, float step, const float* rel, int nrel) {
+    auto* h = static_cast<Harness*>(p);
+    Lidar l;
+    l.rays = rays;
+    l.fov_deg = fov;
+    l.max_dist = maxd;
+    l.step_size = step;
+    if (rel) l.rel_angles.assign(rel, rel + nrel);
+    h->env.lidars.at(size_t(i)) = l;
+}
+
 void rh_reset(void* p) {
     auto* h = static_cast<Harness*>(p);
     h->env.reset();

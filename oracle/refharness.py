@@ -47,6 +47,7 @@ def lib():
         L.rh_num_traffic_routes.argtypes = [vp]
         L.rh_set_reward.argtypes = [vp, fp]
         L.rh_set_lidar.argtypes = [vp, i, f, f, f]
+        L.rh_set_car_lidar.argtypes = [vp, i, i, f, f, f, fp, i]
         L.rh_reset.argtypes = [vp]
         L.rh_state_roundtrip.argtypes = [vp]
         L.rh_add_car.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, i]
@@ -158,6 +159,15 @@ class RefEnv:
         if lib().rh_set_car_path(self.h, int(which), int(k), int(custom)) != 0:
             raise IndexError("bad car or custom path index")
 
+    def set_car_lidar(self, k: int, rays: int, fov: float, max_dist: float, step: float, rel=None):
+        """IntersectionEnv.lidars[k] = a Lidar() with these members written (cpp/bindings.cpp:85-92);
+        rel=None keeps Lidar()'s own 72 beam offsets.  (lidar() then no longer applies: the
+        cars' ray counts differ.)"""
+        r = None if rel is None else np.ascontiguousarray(rel, np.float32)
+        lib().rh_set_car_lidar(self.h, int(k), int(rays), float(fov), float(max_dist), float(step),
+                               None if r is None else _f(r), 0 if r is None else int(r.size))
+        self.mixed_lidar = True
+
     def route_path(self, route: int) -> np.ndarray:
         out = np.zeros((512, 2), np.float32)
         n = lib().rh_route_path(self.h, int(route), _f(out))
@@ -169,6 +179,8 @@ class RefEnv:
         return out[: self.n].copy()
 
     def lidar(self) -> np.ndarray:
+        if getattr(self, "mixed_lidar", False):
+            raise ValueError("per-car LiDAR configurations: raw distances are not one [n][rays] array")
         out = np.zeros((max(self.n, 1), self.rays), np.float32)
         lib().rh_get_lidar(self.h, _f(out))
         return out[: self.n].copy()

@@ -23,6 +23,7 @@ Status codes: 0 ALIVE, 1 DEAD, 2 SUCCESS, 3 CRASH_WALL, 4 CRASH_LINE, 5 CRASH_CA
 from __future__ import annotations
 
 import json
+from typing import List
 import math
 import os
 import sys
@@ -60,10 +61,13 @@ def policy(obs: np.ndarray, rng: np.random.Generator, target_v=3.5, noise=0.05) 
 def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_steps=2000,
         traffic=False, density=0.5, lanes=3, ego_routes=None, reward=None, steps=200,
         act="random", seed=0, dt=1.0 / 60.0, act_scale=1.0, zero_throttle_p=0.0,
-        inject=None, notes="", warmup=0, roundtrip=False, custom_paths=None, ego_paths=None):
+        inject=None, notes="", warmup=0, roundtrip=False, custom_paths=None, ego_paths=None, car_lidars=None):
     """custom_paths: [C][160][2] paths of the caller's own (Car.path writes); ego_paths: per ego
     the custom path written into its Car.path, or -1 (NPCs on custom path k, injected by
-    `inject`, record route 1000 + k)."""
+    `inject`, record route 1000 + k).  car_lidars: per ego None (add_car_with_route's own
+    96-ray Lidar) or (rays, fov_deg, max_dist, step_size, rel_angles or None): the Lidar
+    written into IntersectionEnv.lidars[k] (a Lidar() with those members assigned; None keeps
+    Lidar()'s own 72 offsets, cpp/Lidar.cpp:4-14)."""
     routes = ROUTES3 if lanes == 3 else ROUTES2
     if ego_routes is None:
         ego_routes = [routes[i % len(routes)] for i in range(n_agents)]
@@ -80,6 +84,9 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
         if k >= 0:
             env.set_car_path(0, i, k)  # Car.path = ... (cpp/bindings.cpp:29)
     env.custom_paths = cps
+    for k, cl in enumerate(car_lidars or []):
+        if cl is not None:
+            env.set_car_lidar(k, *cl)
     rng = np.random.default_rng(seed)
     if inject is not None:
         inject(env, rng)
@@ -125,7 +132,8 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
         NC.append(len(f))
         NFl.append(f)
         NIl.append(i)
-        LD.append(env.lidar())
+        if not car_lidars:
+            LD.append(env.lidar())
     kmax = max([len(x) for x in NFl] + [1])
     npc_f = np.zeros((steps, kmax, R.NF), np.float32)
     npc_i = np.zeros((steps, kmax, R.NI), np.int32)
@@ -138,6 +146,12 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
                 act=act, seed=seed, notes=notes, init_step=init_step, warmup=warmup, set_state=bool(roundtrip))
     if cps:
         meta["ego_paths"] = [int(k) for k in ego_paths or [-1] * n]
+    if car_lidars:
+        # per ego: [] (the default 96-ray Lidar) or [rays, fov_deg, max_dist, step_size, n_rel];
+        # car_rel[k, :n_rel] = its rel_angles (n_rel = -1: Lidar()'s own 72)
+        meta["car_lidars"] = [[] if cl is None else [int(cl[0]), float(cl[1]), float(cl[2]), float(cl[3]),
+                                                      -1 if cl[4] is None else int(len(cl[4]))]
+                              for cl in car_lidars]
     arrays = dict(
         meta=np.array(json.dumps(meta)),
         init_ego_f=ef, init_ego_i=ei, init_npc_f=nf.reshape(-1, R.NF), init_npc_i=ni.reshape(-1, R.NI),
@@ -150,6 +164,13 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
         arrays["lidar"] = np.asarray(LD, np.float32)
     if cps:
         arrays["custom_paths"] = np.stack(cps).astype(np.float32)
+    if car_lidars:
+        m = max([len(cl[4]) for cl in car_lidars if cl is not None and cl[4] is not None] + [1])
+        rel = np.zeros((n, m), np.float32)
+        for k, cl in enumerate(car_lidars):
+            if cl is not None and cl[4] is not None:
+                rel[k, : len(cl[4])] = np.asarray(cl[4], np.float32)
+        arrays["car_rel"] = rel
     path = os.path.join(OUT, f"{name}.npz")
     np.savez_compressed(path, **arrays)
     env.close()
@@ -336,6 +357,27 @@ def gen_paths_traffic():
         custom_paths=[bent_npc], ego_paths=[-1], inject=inject_npcs(2, custom=[0, 0]))
 
 
+def rel_angles(rays: int, fov: float) -> List[float]:
+    """Lidar's beam offsets (cpp/Lidar.cpp:4-14, IntersectionEnv.cpp:118-126) in float32."""
+    f32 = np.float32
+    start = f32(-fov) * f32(0.5)
+    step = f32(fov) / f32(rays - 1) if rays > 1 else f32(0.0)
+    return [float((start + f32(i) * step) * f32(np.pi) / f32(180.0)) for i in range(rays)]
+
+
+def gen_lidars():
+    """Per-car LiDAR objects (IntersectionEnv.lidars is read-write, cpp/bindings.cpp:68, each
+    Lidar's members too, :85-92): cars with different ray counts, ranges, steps and beam
+    offsets in one env -- Lidar() as constructed (72 rays), Lidar() with fewer rays than its
+    72 offsets (the first ones are used), offsets written for a 270-degree fan of 128 rays
+    (the observation keeps 96), and NPCs in the beams."""
+    run("lidar_mixed_n4", n_agents=4, rays=96, steps=200, act="policy", seed=430,
+        car_lidars=[None, (72, 360.0, 250.0, 4.0, None), (48, 360.0, 200.0, 5.0, None),
+                    (128, 270.0, 250.0, 4.0, rel_angles(128, 270.0))])
+    run("lidar_mixed_npc", n_agents=2, rays=96, traffic=True, density=0.0, steps=200, act="policy", seed=431,
+        car_lidars=[(32, 360.0, 150.0, 3.0, rel_angles(32, 360.0)), None], inject=inject_npcs(3))
+
+
 # (name prefix or scenario name, generator, deterministic).  Traffic with density > 0 draws
 # its spawns from the reference's unseeded RNG (TrafficFlow.cpp:278,324): not reproducible.
 def _core():
@@ -384,7 +426,7 @@ def _traffic():
     run("traffic_d20_random", n_agents=1, rays=64, traffic=True, density=20.0, steps=400, act="random", seed=15)
 
 
-GROUPS = [("core", _core, True), ("dims", gen_dims, True), ("paths", gen_paths, True),
+GROUPS = [("core", _core, True), ("dims", gen_dims, True), ("paths", gen_paths, True), ("lidars", gen_lidars, True),
           ("traffic", _traffic, False), ("dims_traffic", gen_dims_traffic, False),
           ("paths_traffic", gen_paths_traffic, False)]
 

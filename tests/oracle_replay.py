@@ -24,33 +24,83 @@ def state_from_records(f, i, routes):
     return cars
 
 
-def make_oracle(meta):
-    R = int(meta["rays"])
-    return O.OracleEnv(num_lanes=int(meta["num_lanes"]), n_agents=int(meta["n_agents"]), rays=R,
-                       obs_dim=int(meta.get("obs_dim", 127 if R <= 96 else 31 + R)), use_team=bool(meta["use_team"]),
-                       respawn=bool(meta["respawn"]), max_steps=int(meta["max_steps"]), traffic=bool(meta["traffic"]),
-                       density=float(meta["density"]), reward=meta["reward"], max_npcs=64)
+def make_oracle(meta, lidar=None):
+    """lidar: (rays, max_dist, step_size, rel_angles[:rays]) of a per-car LiDAR (None: meta's)."""
+    R = int(meta["rays"]) if lidar is None else int(lidar[0])
+    kw = {} if lidar is None else dict(max_dist=float(lidar[1]), step=float(lidar[2]), obs_dim=127)
+    env = O.OracleEnv(num_lanes=int(meta["num_lanes"]), n_agents=int(meta["n_agents"]), rays=R,
+                      obs_dim=kw.pop("obs_dim", int(meta.get("obs_dim", 127 if R <= 96 else 31 + R))),
+                      use_team=bool(meta["use_team"]), respawn=bool(meta["respawn"]), max_steps=int(meta["max_steps"]),
+                      traffic=bool(meta["traffic"]), density=float(meta["density"]), reward=meta["reward"], max_npcs=64,
+                      **kw)
+    if lidar is not None:
+        env.set_rel_angles(np.asarray(lidar[3], np.float32))
+    return env
+
+
+def car_lidar_keys(d):
+    """Per ego of a golden with per-car LiDAR objects (meta car_lidars, gen_golden.py gen_lidars):
+    (rays, max_dist, step_size, rel_angles[:rays]); [] = add_car_with_route's 96-ray Lidar,
+    n_rel -1 = Lidar()'s own 72 offsets (cpp/Lidar.cpp:4-14)."""
+    def rel(rays, fov):
+        f32 = np.float32
+        st = f32(fov) / f32(rays - 1) if rays > 1 else f32(0.0)
+        return [float((f32(-fov) * f32(0.5) + f32(i) * st) * f32(np.pi) / f32(180.0)) for i in range(rays)]
+    keys = []
+    for k, cl in enumerate(d["meta"]["car_lidars"]):
+        if not cl:
+            keys.append((96, 250.0, 4.0, tuple(rel(96, 360.0))))
+            continue
+        rays, _, maxd, stp, nrel = cl
+        r = rel(72, 360.0) if nrel < 0 else d["car_rel"][k, :nrel].tolist()
+        keys.append((int(rays), float(maxd), float(stp), tuple(np.asarray(r[:rays], np.float32).tolist())))
+    return keys
 
 
 def replay(name):
+    """Every recorded output of golden `name` against the oracle.  Per-car LiDAR objects: one
+    oracle per distinct configuration, all stepped alike, each car's row from its own (before
+    the first step only the heads are compared: the reference's block then shows the written
+    Lidar's stale distances, which no simulation state holds)."""
     d = G.load(name)
     meta = d["meta"]
     L = int(meta["num_lanes"])
-    env = make_oracle(meta)
+    keys = car_lidar_keys(d) if "car_lidars" in meta else None
+    uniq = list(dict.fromkeys(keys)) if keys else [None]
+    envs = [make_oracle(meta, k) for k in uniq]
+    row_of = np.array([uniq.index(k) for k in keys]) if keys else None
+    env = envs[0]
     cids = G.custom_route_ids(env, d)
+    for o in envs[1:]:
+        G.custom_route_ids(o, d)
     tr = [env.route_id(G.point_index(s, L), G.point_index(e, L)) for s, e in meta["traffic_routes"]]
-    env.set_traffic_routes(tr)
     ego_routes = G.ego_route_ids(env, d, L, cids)
     egos = state_from_records(d["init_ego_f"], d["init_ego_i"], ego_routes)
     k = len(d["init_npc_f"])
     npcs = state_from_records(d["init_npc_f"], d["init_npc_i"], G.npc_route_ids(d["init_npc_i"][:, 3], tr, cids)) \
         if k else []
-    env.set_state(egos, npcs, int(meta.get("init_step", 0)))
+    for o in envs:
+        o.set_traffic_routes(tr)
+        o.set_state(egos, npcs, int(meta.get("init_step", 0)))
+
+    def stitch(rows):
+        out = rows[0].copy()
+        for g in range(1, len(rows)):
+            out[row_of == g] = rows[g][row_of == g]
+        return out
     errs = []
-    if not G.bits_equal(env.observe()[:, :127], d["init_obs"]):
+    if keys is None and not G.bits_equal(env.observe()[:, :127], d["init_obs"]):
         errs.append("initial obs")
+    if keys is not None and not G.bits_equal(env.observe()[:, :31], d["init_obs"][:, :31]):
+        errs.append("initial obs heads")
     for t in range(int(meta["steps"])):
-        r = env.step(d["actions"][t], float(meta["dt"]), int(d["spawned"][t]) if meta["traffic"] else -1)
+        rs = [o.step(d["actions"][t], float(meta["dt"]), int(d["spawned"][t]) if meta["traffic"] else -1)
+              for o in envs]
+        r = rs[0]
+        if keys is not None:
+            r = dict(r, obs=stitch([q["obs"] for q in rs]))
+            if any(not G.bits_equal(q["rew"], r["rew"]) for q in rs[1:]):
+                errs.append(f"step {t + 1}: the per-LiDAR oracles diverged")
         if not G.bits_equal(r["obs"][:, :127], d["obs"][t]):
             errs.append(f"step {t + 1}: obs")
         if not G.bits_equal(r["rew"], d["rew"][t]):
@@ -77,7 +127,8 @@ def replay(name):
                 errs.append(f"step {t + 1}: npc length / width")
         if errs:
             break
-    env.close()
+    for o in envs:
+        o.close()
     return errs
 
 

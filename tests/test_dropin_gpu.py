@@ -331,3 +331,63 @@ def test_cpp_backend_written_cars_replay_reference(name):
     assert [(c.length, c.width) for c in other.cars] == [(c.length, c.width) for c in env.cars]
     env.close()
     other.close()
+
+
+@pytest.mark.parametrize("name", ["lidar_mixed_n4", "lidar_mixed_npc"])
+def test_cpp_backend_per_car_lidars_replay_reference(name):
+    """Per-car LiDAR objects written through IntersectionEnv.lidars (cpp/bindings.cpp:68,85-92):
+    Lidar() as constructed (72 rays), Lidar() with fewer rays than its offsets, a 128-ray
+    270-degree fan with its offsets written, a short-range 32-ray Lidar among NPCs -- every
+    recorded output bit-exact against the reference (gen_golden.py gen_lidars), one device
+    handle per configuration behind the drop-in.  Before the first step only the heads are
+    compared: the reference's LiDAR block then shows the written Lidar's own distances."""
+    g = G.load(name)
+    meta = g["meta"]
+    L = meta["num_lanes"]
+    env = cpp_backend.IntersectionEnv(L)
+    env.configure(meta["use_team"], meta["respawn"], meta["max_steps"])
+    env.configure_traffic(meta["traffic"], meta["density"])
+    env.configure_routes([tuple(r) for r in meta["traffic_routes"]])
+    env.reset()
+    for s, t in meta["ego_routes"]:
+        env.add_car_with_route(s, t)
+    lids = []
+    for k, cl in enumerate(meta["car_lidars"]):
+        if not cl:
+            lids.append(cpp_backend.Lidar(96))  # add_car_with_route's own
+            continue
+        rays, fov, maxd, stp, nrel = cl
+        l_ = cpp_backend.Lidar()  # 72 rays, members written as a MARLEnv user would
+        l_.rays, l_.fov_deg, l_.max_dist, l_.step_size = rays, fov, maxd, stp
+        if nrel >= 0:
+            l_.rel_angles = g["car_rel"][k, :nrel].tolist()
+        lids.append(l_)
+    env.lidars = lids
+    if len(g["init_npc_f"]):
+        P = 8 * L
+        npcs = []
+        for f, i in zip(g["init_npc_f"], g["init_npc_i"]):
+            c = cpp_backend.Car()
+            c.state = cpp_backend.State(*map(float, f[:4]))
+            c.acc, c.steering_angle = float(f[4]), float(f[5])
+            c.length, c.width = float(f[13]), float(f[14])
+            c.alive, c.intention, c.path_index = bool(i[0]), int(i[1]), int(i[2])
+            s, t = meta["traffic_routes"][int(i[3])]
+            c._route = G.point_index(s, L) * P + G.point_index(t, L)  # (its lane route: Car.path left empty)
+            npcs.append(c)
+        env.traffic_cars = npcs
+    assert G.bits_equal(env.get_observations()[:, :31], g["init_obs"][:, :31])
+    got = env.lidars
+    assert [(l_.rays, l_.max_dist, l_.step_size) for l_ in got] == [(l_.rays, l_.max_dist, l_.step_size) for l_ in lids]
+    for t in range(len(g["actions"])):
+        a = g["actions"][t]
+        res = env.step(a[:, 0].tolist(), a[:, 1].tolist(), meta["dt"])
+        info = dict(agents_alive=res.agents_alive, step=res.step, status=res.status, done=res.done)
+        _check_step(name, g, t, res.obs, res.rewards, res.terminated, res.truncated, info)
+    # the Lidars read back carry the reference's distances of the last step
+    last = g["obs"][-1]
+    for k, l_ in enumerate(env.lidars):
+        if last[k].any():  # (a dead car's row is zero)
+            n_ = min(l_.rays, 96)
+            assert G.bits_equal(np.asarray(l_.normalized(), np.float32)[:n_], last[k, 31:31 + n_]), k
+    env.close()

@@ -10,7 +10,9 @@ from conftest import STEP_KERNELS
 
 pytestmark = pytest.mark.gpu
 
-SINGLE = [n for n in G.scenario_names() if not n.startswith("inject_egos")]
+# (per-car LiDAR objects, gen_golden.py gen_lidars: one handle per LiDAR configuration,
+# replayed through the drop-in in test_dropin_gpu.py)
+SINGLE = [n for n in G.scenario_names() if not n.startswith("inject_egos") and "car_lidars" not in G.load(n)["meta"]]
 
 
 def _replay(mev, names, kernel):
@@ -80,6 +82,27 @@ def test_golden_scenario_split_waves(mev, name, split):
     whose beams exceed one 512-beam pool take the automatic choice); all bit-exact."""
     (rep,) = G.replay(mev, name, kernel=2, split=split)
     assert rep.ok, f"{name}: {rep.mismatches[:5]} (steps checked {rep.steps})"
+
+
+# (goldens with other car sizes run the runtime-layout kernel, which has no split)
+TRAFFIC_ONE_EGO = [n for n in SINGLE if G.load(n)["meta"]["traffic"] and G.load(n)["meta"]["n_agents"] == 1
+                   and not G.has_dims(G.load(n))]
+
+
+@pytest.mark.parametrize("name", TRAFFIC_ONE_EGO)
+def test_golden_scenario_traffic_early_split(mev, name):
+    """The traffic early split (four car waves -- NPC phase and car part of one env
+    each -- and one LiDAR wave for their egos per workgroup; E divisible by 32): each
+    one-ego traffic golden replicated into 32 envs, every env bit-exact against the
+    reference, with the split asserted to be the path that ran."""
+    h = G.make_handle(mev, G.load(name)["meta"], 32)
+    h.set_step_kernel(2)
+    h.set_step_split(3)
+    assert h.step_split() == 2, "traffic early split not selected"
+    h.close()
+    reps = G.replay(mev, [name] * 32, kernel=2, split=3)
+    bad = [(i, r.mismatches[:3]) for i, r in enumerate(reps) if not r.ok]
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("pack", [2, 4, 8])
