@@ -283,6 +283,44 @@ def test_resident_servers_are_capped(mev):
         h.close()
 
 
+def test_server_slots_follow_their_owners(mev):
+    """Slot ownership (marlenv.h, mev_set_serve): the first two handles to step own the
+    two server slots; a third is launched while they keep stepping; it takes a slot
+    once an owner turns serving off, or has made no host step for 50 ms -- and every
+    step stays exact against launched twins."""
+    hs = [mev.Handle(seed=s, num_envs=1, num_agents=1, lidar_rays=16) for s in range(3)]
+    tw = [mev.Handle(seed=s, num_envs=1, num_agents=1, lidar_rays=16) for s in range(3)]
+    for h in tw:
+        h.set_serve(0)
+    for h in hs + tw:
+        h.reset()
+    rng = np.random.default_rng(11)
+
+    def rounds(k, who):
+        s0 = [h.serve_stats()["steps"] for h in hs]
+        for _ in range(k):
+            for i in who:
+                act = rng.uniform(-1, 1, (1, 1, 2)).astype(np.float32)
+                _same(hs[i].step(act, auto_reset=True), tw[i].step(act, auto_reset=True), i)
+        return [h.serve_stats()["steps"] - a for h, a in zip(hs, s0)]
+
+    d = rounds(40, [0, 1, 2])
+    assert d[0] >= 35 and d[1] >= 35 and d[2] == 0, d
+    hs[1].set_serve(0)  # handle 1 gives its slot up: handle 2's next step takes it
+    d = rounds(40, [0, 1, 2])
+    assert d[0] >= 35 and d[1] == 0 and d[2] >= 35, d
+    hs[1].set_serve(1)  # handle 1 wants one again: both slots are owned and stepping
+    d = rounds(40, [0, 1, 2])
+    assert d[1] == 0, d
+    d = rounds(40, [1, 2])  # handle 0 goes quiet, but only for a few ms: it keeps its slot
+    assert d[1] == 0, d
+    time.sleep(0.12)  # handle 0 silent for > 50 ms: handle 1 may take its slot
+    d = rounds(40, [1, 2])
+    assert d[1] >= 35 and d[2] >= 35, d
+    for h in hs + tw:
+        h.close()
+
+
 def test_get_state_partial_fields(mev):
     """mev_get_state stages through pinned memory (one copy per SoA block): any subset of
     fields reads the same values as the full call."""
