@@ -3052,7 +3052,14 @@ constexpr int kTsplitEnvs = MEV_TS_ENVS;
 #define MEV_TS_BEAMS kFixedRays
 #endif
 constexpr int kTsplitRays = MEV_TS_BEAMS;  // LiDAR pool beams per env
-constexpr int kTsplitWpe = MEV_TS_ENVS == 4 ? 5 : (MEV_TS_ENVS == 2 ? 6 : 4);
+// (6, not the 5 that 1024 five-wave workgroups need on 1024 SIMDs: a workgroup's five waves
+// do not spread evenly over a CU's four SIMDs, and at a 5-wave budget (93 VGPRs) 4096 envs
+// did not fit one residency round -- 38.3 us against 28.7 us at 3072 envs; at 80 VGPRs
+// they do, profiles/r5_ts_wpe_cfg4.txt)
+#ifndef MEV_TS_WPE
+#define MEV_TS_WPE (MEV_TS_ENVS == 4 ? 6 : (MEV_TS_ENVS == 2 ? 6 : 4))
+#endif
+constexpr int kTsplitWpe = MEV_TS_WPE;
 constexpr int kPrioEsplitRoad = 3;
 constexpr int kPrioEsplitCars = 2;
 constexpr int kPrioEsplitCarPhase = 1;
@@ -3300,8 +3307,14 @@ constexpr int kSplitMaxWg = 2048;
 int esplit_pack(const SimParams& p) {
     // traffic: kTsplitEnvs one-ego envs per workgroup (every workgroup full, and the
     // NPC-aware deal's lists of E / 8 envs split into whole workgroups)
+    // Automatic for 1024 <= E <= 4096 (every workgroup resident at once on the 256 CUs):
+    // config 4 33.3 -> 31.4 us, 1024 / 2048 envs 6-8 % faster; 8192 envs (two residency
+    // rounds) 55.9 -> 59.0 us, so not there (profiles/r5_ab_ts6_cfg4.txt, two rounds).
     if (p.traffic)
-        return fixed_fits<1, 32>(p) && p.R <= kTsplitRays && p.E % (8 * kTsplitEnvs) == 0 && p.step_split == 3 ? kTsplitEnvs : 0;
+        return fixed_fits<1, 32>(p) && p.R <= kTsplitRays && p.E % (8 * kTsplitEnvs) == 0 &&
+                       (p.step_split == 3 || (p.step_split == 0 && p.E >= 1024 && p.E <= 4096))
+                   ? kTsplitEnvs
+                   : 0;
     if (!fixed_fits<8, 0>(p) || p.N > 8) return 0;
     const int nr = p.N * p.R;
     int pk = p.step_pack;

@@ -155,7 +155,7 @@ def test_fused_and_two_kernel_paths_agree_traffic_full_size(mev):
     hs = [mev.Handle(**cfg) for _ in range(3)]
     for h, kernel in zip(hs, (1, 2, 2)):
         h.set_step_kernel(kernel)
-    hs[2].set_step_split(3)
+    hs[1].set_step_split(1)  # one wave per env (the automatic choice here is the early split)
     assert hs[2].step_split() == 2 and hs[1].step_split() == 0
     rng = np.random.default_rng(12)
     most = 0
@@ -192,8 +192,12 @@ def test_env_deal_exact_beyond_residency(mev):
                max_steps=90, seed=21)
     hs = [mev.Handle(**cfg) for _ in range(3)]
     hs[1].set_env_deal(False)
+    hs[0].set_step_split(3)  # the deal on the early split (not automatic beyond 4096 envs)
+    hs[1].set_step_split(1)  # the identity order on the one-wave-per-env kernel
+    hs[2].set_step_split(1)  # the deal on the one-wave kernel, then (below) on the early split
     for h in hs:
         assert h.step_kernel() == 2
+    assert hs[0].step_split() == 2 and hs[1].step_split() == 0 and hs[2].step_split() == 0
     rng = np.random.default_rng(22)
     most = 0
     for t in range(150):
@@ -242,10 +246,17 @@ def test_step_kernel_selection(mev):
     tiny = mev.Handle(num_envs=1, num_agents=1, lidar_rays=16)
     assert tiny.step_kernel() == 2  # automatic: one agent's beams fit one LiDAR wave, one launch
     tiny.close()
-    # config 4 shape (1 ego, traffic, 32 NPC slots): fused automatically
+    # config 4 shape (1 ego, traffic, 32 NPC slots): fused automatically, as the traffic early
+    # split (four car waves + a LiDAR wave per workgroup) where E is a multiple of 32, >= 1024
     t = mev.Handle(num_envs=4096, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32)
-    assert t.step_kernel() == 2
+    assert t.step_kernel() == 2 and t.step_split() == 2
+    t.set_step_split(1)
+    assert t.step_split() == 0
     t.close()
+    for e_ in (4080, 992):  # (not a multiple of 32 / below 1024 envs: one wave per env)
+        t = mev.Handle(num_envs=e_, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32)
+        assert t.step_split() == 0, e_
+        t.close()
 
 
 def test_env_permutation_equivariance(mev):
