@@ -1366,6 +1366,173 @@ struct CarsCtx {
     bool ended;     // (set by cars_post, PK == 1) terminated or truncated this step
 };
 
+// Phase 1 of the car part for agent i of el on lane group (grp, sub): kinematics
+// (IntersectionEnv.cpp:151-163), path index, base reward (:15-46), status (:165-290).
+// cars_pre runs it over its agents 8 per pass; the traffic early split's LiDAR wave
+// runs it for its envs' egos, one env per lane group (el then differs per group).
+// (EARLY: eroute .. ga1 are the group-layout registers of the state round, see cars_pre)
+template <bool EARLY, bool DIMS>
+__device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs& in, const CarsLDS& el, const int i,
+                                           const bool act, const int ii, const int grp, const int sub,
+                                           const unsigned long long gmask, const int eroute, const int epidx,
+                                           const Kin& gk, const uint8_t galive_b, const float ga0, const float ga1) {
+    constexpr bool early = EARLY;
+    constexpr bool dims = DIMS;
+    const GF2 P = gf2(p.rt.path + (size_t)(early ? eroute : el.route[ii]) * (2 * PATH_LEN));
+    const int pidx0 = early ? epidx : el.pidx[ii];
+    const int start_i = pidx0 < 0 ? 0 : pidx0;
+    const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
+    // the window's first point: start_i, or (early: the LDS window of round B)
+    // start_i rounded down to even; the 50-point window and the look-ahead target
+    // lie in [w0, w0 + 64): 8 points per lane
+    const int w0 = early ? (start_i & ~1) : start_i;
+    float2 pt[8];
+    float2 pend, pprev, p10;
+    if (!early) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int q = start_i + sub * 8 + j;
+            pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+        }
+        pend = P[PATH_LEN - 1]; pprev = P[PATH_LEN - 2]; p10 = P[10];
+    }
+    Kin k = early ? gk : Kin{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
+    const bool alive = act && (early ? galive_b : el.alive[ii]) != 0;
+    const float a0_i = early ? ga0 : el.a0[ii], a1_i = early ? ga1 : el.a1[ii];
+    float cH, sH;
+    {
+        // every lane runs the update; a dead agent keeps its state (one sincosf)
+        Kin ku = k;
+        car_update_heading(ku, a0_i, a1_i, in.dt);
+        sincosf(alive ? ku.h : k.h, &sH, &cH);
+        car_update_move(ku, cH, sH);
+        if (alive) k = ku;
+    }
+    if (early) {  // round B's window: wait for the LDS DMA, then 4 aligned 16-B reads per lane
+        __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+        const float4* wl = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + grp * 128 + sub * 16);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const float4 q = wl[m * 64];  // + m KB
+            pt[2 * m] = make_float2(q.x, q.y);
+            pt[2 * m + 1] = make_float2(q.z, q.w);
+        }
+        // lane (grp, 0): points 158, 159; lane (grp, 1): points 10, 11
+        const float4* wx = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + 4096 + grp * 128);
+        const float4 ends = wx[0], ten = wx[1];
+        pprev = make_float2(ends.x, ends.y);
+        pend = make_float2(ends.z, ends.w);
+        p10 = make_float2(ten.x, ten.y);
+    }
+    // Car::update_path_index (Car.cpp:47-74): first minimum over the window, in order
+    float bd = __builtin_inff();
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int q = w0 + sub * 8 + j;  // the point's path index
+        if (q >= start_i && q < start_i + cnt) {
+            const float dx = pt[j].x - k.x, dy = pt[j].y - k.y;
+            const float d = dx * dx + dy * dy;
+            if (d < bd) { bd = d; bi = q; }
+        }
+    }
+    // minimum over the 8 lanes of the group (first index on ties): DPP swaps
+    // within quads, then the mirror within each half-row (VALU, no LDS)
+    auto take = [&](float od, int oi) {
+        if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
+    };
+    take(dpp_f(bd, 0xB1), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xf, 0xf, false));    // quad_perm [1,0,3,2]
+    take(dpp_f(bd, 0x4E), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xf, 0xf, false));    // quad_perm [2,3,0,1]
+    take(dpp_f(bd, 0x141), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xf, 0xf, false));  // row_half_mirror
+    const int pidx = alive ? (bi == 0x7fffffff ? start_i : bi) : pidx0;
+    // look-ahead point of the observation (:444-452), picked from the window
+    {
+        const int tidx = pidx + 10 < PATH_LEN - 1 ? pidx + 10 : PATH_LEN - 1;
+        const int toff = tidx - w0;
+        if (act && toff >= 0 && toff < 64 && sub == (toff >> 3)) {
+            float2 t = pt[0];
+#pragma unroll
+            for (int j = 1; j < 8; ++j) t = ((toff & 7) == j) ? pt[j] : t;
+            el.tgx[i] = t.x;
+            el.tgy[i] = t.y;
+        } else if (act && (toff < 0 || toff >= 64) && sub == 0) {
+            el.tgx[i] = P[tidx].x;
+            el.tgy[i] = P[tidx].y;
+        }
+    }
+    float rew = 0.0f, cur = 0.0f, an = 0.0f, sn = 0.0f;
+    bool succ = false;
+    float ccx[4], ccy[4];
+    car_corners_d(k.x, k.y, cH, sH, (dims ? el.len[ii] : CAR_LENGTH), (dims ? el.wid[ii] : CAR_WIDTH), ccx, ccy);
+    {  // (branch-free: every lane evaluates the terms, a dead agent's are zeroed)
+        // compute_progress / compute_stuck / compute_smooth (:15-46)
+        cur = hypotf(k.x - pend.x, k.y - pend.y);
+        const float prev = el.prev_dist[ii];
+        float r_prog = 0.0f;
+        if (prev > 0.0f) {
+            const float progress = prev - cur;
+            const float normalized = (p.max_progress > 0.0f) ? (progress / p.max_progress) : 0.0f;
+            r_prog = p.k_prog * normalized;
+        }
+        const float speed_ms = (k.v * FPS) / SCALE;
+        const float r_stuck = (speed_ms < p.v_min) ? p.k_stuck : 0.0f;
+        an = k.acc / MAX_ACC;
+        sn = k.steer / MAX_STEERING_ANGLE;
+        const float d0 = an - el.pa0[ii];
+        const float d1 = sn - el.pa1[ii];
+        const float r_smooth = p.k_sm * (d0 * d0 + d1 * d1);
+        rew = r_prog + r_stuck + r_smooth;
+        // SUCCESS by the last path segment's axis
+        const float dxr = pend.x - pprev.x, dyr = pend.y - pprev.y;
+        const bool sx_ = fabs_f(k.y - pend.y) < 15.0f && fabs_f(k.x - pend.x) < 40.0f;
+        const bool sy_ = fabs_f(k.x - pend.x) < 15.0f && fabs_f(k.y - pend.y) < 40.0f;
+        succ = fabs_f(dxr) > fabs_f(dyr) ? sx_ : sy_;
+        if (!alive) { rew = 0.0f; cur = 0.0f; an = 0.0f; sn = 0.0f; succ = false; }
+    }
+    // corner tests, one per lane: sub 0-3 corner q (screen margin, road, yellow line,
+    // line mask), sub 4-7 edge midpoint q (line mask)
+    bool oos_q = false, off_q = false, line_q = false;
+    {
+        // lane sub < 4: corner q (screen margin, road, yellow line, line mask);
+        // sub >= 4: the midpoint of edge (q, q + 1) (line mask only)
+        const int q = sub & 3;
+        float qx = ccx[0], qy = ccy[0], rx = ccx[1], ry = ccy[1];
+#pragma unroll
+        for (int u = 1; u < 4; ++u) {
+            if (q == u) { qx = ccx[u]; qy = ccy[u]; rx = ccx[(u + 1) & 3]; ry = ccy[(u + 1) & 3]; }
+        }
+        const bool corner = sub < 4;
+        const float px_ = corner ? qx : 0.5f * (qx + rx), py_ = corner ? qy : 0.5f * (qy + ry);
+        const float M = 100.0f;
+        const bool lm = is_line_px((int)px_, (int)py_, p.line_stop);
+        oos_q = alive && corner && (qx < -M || qx > float(WIDTH) + M || qy < -M || qy > float(HEIGHT) + M);
+        off_q = alive && corner && !is_on_road(qx, qy, p.rw);
+        line_q = alive && ((corner && hits_yellow_line(qx, qy, p.rw)) || lm);
+    }
+    const bool any_oos = (ballot(oos_q) & gmask) != 0ull;
+    const bool any_off = (ballot(off_q) & gmask) != 0ull;
+    const bool any_line = (ballot(line_q) & gmask) != 0ull;
+    if (act) {
+        if (sub < 4) {
+            reinterpret_cast<float*>(&el.cx[i])[sub] = ccx[sub];
+            reinterpret_cast<float*>(&el.cy[i])[sub] = ccy[sub];
+        }
+        if (sub == 0) {
+            uint8_t done = 0, status = ST_ALIVE;
+            if (!alive) { done = 1; status = ST_DEAD; }
+            else if (succ) { done = 1; status = ST_SUCCESS; }
+            else if (any_oos || any_off) { done = 1; status = ST_CRASH_WALL; }
+            else if (any_line) { done = 1; status = ST_CRASH_LINE; }
+            el.x[i] = k.x; el.y[i] = k.y; el.v[i] = k.v; el.h[i] = k.h; el.c[i] = cH; el.s[i] = sH;
+            el.acc[i] = k.acc; el.steer[i] = k.steer; el.pidx[i] = pidx;
+            if (alive) { el.prev_dist[i] = cur; el.pa0[i] = an; el.pa1[i] = sn; }
+            el.t10x[i] = p10.x; el.t10y[i] = p10.y;
+            el.done[i] = done; el.status[i] = status; el.rew[i] = rew;
+            el.col[i] = 0ull; el.colnpc[i] = 0;
+        }
+    }
+}
+
 // The per-env body of the step before the LiDAR (k_cars, or the first part of
 // k_step): el and nl are this wave's LDS.  Only what the LiDAR needs runs
 // here -- kinematics, status, car-car resolution, respawn, the obstacle table
@@ -1384,7 +1551,13 @@ struct CarsCtx {
 // DIMS: the kernel can run a handle whose cars have other sizes than 54 x 24 px
 // (k_cars, k_step<NM = 0>); p.dims then says whether this one does, and the car
 // corners, the SAT pre-test and the LiDAR boxes take each car's length / width.
-template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false, bool DIMS = false>
+// TSC (the traffic early split's car waves, one ego per env): the workgroup's LiDAR wave
+// loads the ego into this env's LDS and runs its phase 1 (ts_ego_phase) while this wave
+// runs the NPC phase; the two meet at workgroup barrier H, then this wave goes on from the
+// SAT.  The NPC phase's spawn test reads the ego's start-of-step position, which this wave
+// keeps in envw[0..1] (the LiDAR wave overwrites el.x / el.y with the moved pose).
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false, bool DIMS = false,
+          bool TSC = false>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
                                             const CarsLDS& el, NL* nl) {
     static_assert(!ESPLIT || FUSED, "early split: k_step");
@@ -1485,12 +1658,23 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // every load above is issued before any of their values is used (a use scheduled
     // between them would put a wait for the first loads in front of the rest)
     __builtin_amdgcn_sched_barrier(0);
+    static_assert(!TSC || (TRAFFIC && ESPLIT && PK == 1 && !DIMS), "TSC: the traffic early split's car waves");
     const bool pending = pending_b != 0;
     gpend = gpend_b != 0;
     const bool do_reset = in.auto_reset && pending;
     const int prev_step = do_reset ? 0 : step_prev;
     const int prev_npcs = TRAFFIC ? (do_reset ? 0 : npcs_prev) : 0;
-    if (lane_on) {
+    if (TSC && tid == 0) {  // the start-of-step position (the spawn after an auto-reset) for the NPC spawn test
+        float sx_ = x0, sy_ = y0;
+        if (do_reset) {
+            const int rid = reset_route(p, in.rng_counter, ee, 0, route_l);
+            sx_ = gmem(p.rt.spawn)[3 * rid];
+            sy_ = gmem(p.rt.spawn)[3 * rid + 1];
+        }
+        el.envw[0] = __float_as_int(sx_);
+        el.envw[1] = __float_as_int(sy_);
+    }
+    if (!TSC && lane_on) {
         el.a0[il] = a0;
         el.a1[il] = a1;
         el.route[il] = route_l;
@@ -1512,7 +1696,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             for (int b = tid; b < p.R; b += WAVE) el.rel[b] = gmem(p.rel_angles)[b];
         }
     }
-    if (lane_on && do_reset) {  // the lane's env was auto-reset: its agents start from their spawns
+    if (!TSC && lane_on && do_reset) {  // the lane's env was auto-reset: its agents start from their spawns
         const int rid = reset_route(p, in.rng_counter, ee, PK == 1 ? il : il - (ee - e) * NE, route_l);
         const float rx = gmem(p.rt.spawn)[3 * rid], ry = gmem(p.rt.spawn)[3 * rid + 1], rh = gmem(p.rt.spawn)[3 * rid + 2];
         el.route[il] = rid;
@@ -1569,7 +1753,14 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
 
     STAMP(0);
     int ncnt = 0;
-    if constexpr (TRAFFIC) ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg);
+    if constexpr (TSC) {
+        wave_lds_sync();
+        ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, reinterpret_cast<const float*>(el.envw),
+                         reinterpret_cast<const float*>(el.envw + 1), nreg);
+        __syncthreads();  // barrier H: the LiDAR wave has run this env's ego through phase 1
+    } else if constexpr (TRAFFIC) {
+        ncnt = npc_phase(p, in, e, prev_npcs, *nl, tid, el.x, el.y, nreg);
+    }
 
     if (TRAFFIC && FUSED) {
         // the envs with many NPCs set the kernel's end: the rest of their step goes first
@@ -1586,163 +1777,11 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // status (:165-290).  Lane (grp, sub): agent i0 + grp, sub-task sub.
     const int grp = tid >> 3, sub = tid & 7;
     const unsigned long long gmask = 0xFFull << (grp * 8);
-    for (int i0 = 0; i0 < N; i0 += 8) {
+    for (int i0 = 0; i0 < (TSC ? 0 : N); i0 += 8) {  // (TSC: the LiDAR wave ran it)
         const int i = i0 + grp;
         const bool act = i < N;
         const int ii = act ? i : 0;  // idle groups mirror agent 0 so every lane reaches the ballots
-        const GF2 P = gf2(p.rt.path + (size_t)(early ? eroute : el.route[ii]) * (2 * PATH_LEN));
-        const int pidx0 = early ? epidx : el.pidx[ii];
-        const int start_i = pidx0 < 0 ? 0 : pidx0;
-        const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
-        // the window's first point: start_i, or (early: the LDS window of round B)
-        // start_i rounded down to even; the 50-point window and the look-ahead target
-        // lie in [w0, w0 + 64): 8 points per lane
-        const int w0 = early ? (start_i & ~1) : start_i;
-        float2 pt[8];
-        float2 pend, pprev, p10;
-        if (!early) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int q = start_i + sub * 8 + j;
-                pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
-            }
-            pend = P[PATH_LEN - 1]; pprev = P[PATH_LEN - 2]; p10 = P[10];
-        }
-        Kin k = early ? gk : Kin{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
-        const bool alive = act && (early ? galive_b : el.alive[ii]) != 0;
-        const float a0_i = early ? ga0 : el.a0[ii], a1_i = early ? ga1 : el.a1[ii];
-        float cH, sH;
-        {
-            // every lane runs the update; a dead agent keeps its state (one sincosf)
-            Kin ku = k;
-            car_update_heading(ku, a0_i, a1_i, in.dt);
-            sincosf(alive ? ku.h : k.h, &sH, &cH);
-            car_update_move(ku, cH, sH);
-            if (alive) k = ku;
-        }
-        if (early) {  // round B's window: wait for the LDS DMA, then 4 aligned 16-B reads per lane
-            __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-            const float4* wl = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + grp * 128 + sub * 16);
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const float4 q = wl[m * 64];  // + m KB
-                pt[2 * m] = make_float2(q.x, q.y);
-                pt[2 * m + 1] = make_float2(q.z, q.w);
-            }
-            // lane (grp, 0): points 158, 159; lane (grp, 1): points 10, 11
-            const float4* wx = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + 4096 + grp * 128);
-            const float4 ends = wx[0], ten = wx[1];
-            pprev = make_float2(ends.x, ends.y);
-            pend = make_float2(ends.z, ends.w);
-            p10 = make_float2(ten.x, ten.y);
-        }
-        // Car::update_path_index (Car.cpp:47-74): first minimum over the window, in order
-        float bd = __builtin_inff();
-        int bi = 0x7fffffff;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int q = w0 + sub * 8 + j;  // the point's path index
-            if (q >= start_i && q < start_i + cnt) {
-                const float dx = pt[j].x - k.x, dy = pt[j].y - k.y;
-                const float d = dx * dx + dy * dy;
-                if (d < bd) { bd = d; bi = q; }
-            }
-        }
-        // minimum over the 8 lanes of the group (first index on ties): DPP swaps
-        // within quads, then the mirror within each half-row (VALU, no LDS)
-        auto take = [&](float od, int oi) {
-            if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; }
-        };
-        take(dpp_f(bd, 0xB1), __builtin_amdgcn_mov_dpp(bi, 0xB1, 0xf, 0xf, false));    // quad_perm [1,0,3,2]
-        take(dpp_f(bd, 0x4E), __builtin_amdgcn_mov_dpp(bi, 0x4E, 0xf, 0xf, false));    // quad_perm [2,3,0,1]
-        take(dpp_f(bd, 0x141), __builtin_amdgcn_mov_dpp(bi, 0x141, 0xf, 0xf, false));  // row_half_mirror
-        const int pidx = alive ? (bi == 0x7fffffff ? start_i : bi) : pidx0;
-        // look-ahead point of the observation (:444-452), picked from the window
-        {
-            const int tidx = pidx + 10 < PATH_LEN - 1 ? pidx + 10 : PATH_LEN - 1;
-            const int toff = tidx - w0;
-            if (act && toff >= 0 && toff < 64 && sub == (toff >> 3)) {
-                float2 t = pt[0];
-#pragma unroll
-                for (int j = 1; j < 8; ++j) t = ((toff & 7) == j) ? pt[j] : t;
-                el.tgx[i] = t.x;
-                el.tgy[i] = t.y;
-            } else if (act && (toff < 0 || toff >= 64) && sub == 0) {
-                el.tgx[i] = P[tidx].x;
-                el.tgy[i] = P[tidx].y;
-            }
-        }
-        float rew = 0.0f, cur = 0.0f, an = 0.0f, sn = 0.0f;
-        bool succ = false;
-        float ccx[4], ccy[4];
-        car_corners_d(k.x, k.y, cH, sH, (dims ? el.len[ii] : CAR_LENGTH), (dims ? el.wid[ii] : CAR_WIDTH), ccx, ccy);
-        {  // (branch-free: every lane evaluates the terms, a dead agent's are zeroed)
-            // compute_progress / compute_stuck / compute_smooth (:15-46)
-            cur = hypotf(k.x - pend.x, k.y - pend.y);
-            const float prev = el.prev_dist[ii];
-            float r_prog = 0.0f;
-            if (prev > 0.0f) {
-                const float progress = prev - cur;
-                const float normalized = (p.max_progress > 0.0f) ? (progress / p.max_progress) : 0.0f;
-                r_prog = p.k_prog * normalized;
-            }
-            const float speed_ms = (k.v * FPS) / SCALE;
-            const float r_stuck = (speed_ms < p.v_min) ? p.k_stuck : 0.0f;
-            an = k.acc / MAX_ACC;
-            sn = k.steer / MAX_STEERING_ANGLE;
-            const float d0 = an - el.pa0[ii];
-            const float d1 = sn - el.pa1[ii];
-            const float r_smooth = p.k_sm * (d0 * d0 + d1 * d1);
-            rew = r_prog + r_stuck + r_smooth;
-            // SUCCESS by the last path segment's axis
-            const float dxr = pend.x - pprev.x, dyr = pend.y - pprev.y;
-            const bool sx_ = fabs_f(k.y - pend.y) < 15.0f && fabs_f(k.x - pend.x) < 40.0f;
-            const bool sy_ = fabs_f(k.x - pend.x) < 15.0f && fabs_f(k.y - pend.y) < 40.0f;
-            succ = fabs_f(dxr) > fabs_f(dyr) ? sx_ : sy_;
-            if (!alive) { rew = 0.0f; cur = 0.0f; an = 0.0f; sn = 0.0f; succ = false; }
-        }
-        // corner tests, one per lane: sub 0-3 corner q (screen margin, road, yellow line,
-        // line mask), sub 4-7 edge midpoint q (line mask)
-        bool oos_q = false, off_q = false, line_q = false;
-        {
-            // lane sub < 4: corner q (screen margin, road, yellow line, line mask);
-            // sub >= 4: the midpoint of edge (q, q + 1) (line mask only)
-            const int q = sub & 3;
-            float qx = ccx[0], qy = ccy[0], rx = ccx[1], ry = ccy[1];
-#pragma unroll
-            for (int u = 1; u < 4; ++u) {
-                if (q == u) { qx = ccx[u]; qy = ccy[u]; rx = ccx[(u + 1) & 3]; ry = ccy[(u + 1) & 3]; }
-            }
-            const bool corner = sub < 4;
-            const float px_ = corner ? qx : 0.5f * (qx + rx), py_ = corner ? qy : 0.5f * (qy + ry);
-            const float M = 100.0f;
-            const bool lm = is_line_px((int)px_, (int)py_, p.line_stop);
-            oos_q = alive && corner && (qx < -M || qx > float(WIDTH) + M || qy < -M || qy > float(HEIGHT) + M);
-            off_q = alive && corner && !is_on_road(qx, qy, p.rw);
-            line_q = alive && ((corner && hits_yellow_line(qx, qy, p.rw)) || lm);
-        }
-        const bool any_oos = (ballot(oos_q) & gmask) != 0ull;
-        const bool any_off = (ballot(off_q) & gmask) != 0ull;
-        const bool any_line = (ballot(line_q) & gmask) != 0ull;
-        if (act) {
-            if (sub < 4) {
-                reinterpret_cast<float*>(&el.cx[i])[sub] = ccx[sub];
-                reinterpret_cast<float*>(&el.cy[i])[sub] = ccy[sub];
-            }
-            if (sub == 0) {
-                uint8_t done = 0, status = ST_ALIVE;
-                if (!alive) { done = 1; status = ST_DEAD; }
-                else if (succ) { done = 1; status = ST_SUCCESS; }
-                else if (any_oos || any_off) { done = 1; status = ST_CRASH_WALL; }
-                else if (any_line) { done = 1; status = ST_CRASH_LINE; }
-                el.x[i] = k.x; el.y[i] = k.y; el.v[i] = k.v; el.h[i] = k.h; el.c[i] = cH; el.s[i] = sH;
-                el.acc[i] = k.acc; el.steer[i] = k.steer; el.pidx[i] = pidx;
-                if (alive) { el.prev_dist[i] = cur; el.pa0[i] = an; el.pa1[i] = sn; }
-                el.t10x[i] = p10.x; el.t10y[i] = p10.y;
-                el.done[i] = done; el.status[i] = status; el.rew[i] = rew;
-                el.col[i] = 0ull; el.colnpc[i] = 0;
-            }
-        }
+        ego_phase1<early, dims>(p, in, el, i, act, ii, grp, sub, gmask, eroute, epidx, gk, galive_b, ga0, ga1);
     }
     // The LDS DMA of round B has landed (the loop waited for it before reading the
     // window), but the compiler cannot see that on every path into here, and with an
@@ -1899,6 +1938,63 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         __syncthreads();  // barrier B: obstacle table, candidate masks, respawns
     }
     return CarsCtx{step_no, do_reset, ncnt, false};
+}
+
+// The traffic early split's LiDAR wave before its road march (the car waves' cars_pre<TSC>
+// meanwhile run the NPC phase): the egos of the workgroup's PK envs, one each, from HBM
+// into their envs' car LDS exactly as cars_pre's round A and auto-reset write them (lane j
+// = env es[j]), then phase 1 for all of them in one pass (lane group j = env j's ego in its
+// own LDS: the group's CarsLDS pointers differ per lane).  Returns the slots' alive mask.
+template <int PK, int KF>
+__device__ __forceinline__ unsigned long long ts_ego_phase(const SimParams& p, const StepInputs& in,
+                                                           unsigned char* step_lds, const int reg, const int* es,
+                                                           const int lane) {
+    const bool on = lane < PK;
+    int ee = es[0];
+#pragma unroll
+    for (int j = 1; j < PK; ++j) ee = lane == j ? es[j] : ee;
+    const uint32_t ug = (uint32_t)ee;  // (one ego per env: the agent index is the env index)
+    const uint8_t pending_b = ldu(gmem(p.pending_reset), ug);
+    const float a0 = ldu(gmem(in.actions), 2 * ug), a1 = ldu(gmem(in.actions), 2 * ug + 1);
+    const int route_l = ldu(egoi(p, EF_ROUTE), ug);
+    const float x0 = ldu(egof(p, EF_X), ug), y0 = ldu(egof(p, EF_Y), ug), v0 = ldu(egof(p, EF_V), ug);
+    const float h0 = ldu(egof(p, EF_H), ug), acc0 = ldu(egof(p, EF_ACC), ug), steer0 = ldu(egof(p, EF_STEER), ug);
+    const float pd0 = ldu(egof(p, EF_PREV_DIST), ug), pa00 = ldu(egof(p, EF_PA0), ug), pa10 = ldu(egof(p, EF_PA1), ug);
+    const float sx0 = ldu(egof(p, EF_SX), ug), sy0 = ldu(egof(p, EF_SY), ug), sv0 = ldu(egof(p, EF_SV), ug);
+    const float sh0 = ldu(egof(p, EF_SH), ug);
+    const int pidx_l = ldu(egoi(p, EF_PIDX), ug), intent_l = ldu(egoi(p, EF_INTENT), ug);
+    const uint8_t alive_l = ldu(gmem(p.ego.alive), ug);
+    __builtin_amdgcn_sched_barrier(0);
+    const CarsLDS el = carve_cars_lds(step_lds + (on ? lane : 0) * reg, 1, KF);
+    const bool do_reset = in.auto_reset && pending_b != 0;
+    if (on) {
+        el.a0[0] = a0; el.a1[0] = a1;
+        el.route[0] = route_l;
+        el.x[0] = x0; el.y[0] = y0; el.v[0] = v0; el.h[0] = h0;
+        el.acc[0] = acc0; el.steer[0] = steer0; el.prev_dist[0] = pd0;
+        el.pa0[0] = pa00; el.pa1[0] = pa10;
+        el.sx[0] = sx0; el.sy[0] = sy0; el.sv[0] = sv0; el.sh[0] = sh0;
+        el.pidx[0] = pidx_l; el.intent[0] = intent_l; el.alive[0] = alive_l;
+    }
+    if (on && do_reset) {  // the env was auto-reset: its ego starts from its spawn (as cars_pre)
+        const int rid = reset_route(p, in.rng_counter, ee, 0, route_l);
+        const float rx = gmem(p.rt.spawn)[3 * rid], ry = gmem(p.rt.spawn)[3 * rid + 1], rh = gmem(p.rt.spawn)[3 * rid + 2];
+        el.route[0] = rid;
+        el.x[0] = rx; el.y[0] = ry; el.v[0] = 0.0f; el.h[0] = rh;
+        el.acc[0] = 0.0f; el.steer[0] = 0.0f; el.prev_dist[0] = 0.0f; el.pa0[0] = 0.0f; el.pa1[0] = 0.0f;
+        el.sx[0] = rx; el.sy[0] = ry; el.sv[0] = 0.0f; el.sh[0] = rh;
+        el.pidx[0] = 0; el.intent[0] = gmem(p.rt.intent)[rid]; el.alive[0] = 1;
+    }
+    wave_lds_sync();
+    const unsigned long long am = ballot(on && el.alive[0] != 0);
+    // phase 1, lane group g = env g's ego (N = 1: agent 0 of its own LDS)
+    const int grp = lane >> 3, sub = lane & 7;
+    const unsigned long long gmask = 0xFFull << (grp * 8);
+    const bool act = grp < PK;
+    const CarsLDS eg = carve_cars_lds(step_lds + (act ? grp : 0) * reg, 1, KF);
+    ego_phase1<false, false>(p, in, eg, 0, act, 0, grp, sub, gmask, 0, 0, Kin{}, 0, 0.0f, 0.0f);
+    wave_lds_sync();
+    return am;
 }
 
 // The rest of the car part (after the LiDAR in k_step, right after cars_pre in
@@ -2354,7 +2450,7 @@ struct LidarSrcLdsEnvs {
     const CarsLDS& el0;  // env 0's arrays
     int reg;             // bytes between two envs' car LDS
     const float* relp;
-    const int* env;      // [ENVS] the workgroup's envs (wave-uniform)
+    int env[ENVS];       // the workgroup's envs (wave-uniform)
     __device__ int off(int g) const {
         int j = 0;
 #pragma unroll
