@@ -3144,6 +3144,11 @@ constexpr int kEsplitWpe = 8;
 #define MEV_TS_ENVS 4
 #endif
 constexpr int kTsplitEnvs = MEV_TS_ENVS;
+// the traffic early split's LiDAR wave issues at level 1 (its ego phase 1 and road march
+// have slack beside a heavy env's NPC phase, which sets the kernel's end): config 4
+// 143.4 -> 151.2 M against level 3 (profiles/r5_ab_tsprio*_cfg4.txt, four rounds; 2: 149 M,
+// 0: 150 M)
+constexpr int kPrioTsplitLidar = 1;
 #ifndef MEV_TS_BEAMS
 #define MEV_TS_BEAMS kFixedRays
 #endif
