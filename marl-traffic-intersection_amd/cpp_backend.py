@@ -190,8 +190,12 @@ class _LidarGroup:
     stay identical; reads come from the first; car i's observation row from handle
     row_of[i]."""
 
+    # every call that changes the env or how it is stepped (not set_beam_angles: each handle
+    # keeps its own configuration); snapshot / restore and the gather have no per-car-LiDAR use
     _ALL = ("set_state", "set_car_dims", "set_traffic_routes", "set_ego_routes", "reset", "configure",
-            "configure_traffic", "set_reward", "add_route")
+            "configure_traffic", "set_reward", "add_route", "set_reset_routes", "set_stream", "use_own_stream",
+            "set_step_kernel", "set_step_pack", "set_step_split", "set_env_deal", "set_serve", "kernel_timing")
+    _REFUSED = ("snapshot", "restore", "comm_init", "set_gather_format", "set_beam_angles")
 
     def __init__(self, handles, row_of):
         self._hs = list(handles)
@@ -199,6 +203,8 @@ class _LidarGroup:
         self._outs = None
 
     def __getattr__(self, name):
+        if name in _LidarGroup._REFUSED:
+            raise AttributeError(f"{name}: not available on an env whose cars have different LiDAR configurations")
         if name in _LidarGroup._ALL:
             def call(*a, **k):
                 r = [getattr(h, name)(*a, **k) for h in self._hs]
