@@ -33,6 +33,9 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                "ts1": ["-DMEV_EXP_TS=1"], "ts2": ["-DMEV_EXP_TS=2"], "ts3": ["-DMEV_EXP_TS=3"],
                "tsilp2": ["-DMEV_TS_ILP=2"], "ts2env": ["-DMEV_TS_ENVS=2"], "tswpe5": ["-DMEV_TS_WPE=5"], "tslp3": ["-DMEV_TS_LPRIO=3"], "tslp2": ["-DMEV_TS_LPRIO=2"],
                "tslp0": ["-DMEV_TS_LPRIO=0"], "tslp1c3": ["-DMEV_TS_CPRIO=3"],
+               # the LiDAR wave of workgroups whose envs all hold fewer than T NPCs at level L
+               "tsad2l2": ["-DMEV_TS_ADAPT=2", "-DMEV_TS_ALPRIO=2"], "tsad2l3": ["-DMEV_TS_ADAPT=2", "-DMEV_TS_ALPRIO=3"],
+               "tsad1l3": ["-DMEV_TS_ADAPT=1", "-DMEV_TS_ALPRIO=3"],
                # the early split without traffic: the road march's / the car wave's issue level
                "esr2": ["-DMEV_ES_RPRIO=2"], "esr1": ["-DMEV_ES_RPRIO=1"], "esc3": ["-DMEV_ES_CPRIO=3"], "tswpe7": ["-DMEV_TS_WPE=7"],
                "tsb64": ["-DMEV_TS_BEAMS=64"], "ts2b64": ["-DMEV_TS_BEAMS=64", "-DMEV_EXP_TS=2"],
