@@ -83,6 +83,56 @@ def test_gather_world1_row_equals_plain_step(mev, fmt):
         gat.close()
 
 
+@pytest.mark.parametrize("fmt", [0, 1], ids=["f32", "lidar_u8"])
+def test_gather_world1_traffic_early_split(mev, fmt):
+    """Config-4 shape at 1024 envs (the traffic early split: four car waves and one
+    LiDAR wave per workgroup, which writes the LiDAR codes and the dead egos' rows
+    itself): the gathered row equals the plain step's bit for bit, with dead egos (code
+    255 rows) and no auto-reset.  (The state format is refused with traffic.)"""
+    from marl_traffic_intersection_amd import _capi, sharding
+    import torch.utils.dlpack as tdl
+
+    E, T = 1024, 80
+    cfg = dict(num_envs=E, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=2.0, max_npcs=32,
+               respawn_enabled=0, device=0)
+    plain = mev.Handle(**cfg)
+    gat = mev.Handle(**cfg)
+    try:
+        assert plain.step_split() == 2 and gat.step_split() == 2
+        if fmt:
+            gat.set_gather_format(fmt)
+        gat.comm_init(_capi.comm_unique_id(), world=1, rank=0, root=0)
+        lay = sharding.PackedOutputs(E, 1, plain.D, fmt=fmt, lidar_slots=gat.lidar_slots(),
+                                     table=gat.lidar_decode_table() if fmt == 1 else None)
+        # every 7th env's ego dead (Car::alive written through set_state; the reference's step
+        # never revives it): the LiDAR wave writes those rows itself (zeros / code 255)
+        for h in (plain, gat):
+            st = h.get_state()
+            st["alive"][::7, 0] = 0
+            h.set_state(st)
+        rng = np.random.default_rng(6)
+        dead = 0
+        for t in range(T):
+            act = rng.uniform(-1, 1, (E, 1, 2)).astype(np.float32)
+            act[..., 0] = np.abs(act[..., 0])  # (throttle on: egos reach walls and cars)
+            # (no auto-reset: the dead egos stay dead, the envs that ended stay over; the same
+            # seed: the same Philox spawns)
+            ref = plain.step(act)
+            gat.step(act, gather=True,
+                     out={"agents_alive": np.zeros(E, np.int32), "step": np.zeros(E, np.int32)})
+            gat.gather_wait(30000)
+            dbuf = tdl.from_dlpack(gat.output_dlpack("gathered"))
+            got = lay.unpack(dbuf.cpu().numpy()[0])
+            for k in FIELDS:
+                assert np.array_equal(_bits(got[k]), _bits(ref[k])), (t, k)
+            dead += int((ref["agents_alive"] == 0).sum())
+        assert dead > 0  # dead egos' rows were exercised
+        gat.comm_destroy()
+    finally:
+        plain.close()
+        gat.close()
+
+
 def test_gather_argument_errors(mev):
     from marl_traffic_intersection_amd import _capi
 
