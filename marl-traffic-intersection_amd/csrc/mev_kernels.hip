@@ -3140,27 +3140,18 @@ constexpr int kSplitWpe = 4;
 constexpr int kEsplitWpe = 8;
 // the traffic early split: kTsplitEnvs envs (car waves) + one LiDAR wave per workgroup,
 // kTsplitWpe waves per SIMD (config 4: 4096 envs -> 5120 waves on 1024 SIMDs)
-#ifndef MEV_TS_ENVS
-#define MEV_TS_ENVS 4
-#endif
-constexpr int kTsplitEnvs = MEV_TS_ENVS;
+constexpr int kTsplitEnvs = 4;
 // the traffic early split's LiDAR wave issues at level 1 (its ego phase 1 and road march
 // have slack beside a heavy env's NPC phase, which sets the kernel's end): config 4
 // 143.4 -> 151.2 M against level 3 (profiles/r5_ab_tsprio*_cfg4.txt, four rounds; 2: 149 M,
 // 0: 150 M)
 constexpr int kPrioTsplitLidar = 1;
-#ifndef MEV_TS_BEAMS
-#define MEV_TS_BEAMS kFixedRays
-#endif
-constexpr int kTsplitRays = MEV_TS_BEAMS;  // LiDAR pool beams per env
+constexpr int kTsplitRays = kFixedRays;  // LiDAR pool beams per env
 // (6, not the 5 that 1024 five-wave workgroups need on 1024 SIMDs: a workgroup's five waves
 // do not spread evenly over a CU's four SIMDs, and at a 5-wave budget (93 VGPRs) 4096 envs
 // did not fit one residency round -- 38.3 us against 28.7 us at 3072 envs; at 80 VGPRs
 // they do, profiles/r5_ts_wpe_cfg4.txt)
-#ifndef MEV_TS_WPE
-#define MEV_TS_WPE (MEV_TS_ENVS == 4 ? 6 : (MEV_TS_ENVS == 2 ? 6 : 4))
-#endif
-constexpr int kTsplitWpe = MEV_TS_WPE;
+constexpr int kTsplitWpe = 6;
 constexpr int kPrioEsplitRoad = 3;
 constexpr int kPrioEsplitCars = 2;
 constexpr int kPrioEsplitCarPhase = 1;

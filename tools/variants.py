@@ -27,18 +27,9 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                # timing-only: k_step stopped after the car part / LiDAR phase 1 / 2 / 3 (instruction budgets)
                "stop1": ["-DMEV_EXP_STOP=1"], "stop2": ["-DMEV_EXP_STOP=2"], "stop3": ["-DMEV_EXP_STOP=3"],
                "stop4": ["-DMEV_EXP_STOP=4"], "stop0": ["-DMEV_EXP_STOP=0"],
-               # the traffic early split (mev_set_step_split(3)): timing-only cuts -- the LiDAR wave
-               # without its work after barrier B / without any work, the car waves without cars_post
-               # -- and the LiDAR wave's phase 1 at two agents per pass (exact)
-               "ts1": ["-DMEV_EXP_TS=1"], "ts2": ["-DMEV_EXP_TS=2"], "ts3": ["-DMEV_EXP_TS=3"],
-               "tsilp2": ["-DMEV_TS_ILP=2"], "ts2env": ["-DMEV_TS_ENVS=2"], "tswpe5": ["-DMEV_TS_WPE=5"], "tslp3": ["-DMEV_TS_LPRIO=3"], "tslp2": ["-DMEV_TS_LPRIO=2"],
-               "tslp0": ["-DMEV_TS_LPRIO=0"], "tslp1c3": ["-DMEV_TS_CPRIO=3"],
-               # the LiDAR wave of workgroups whose envs all hold fewer than T NPCs at level L
-               "tsad2l2": ["-DMEV_TS_ADAPT=2", "-DMEV_TS_ALPRIO=2"], "tsad2l3": ["-DMEV_TS_ADAPT=2", "-DMEV_TS_ALPRIO=3"],
-               "tsad1l3": ["-DMEV_TS_ADAPT=1", "-DMEV_TS_ALPRIO=3"],
-               # the early split without traffic: the road march's / the car wave's issue level
-               "esr2": ["-DMEV_ES_RPRIO=2"], "esr1": ["-DMEV_ES_RPRIO=1"], "esc3": ["-DMEV_ES_CPRIO=3"], "tswpe7": ["-DMEV_TS_WPE=7"],
-               "tsb64": ["-DMEV_TS_BEAMS=64"], "ts2b64": ["-DMEV_TS_BEAMS=64", "-DMEV_EXP_TS=2"],
+               # (round 5's traffic / early-split variants -- timing cuts ts1-3, tsb64, ts2env, tswpe*,
+               # tsilp2, tslp*, tsad*, esr*, esc3 -- were removed from the sources after measuring; their
+               # results are in DESIGN.md §9 / §3.1e, the macros in git history up to commit 55a6684)
                # compiler options (exact): SLP vectorization back on, no loop vectorization, the max-ilp
                # scheduler, kernel-argument preloading, AMDGPU register-pressure trackers, no unclustered
                # high-pressure reschedule stage, latency over occupancy, relaxed occupancy
