@@ -140,3 +140,35 @@ def test_render_masks_match_reference_geometry():
         g = np.load(f"{G.GOLDEN_DIR}/static_lanes{L}.npz")["grid"]
         assert np.array_equal(render.road_mask(L), (g & 1).astype(bool))
         assert np.array_equal(render.line_mask(L), (g & 4).astype(bool))
+
+
+def test_lidars_setter_groups_cars_by_configuration():
+    """IntersectionEnv.lidars (cpp/bindings.cpp:68, per-car Lidar objects): one configuration
+    for every car keeps one handle; different ones become a per-car configuration (one device
+    handle per distinct key when the env is stepped); cars added later get
+    add_car_with_route's own 96-ray Lidar; reset() goes back to that default.  Host logic
+    only -- no handle is created here."""
+    env = cpp_backend.IntersectionEnv(3)
+    env.reset()
+    for s, e in [("IN_1", "OUT_4"), ("IN_4", "OUT_7"), ("IN_7", "OUT_10")]:
+        env.add_car_with_route(s, e)
+    env.lidars = [cpp_backend.Lidar(64, 360.0, 250.0, 4.0)] * 3  # one configuration: uniform
+    assert env._lidar == (64, 360.0, 250.0, 4.0)
+    short = cpp_backend.Lidar()  # 72 offsets, 48 rays: the first 48 offsets are the beams
+    short.rays, short.max_dist = 48, 200.0
+    env.lidars = [cpp_backend.Lidar(96), short, cpp_backend.Lidar(128, 270.0)]
+    kind, keys = env._lidar
+    assert kind == "per_car" and len(keys) == 3
+    assert keys[0] == cpp_backend._default_key((96, 360.0, 250.0, 4.0))
+    assert keys[1][0] == 48 and len(keys[1][4]) == 72 and keys[1][2] == 200.0
+    assert keys[1][4][:48] == tuple(np.asarray(cpp_backend._rel_angles(72, 360.0), np.float32).tolist())[:48]
+    env.add_car_with_route("IN_10", "OUT_1")  # a new car: its own 96-ray Lidar
+    assert len(env._lidar[1]) == 4 and env._lidar[1][3] == cpp_backend._default_key(cpp_backend.DEFAULT_LIDAR)
+    with pytest.raises(ValueError, match="one per car"):
+        env.lidars = [short, cpp_backend.Lidar(96)]  # two configurations for four cars
+    bad = cpp_backend.Lidar()
+    bad.rays = 100  # more rays than offsets: the reference would read past rel_angles
+    with pytest.raises(ValueError, match="rel_angles"):
+        env.lidars = [bad] * 4
+    env.reset()
+    assert env._lidar == cpp_backend.DEFAULT_LIDAR
