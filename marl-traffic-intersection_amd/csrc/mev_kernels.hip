@@ -303,7 +303,9 @@ __device__ inline int xcd_env(int b, int E) {
 // (k = 4 envs per workgroup, the traffic early split: workgroup b takes ranks
 // 4 (b / 8) + j, j < 4, of its list; every list holds E / 8 envs whichever kernel
 // built it, so any E divisible by 32 keeps the deal a bijection)
-__device__ inline int deal_env(const SimParams& p, int ring, int b, int k = 1, int j = 0) {
+// cls (optional): the env's NPC class in the deal, i.e. its NPC count after the previous
+// step (kDealClasses - 1: that many or more)
+__device__ inline int deal_env(const SimParams& p, int ring, int b, int k = 1, int j = 0, int* cls = nullptr) {
     const int x = b & (kDealLists - 1);
     int i = (b >> 3) * k + j;
     const __attribute__((address_space(1))) int32_t* cnt =
@@ -317,6 +319,7 @@ __device__ inline int deal_env(const SimParams& p, int ring, int b, int k = 1, i
         if (c == k && i >= n[k]) { i -= n[k]; c = k - 1; }
     }
     i = i < p.E - 1 ? i : p.E - 1;  // (the host keeps the rings consistent; never out of bounds)
+    if (cls) *cls = c;
     const size_t ring_off = (size_t)ring * kDealLists * kDealClasses * (size_t)p.E;
     return __builtin_amdgcn_readfirstlane(gmem(p.deal_order)[ring_off + ((size_t)x * kDealClasses + c) * p.E + i]);
 }
@@ -398,9 +401,9 @@ struct NpcRegs {
 // update_traffic_flow, cpp/TrafficFlow.cpp:317-367, for env e.  Egos (positions
 // in LDS) are read for spawn blocking but not moved.  On return NpcLDS holds the compacted NPCs.
 template <bool DIMS>
-__device__ __forceinline__ NpcRegs npc_load(const SimParams& p, int e, int lane) {
+__device__ __forceinline__ NpcRegs npc_load(const SimParams& p, int e, int lane, int kload) {
     NpcRegs r{};
-    if (lane < p.K) {
+    if (lane < kload) {  // (kload <= K: the slots that can hold an NPC)
         const int g = e * p.K + lane;
         r.x = npcf(p, NF_X)[g]; r.y = npcf(p, NF_Y)[g]; r.v = npcf(p, NF_V)[g]; r.h = npcf(p, NF_H)[g];
         r.acc = npcf(p, NF_ACC)[g]; r.steer = npcf(p, NF_STEER)[g];
@@ -1559,7 +1562,7 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
 template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false, bool DIMS = false,
           bool TSC = false>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
-                                            const CarsLDS& el, NL* nl) {
+                                            const CarsLDS& el, NL* nl, int npc_cls = kDealClasses - 1) {
     static_assert(!ESPLIT || FUSED, "early split: k_step");
     static_assert(PK == 1 || (FUSED && !TRAFFIC), "several envs per wave: k_step without traffic");
     static_assert(!DIMS || (PK == 1 && !EARLY && !ESPLIT), "per-car sizes: the runtime-layout kernels");
@@ -1654,7 +1657,9 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         rl1 = ldu(gmem(p.rel_angles), (uint32_t)(tid + WAVE < rmax ? tid + WAVE : rmax));
     }
     NpcRegs nreg{};
-    if constexpr (TRAFFIC) nreg = npc_load<DIMS>(p, e, tid);  // in flight with the ego loads
+    // in flight with the ego loads; only the slots the env's deal class says are filled (the
+    // class is its NPC count after the previous step; the last class and no deal: every slot)
+    if constexpr (TRAFFIC) nreg = npc_load<DIMS>(p, e, tid, npc_cls < kDealClasses - 1 ? npc_cls : p.K);
     // every load above is issued before any of their values is used (a use scheduled
     // between them would put a wait for the first loads in front of the rest)
     __builtin_amdgcn_sched_barrier(0);
