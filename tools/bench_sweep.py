@@ -61,7 +61,9 @@ def run(cfg, steps, warmup, step_kernel=0, pack=0, split=0):
     h.close()
     r = dict(name=cfg["name"], workload=cfg["desc"], agent_steps_per_s=round(E * N / dt, 1),
              ms_per_step=round(dt * 1e3, 5), step_kernel="k_step (fused)" if fused else "k_cars + k_lidar",
-             envs_per_wave=pk, waves_per_workgroup=2 if split else 1,
+             # traffic early split: four car waves (one env each) + one LiDAR wave per workgroup
+             envs_per_wave=pk, waves_per_workgroup=(5 if cfg.get("traffic") and split == 2 else
+                                                    2 if split else 1),
              mean_npcs=round(npc, 3))
     if fused:
         r["k_step_ms_events"] = round(c / n, 5)
