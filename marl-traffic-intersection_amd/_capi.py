@@ -38,7 +38,7 @@ PATH_LEN = 160
 EXPORTED = (
     "mev_last_error", "mev_abi_version", "mev_device_count", "mev_config_default", "mev_create", "mev_destroy",
     "mev_get_config", "mev_obs_dim", "mev_set_stream", "mev_sync", "mev_num_points", "mev_point_xy",
-    "mev_route_id", "mev_route_info", "mev_path_len", "mev_set_ego_routes", "mev_set_traffic_routes",
+    "mev_route_id", "mev_route_info", "mev_route_len", "mev_path_len", "mev_set_ego_routes", "mev_set_traffic_routes",
     "mev_default_traffic_routes", "mev_reset", "mev_step", "mev_get_outputs", "mev_get_state", "mev_set_state",
     "mev_device_outputs", "mev_npc_overflow", "mev_npc_stats", "mev_use_own_stream", "mev_debug_stamps",
     "mev_configure", "mev_configure_traffic", "mev_set_reward", "mev_car_update", "mev_car_check_collision",
@@ -47,7 +47,7 @@ EXPORTED = (
     "mev_set_step_split", "mev_get_step_split", "mev_set_env_deal", "mev_set_serve", "mev_serve_stats",
     "mev_packed_layout", "mev_comm_unique_id", "mev_comm_init", "mev_comm_destroy", "mev_gather_result",
     "mev_gather_wait", "mev_output_dlpack", "mev_packed_layout2", "mev_set_gather_format", "mev_lidar_decode_table",
-    "mev_unpack_gathered", "mev_add_route", "mev_set_car_dims", "mev_get_car_dims", "mev_car_dims_active",
+    "mev_unpack_gathered", "mev_add_route", "mev_add_route_n", "mev_set_car_dims", "mev_get_car_dims", "mev_car_dims_active",
     "mev_set_beam_angles", "mev_get_beam_angles", "mev_decode_errors",
 )
 
@@ -176,6 +176,8 @@ def load_library(variant: str = None):
     L.mev_gather_wait.argtypes = [_vp, ctypes.c_int32]
     L.mev_unpack_gathered.argtypes = [_vp, _vp, ctypes.c_int32, _vp]
     L.mev_add_route.argtypes = [_vp, f32p, ctypes.c_int32, i32p]
+    L.mev_add_route_n.argtypes = [_vp, f32p, ctypes.c_int32, ctypes.c_int32, i32p]
+    L.mev_route_len.argtypes = [_vp, ctypes.c_int32, i32p]
     L.mev_output_dlpack.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(_vp)]
     L.mev_set_car_dims.argtypes = [_vp, f32p, f32p]
     L.mev_get_car_dims.argtypes = [_vp, f32p, f32p]
@@ -381,15 +383,21 @@ class Handle:
                                         ctypes.byref(intent), spawn.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
         return path, intent.value, spawn
 
+    def route_len(self, route: int) -> int:
+        """Points of a route's path (160, or a shorter path's own n; mev_route_len)."""
+        n = ctypes.c_int32()
+        _check(self._lib.mev_route_len(self._h, int(route), ctypes.byref(n)))
+        return n.value
+
     def add_route(self, path, intent: int) -> int:
-        """Append a route of the caller's own (path [160, 2] f32, intent 0 straight / 1 left / 2 right) to
-        the route table (mev_add_route); returns its id."""
+        """Append a route of the caller's own (path [n, 2] f32 with 2 <= n <= 160, intent 0 straight /
+        1 left / 2 right) to the route table (mev_add_route_n); returns its id."""
         a = np.ascontiguousarray(path, np.float32)
-        if a.shape != (PATH_LEN, 2):
-            raise ValueError(f"a route path has {PATH_LEN} points (x, y), got shape {a.shape}")
+        if a.ndim != 2 or a.shape[1] != 2 or not 2 <= a.shape[0] <= PATH_LEN:
+            raise ValueError(f"a route path has 2 .. {PATH_LEN} points (x, y), got shape {a.shape}")
         r = ctypes.c_int32()
-        _check(self._lib.mev_add_route(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), int(intent),
-                                       ctypes.byref(r)))
+        _check(self._lib.mev_add_route_n(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), a.shape[0],
+                                         int(intent), ctypes.byref(r)))
         return r.value
 
     def point_xy(self, point: int):

@@ -19,10 +19,11 @@ Deviations from MARLEnv (all outside the hot path):
    (every list Lidar() or add_car_with_route makes, and any prefix of one, is), with at
    least `rays` entries and rays >= 1 (the reference reads past the end otherwise);
    `lidars` must hold one Lidar per car, or one configuration for all of them;
- * Car.path may be any 160-point path (every path MARLEnv itself generates has
-   160 points, RouteGen.cpp:111-205); a path that is not a lane-layout route is
-   appended to the device route table (mev_add_route); other lengths raise
-   ValueError;
+ * Car.path may be any path of 2 .. 160 points (every path MARLEnv itself
+   generates has 160, RouteGen.cpp:111-205); a path that is not a lane-layout route
+   is appended to the device route table (mev_add_route_n); longer paths, and
+   shorter ones than 2 points, raise ValueError, as does a traffic car whose
+   path_index is not below its path's length (its ghost scan would differ);
  * Car.length / Car.width (bindings.cpp:24-25) are simulated per car, as in the
    reference (status corners, SAT collisions, LiDAR boxes; mev_set_car_dims), in
    |value| <= 1e4 px;
@@ -481,7 +482,8 @@ class IntersectionEnv:
             c._route = int(get("route", i))
             path = self._paths.get(c._route)
             if path is None:  # route tables are constant for the env's lane count: built once per route
-                path = self._paths[c._route] = [tuple(map(float, p)) for p in h.route_info(c._route)[0]]
+                pts = h.route_info(c._route)[0][: h.route_len(c._route)]  # (a shorter path's own points)
+                path = self._paths[c._route] = [tuple(map(float, p)) for p in pts]
             c.path = list(path)
             if dims is not None:  # Car::length / Car::width (cpp/Car.h:19-20)
                 c.length, c.width = float(dims[0 if ego else 1][0, i, 0]), float(dims[0 if ego else 1][0, i, 1])
@@ -578,7 +580,7 @@ class IntersectionEnv:
 
     def _route_of(self, c: Car) -> int:
         """The route id of Car.path (read-write in MARLEnv, cpp/bindings.cpp:29): a lane-layout route or one
-        registered before, else a new route of the caller's own (mev_add_route; 160 points)."""
+        registered before, else a new route of the caller's own (mev_add_route_n; 2 .. 160 points)."""
         if len(c.path) == 0:
             if c._route >= 0:
                 return c._route
@@ -592,9 +594,9 @@ class IntersectionEnv:
         r = self._route_ids.get(want.tobytes())
         if r is not None:
             return r
-        if want.shape != (_capi.PATH_LEN, 2):
-            raise ValueError(f"Car.path must have {_capi.PATH_LEN} points (every path the reference generates "
-                             f"does, RouteGen.cpp:111-205); got {len(want)}")
+        if not 2 <= len(want) <= _capi.PATH_LEN:
+            raise ValueError(f"Car.path must have 2 .. {_capi.PATH_LEN} points (every path the reference "
+                             f"generates has {_capi.PATH_LEN}, RouteGen.cpp:111-205); got {len(want)}")
         intent = min(max(int(c.intention), 0), 2)
         r = self._h.add_route(want, intent)
         self._custom.append((want.copy(), intent))
@@ -637,6 +639,11 @@ class IntersectionEnv:
         if n == 0:
             self._routes = []
             return
+        for c in s.traffic_cars:
+            # past the end of a short path the reference's ghost scan is empty (TrafficFlow.cpp:89);
+            # the device row repeats the last point there (mev_add_route_n)
+            if 0 < len(c.path) < _capi.PATH_LEN and c.path_index >= len(c.path):
+                raise ValueError(f"traffic car path_index {c.path_index} is past its {len(c.path)}-point path")
         if self._h is None or self._h.N != n or self._h_lidar != lidar:
             if self._h is not None:
                 self._h.close()

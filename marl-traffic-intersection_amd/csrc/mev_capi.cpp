@@ -53,7 +53,8 @@ struct mev_handle {
     int D = 0, lidar_slots = 0, P = 0, nroutes = 0;
     int route_cap = 0;  // routes the device route tables have room for (mev_add_route)
     std::vector<mev::LanePoint> pts;
-    std::vector<float> h_paths, h_spawn;
+    std::vector<float> h_paths, h_spawn;  // h_paths: [nroutes][ROUTE_PTS][2] (mev_world.h)
+    std::vector<int32_t> h_len;           // points of each route's path (2 .. PATH_LEN)
     std::vector<float> h_pbox;  // [nroutes][3][4] piece bounding boxes (RouteTab::pbox)
     std::vector<int32_t> h_intent;
     // route_hash[r]: FNV-1a of routes [0, r) (paths and intents), so a snapshot or a gather
@@ -67,7 +68,7 @@ struct mev_handle {
                 const uint8_t* b = static_cast<const uint8_t*>(p);
                 for (size_t i = 0; i < n; ++i) x = (x ^ b[i]) * 1099511628211ull;
             };
-            mix(&h_paths[r * 2 * mev::PATH_LEN], 2 * mev::PATH_LEN * sizeof(float));
+            mix(&h_paths[r * 2 * mev::ROUTE_PTS], 2 * mev::ROUTE_PTS * sizeof(float));
             mix(&h_intent[r], sizeof(int32_t));
             route_hash.push_back(x);
         }
@@ -312,14 +313,16 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     h->nroutes = h->P * h->P;
     h->route_cap = h->nroutes;
     h->pts = mev::build_lane_points(c.num_lanes);
-    h->h_paths.resize(size_t(h->nroutes) * 2 * mev::PATH_LEN);
+    h->h_paths.resize(size_t(h->nroutes) * 2 * mev::ROUTE_PTS);
+    h->h_len.assign(size_t(h->nroutes), mev::PATH_LEN);
     h->h_intent.resize(size_t(h->nroutes));
     h->h_spawn.resize(size_t(h->nroutes) * 3);
     for (int s = 0; s < h->P; ++s)
         for (int e = 0; e < h->P; ++e) {
             const int r = s * h->P + e;
-            float* path = &h->h_paths[size_t(r) * 2 * mev::PATH_LEN];
+            float* path = &h->h_paths[size_t(r) * 2 * mev::ROUTE_PTS];
             h->h_intent[size_t(r)] = mev::generate_route(h->pts, c.num_lanes, s, e, path);
+            std::copy(path + 2 * (mev::PATH_LEN - 2), path + 2 * mev::PATH_LEN, path + 2 * mev::ROUTE_END);
             h->h_spawn[size_t(3 * r)] = h->pts[size_t(s)].x;
             h->h_spawn[size_t(3 * r + 1)] = h->pts[size_t(s)].y;
             h->h_spawn[size_t(3 * r + 2)] = mev::spawn_heading(path);
@@ -327,7 +330,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     // each route's pieces [0, 50), [50, 110), [110, 160): bounding boxes of the float points
     h->h_pbox.resize(size_t(h->nroutes) * 12);
     for (int r = 0; r < h->nroutes; ++r) {
-        const float* path = &h->h_paths[size_t(r) * 2 * mev::PATH_LEN];
+        const float* path = &h->h_paths[size_t(r) * 2 * mev::ROUTE_PTS];
         const int cut[4] = {0, 50, 110, mev::PATH_LEN};
         for (int q = 0; q < 3; ++q) {
             float x0 = path[2 * cut[q]], x1 = x0, y0 = path[2 * cut[q] + 1], y1 = y0;
@@ -638,20 +641,40 @@ int mev_route_id(const mev_handle* h, int32_t s, int32_t e, int32_t* route) {
     return MEV_OK;
 }
 
+int mev_route_len(const mev_handle* h, int32_t route, int32_t* npoints) {
+    if (!h || !npoints) return fail(MEV_E_INVALID, "null argument");
+    if (route < 0 || route >= h->nroutes) return fail(MEV_E_RANGE, "route out of range");
+    *npoints = h->h_len[size_t(route)];
+    return MEV_OK;
+}
+
 int mev_route_info(const mev_handle* h, int32_t route, float* path, int32_t* intent, float* spawn) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (route < 0 || route >= h->nroutes) return fail(MEV_E_RANGE, "route out of range");
-    if (path) memcpy(path, &h->h_paths[size_t(route) * 2 * mev::PATH_LEN], sizeof(float) * 2 * mev::PATH_LEN);
+    if (path) memcpy(path, &h->h_paths[size_t(route) * 2 * mev::ROUTE_PTS], sizeof(float) * 2 * mev::PATH_LEN);
     if (intent) *intent = h->h_intent[size_t(route)];
     if (spawn) memcpy(spawn, &h->h_spawn[size_t(3 * route)], sizeof(float) * 3);
     return MEV_OK;
 }
 
 int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* route) {
-    if (!h || !path || !route) return fail(MEV_E_INVALID, "null argument");
+    return mev_add_route_n(h, path, mev::PATH_LEN, intent, route);
+}
+
+int mev_add_route_n(mev_handle* h, const float* path_in, int32_t npoints, int32_t intent, int32_t* route) {
+    if (!h || !path_in || !route) return fail(MEV_E_INVALID, "null argument");
     if (intent < 0 || intent > 2) return fail(MEV_E_INVALID, "intent must be 0 (straight), 1 (left) or 2 (right)");
-    for (int i = 0; i < 2 * mev::PATH_LEN; ++i)
-        if (!(fabsf(path[i]) < 1.0e6f)) return fail(MEV_E_INVALID, "path points must be finite (|coordinate| < 1e6)");
+    if (npoints < 2 || npoints > mev::PATH_LEN) return fail(MEV_E_INVALID, "a route path has 2 .. 160 points");
+    for (int i = 0; i < 2 * npoints; ++i)
+        if (!(fabsf(path_in[i]) < 1.0e6f)) return fail(MEV_E_INVALID, "path points must be finite (|coordinate| < 1e6)");
+    // the table row: the n points, padded with the last one, then the last segment (mev_world.h)
+    float path[2 * mev::ROUTE_PTS] = {};
+    for (int i = 0; i < mev::PATH_LEN; ++i) {
+        const int q = i < npoints ? i : npoints - 1;
+        path[2 * i] = path_in[2 * q];
+        path[2 * i + 1] = path_in[2 * q + 1];
+    }
+    std::copy(path_in + 2 * (npoints - 2), path_in + 2 * npoints, path + 2 * mev::ROUTE_END);
     if (h->nroutes >= 32767) return fail(MEV_E_INVALID, "too many routes (the state gather format ships i16 ids)");
     if (h->comm && h->gather_fmt == MEV_GATHER_STATE)  // every rank's route ids are decoded with the root's table
         return fail(MEV_E_INVALID, "routes cannot be added while a state-format gather communicator exists");
@@ -659,7 +682,8 @@ int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* rou
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     const int r = h->nroutes;
-    h->h_paths.insert(h->h_paths.end(), path, path + 2 * mev::PATH_LEN);
+    h->h_paths.insert(h->h_paths.end(), path, path + 2 * mev::ROUTE_PTS);
+    h->h_len.push_back(npoints);
     h->h_intent.push_back(intent);
     h->h_spawn.push_back(path[0]);  // add_car_with_route's spawn: the path's first point (RouteGen.cpp:111-205)
     h->h_spawn.push_back(path[1]);
@@ -678,7 +702,7 @@ int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* rou
     // the four route tables: the new route's rows go into spare capacity; a full table is
     // reallocated at twice the routes (so n added routes cost O(log n) reallocations, each a
     // hipFree that waits for the device) and uploaded whole
-    const size_t per[4] = {2 * mev::PATH_LEN * sizeof(float), sizeof(int32_t), 3 * sizeof(float), 12 * sizeof(float)};
+    const size_t per[4] = {2 * mev::ROUTE_PTS * sizeof(float), sizeof(int32_t), 3 * sizeof(float), 12 * sizeof(float)};
     const void* src[4] = {h->h_paths.data(), h->h_intent.data(), h->h_spawn.data(), h->h_pbox.data()};
     if (r < h->route_cap) {
         void* cur[4] = {h->d_paths, h->d_intent, h->d_spawn_tab, h->d_pbox};
@@ -687,7 +711,8 @@ int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* rou
             e = hipMemcpy(static_cast<uint8_t*>(cur[k]) + size_t(r) * per[k],
                           static_cast<const uint8_t*>(src[k]) + size_t(r) * per[k], per[k], hipMemcpyHostToDevice);
         if (e != hipSuccess) {
-            h->h_paths.resize(h->h_paths.size() - 2 * mev::PATH_LEN);
+            h->h_paths.resize(h->h_paths.size() - 2 * mev::ROUTE_PTS);
+            h->h_len.pop_back();
             h->h_intent.pop_back();
             h->h_spawn.resize(h->h_spawn.size() - 3);
             h->h_pbox.resize(h->h_pbox.size() - 12);
@@ -708,7 +733,8 @@ int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* rou
     }
     if (e != hipSuccess) {
         for (void* q : np) if (q) (void)hipFree(q);
-        h->h_paths.resize(h->h_paths.size() - 2 * mev::PATH_LEN);
+        h->h_paths.resize(h->h_paths.size() - 2 * mev::ROUTE_PTS);
+        h->h_len.pop_back();
         h->h_intent.pop_back();
         h->h_spawn.resize(h->h_spawn.size() - 3);
         h->h_pbox.resize(h->h_pbox.size() - 12);

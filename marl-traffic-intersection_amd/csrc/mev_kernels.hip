@@ -703,7 +703,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // each, 8 window points per lane, first minimum wins); returns the new index
     // and leaves the 64-point window in pt
     auto npc_window = [&](int kk, int idx, float x, float y, float2* pt, int& start_i) -> int {
-        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * ROUTE_PTS));
         start_i = idx < 0 ? 0 : idx;
         const int wcnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
 #pragma unroll
@@ -765,7 +765,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             nl.pidx0[k] = pidx0;
         }
         if (act && sub == 7) {  // the route's end point, for the arrival test after the turns
-            const float2 pe = gf2(p.rt.path + (size_t)nl.route[k] * (2 * PATH_LEN))[PATH_LEN - 1];
+            const float2 pe = gf2(p.rt.path + (size_t)nl.route[k] * (2 * ROUTE_PTS))[PATH_LEN - 1];
             nl.endx[k] = pe.x;
             nl.endy[k] = pe.y;
         }
@@ -795,7 +795,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // NPC kk's ghost points path[idx0 + lane] and path[idx0 + 64 + lane] (clamped;
     // only indices below min(idx0 + 120, 160) are used)
     auto fetch_ghost = [&](int kk, float2& a, float2& b) {
-        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * ROUTE_PTS));
         const int i0 = nl.pidx0[kk] + lane, i1 = i0 + WAVE;
         a = P[i0 < PATH_LEN ? i0 : PATH_LEN - 1];
         b = P[i1 < PATH_LEN ? i1 : PATH_LEN - 1];
@@ -804,7 +804,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // path[idx0 + 8t .. idx0 + 8t + 7] (clamped; only indices below min(idx0 + 120,
     // 160) are used)
     auto load_ghost8 = [&](int kk, float2* gp) {
-        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * ROUTE_PTS));
         const int q0 = nl.pidx0[kk] + 8 * (lane & 15);
 #pragma unroll
         for (int i = 0; i < 8; ++i) gp[i] = P[q0 + i < PATH_LEN ? q0 + i : PATH_LEN - 1];
@@ -985,7 +985,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // and the second update_path_index (:343) over path[idx0, idx0 + 50), 8 lanes
     // per NPC (7 window points each, first minimum wins)
     auto load_window = [&](int kk, float2* w) {
-        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * PATH_LEN));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * ROUTE_PTS));
         const int pidx0 = nl.pidx0[kk];
 #pragma unroll
         for (int t = 0; t < 7; ++t) {
@@ -1381,7 +1381,7 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
                                            const Kin& gk, const uint8_t galive_b, const float ga0, const float ga1) {
     constexpr bool early = EARLY;
     constexpr bool dims = DIMS;
-    const GF2 P = gf2(p.rt.path + (size_t)(early ? eroute : el.route[ii]) * (2 * PATH_LEN));
+    const GF2 P = gf2(p.rt.path + (size_t)(early ? eroute : el.route[ii]) * (2 * ROUTE_PTS));
     const int pidx0 = early ? epidx : el.pidx[ii];
     const int start_i = pidx0 < 0 ? 0 : pidx0;
     const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
@@ -1397,7 +1397,7 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
             const int q = start_i + sub * 8 + j;
             pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
         }
-        pend = P[PATH_LEN - 1]; pprev = P[PATH_LEN - 2]; p10 = P[10];
+        pend = P[ROUTE_END + 1]; pprev = P[ROUTE_END]; p10 = P[10];  // the row's last segment (mev_world.h)
     }
     Kin k = early ? gk : Kin{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
     const bool alive = act && (early ? galive_b : el.alive[ii]) != 0;
@@ -1420,7 +1420,7 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
             pt[2 * m] = make_float2(q.x, q.y);
             pt[2 * m + 1] = make_float2(q.z, q.w);
         }
-        // lane (grp, 0): points 158, 159; lane (grp, 1): points 10, 11
+        // lane (grp, 0): the row's last segment (points 160, 161); lane (grp, 1): points 10, 11
         const float4* wx = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + 4096 + grp * 128);
         const float4 ends = wx[0], ten = wx[1];
         pprev = make_float2(ends.x, ends.y);
@@ -1718,7 +1718,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // lane (grp, sub) loads chunks 4 sub .. 4 sub + 3 (instruction m: chunk 4 sub +
     // m at win + m KB + grp * 128 + sub * 16) and reads back exactly those, so each
     // lane's 8 points arrive as 4 aligned 16-B LDS reads.  A fifth instruction brings
-    // the route's last chunk (points 158, 159: lane sub 0) and path[10, 11] (sub 1).
+    // the route row's last segment (points 160, 161: lane sub 0) and path[10, 11] (sub 1).
     // Chunks past the path's end are clamped to its last one: those points lie
     // beyond every window's range and are never used.
     int eroute = 0, epidx = 0;
@@ -1733,7 +1733,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         }
         const int start_i = epidx < 0 ? 0 : epidx;
         const int sub = tid & 7;
-        const uint32_t rbase = (uint32_t)eroute * (2 * PATH_LEN * 4);  // bytes
+        const uint32_t rbase = (uint32_t)eroute * (2 * ROUTE_PTS * 4);  // bytes
         typedef const __attribute__((address_space(1))) char gchar;
         gchar* path_b = (gchar*)gmem(p.rt.path);
         __attribute__((address_space(3))) char* win = (__attribute__((address_space(3))) char*)el.win;
@@ -1744,7 +1744,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(path_b + rbase + c * 16),
                                              (__attribute__((address_space(3))) void*)(win + m * 1024), 16, 0, 0);
         }
-        const int cx = sub == 0 ? PATH_LEN / 2 - 1 : 5;  // points 158, 159 / 10, 11
+        const int cx = sub == 0 ? ROUTE_END / 2 : 5;  // points 160, 161 (last segment) / 10, 11
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(path_b + rbase + cx * 16),
                                          (__attribute__((address_space(3))) void*)(win + 4 * 1024), 16, 0, 0);
     }
@@ -3300,7 +3300,7 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
             for (int c = 0; c < p.D; ++c) row[c] = 0.0f;
             continue;
         }
-        const float* path = p.rt.path + (size_t)egoi(p, EF_ROUTE)[g] * (2 * PATH_LEN);
+        const float* path = p.rt.path + (size_t)egoi(p, EF_ROUTE)[g] * (2 * ROUTE_PTS);
         write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row);
         for (int b = 0; b < p.lidar_slots; ++b) row[OBS_HEAD + b] = p.lidar_max * p.lidar_inv;
     }
@@ -3612,7 +3612,7 @@ __global__ __launch_bounds__(WAVE) void k_decode_state(SimParams p, const uint8_
         if (bad) atomicAdd(p.overflow + 2, 1ull);
         const int rt = bad ? 0 : route;
         const int ti = pidx + 10 < PATH_LEN - 1 ? (pidx + 10 < 0 ? 0 : pidx + 10) : PATH_LEN - 1;
-        const float* path = p.rt.path + (size_t)rt * (2 * PATH_LEN);
+        const float* path = p.rt.path + (size_t)rt * (2 * ROUTE_PTS);
         const float nan = __builtin_nanf("");
         write_obs_head_tg<false>(p, i, el, (const NpcLDST<MAXK>*)nullptr, 0, bad ? nan : path[2 * ti],
                                  bad ? nan : path[2 * ti + 1], row, false);

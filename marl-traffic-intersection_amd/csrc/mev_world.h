@@ -24,6 +24,16 @@ constexpr float PHYSICS_MAX_SPEED = 8.0f;
 constexpr float PI_F = 3.14159265358979323846f;
 constexpr int NEIGHBOR_COUNT = 5;
 constexpr int PATH_LEN = 160;  // 50 + 60 + 50 points (cpp/RouteGen.cpp:160-237)
+// A route-table row: the path's PATH_LEN points, then at ROUTE_END, ROUTE_END + 1 its
+// last segment (path[n-2], path[n-1]) for the SUCCESS axis (IntersectionEnv.cpp:177-182),
+// then zeros up to ROUTE_PTS points (1408 B: rows stay aligned to 128-B lines).  A
+// written Car.path of n < PATH_LEN points is stored padded with its last point:
+// every other read of a path -- the index search's first minimum (Car.cpp:56-73),
+// the look-ahead targets clamped to n-1 (IntersectionEnv.cpp:446, TrafficFlow.cpp:55),
+// the ghost scan (TrafficFlow.cpp:89-185: a repeated point repeats its verdict),
+// path.back() -- then reads exactly what the n-point path gives.
+constexpr int ROUTE_END = PATH_LEN;
+constexpr int ROUTE_PTS = 176;
 constexpr int OBS_HEAD = 6 + 5 * NEIGHBOR_COUNT;  // 31
 
 enum Status : uint8_t { ST_ALIVE = 0, ST_DEAD = 1, ST_SUCCESS = 2, ST_CRASH_WALL = 3, ST_CRASH_LINE = 4, ST_CRASH_CAR = 5 };

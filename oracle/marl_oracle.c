@@ -61,6 +61,7 @@ typedef struct orc_env {
     lane_pt* pts;
     float* paths;        /* [nroutes][160][2]: the P*P lane-layout routes, then orc_add_route's */
     int* intent;         /* [nroutes] */
+    int* plen;           /* [nroutes]: points of each path (Car.path.size(); 160 for the lane routes) */
     int nroutes;
     float* rel;          /* [rays] */
     uint8_t* line_grid;  /* [750*750] LineMask */
@@ -246,6 +247,7 @@ static int yellow(const orc_env* e, float x, float y) {
 
 /* ------------------------------------------------------------------ cars */
 static const float* path_of(const orc_env* e, const orc_car* c) { return e->paths + (size_t)c->route * 2 * PATH_LEN; }
+static int len_of(const orc_env* e, const orc_car* c) { return e->plen[c->route]; } /* path.size() */
 
 /* Car::update, cpp/Car.cpp:9-40 */
 static void car_update(orc_car* c, float thr, float st, float dt) {
@@ -271,7 +273,8 @@ static void car_update(orc_car* c, float thr, float st, float dt) {
 static void update_path_index(const orc_env* e, orc_car* c) {
     const float* p = path_of(e, c);
     int s = c->path_index < 0 ? 0 : c->path_index;
-    int end = s + 50 < PATH_LEN ? s + 50 : PATH_LEN;
+    const int L = len_of(e, c);
+    int end = s + 50 < L ? s + 50 : L;
     float best = INFINITY;
     int bi = s;
     for (int i = s; i < end; ++i) {
@@ -388,7 +391,7 @@ static void plan_npc(const orc_env* e, int k, float* thr_out, float* st_out) {
     float steer = 0.0f;
     {
         int ti = n->path_index + 12;
-        if (ti > PATH_LEN - 1) ti = PATH_LEN - 1;
+        if (ti > len_of(e, n) - 1) ti = len_of(e, n) - 1;
         float dx = path[2 * ti] - n->x, dy = path[2 * ti + 1] - n->y;
         float err = wrap_angle(atan2f(-dy, dx) - n->h);
         float v = err * 3.0f;
@@ -407,7 +410,7 @@ static void plan_npc(const orc_env* e, int k, float* thr_out, float* st_out) {
     float minc = 1e9f;
     const float SAFE = CAR_WIDTH * 2.0f, SAFE_SQ = SAFE * SAFE;
     float mdc = hypotf(n->x - W * 0.5f, n->y - H * 0.5f);
-    int s = n->path_index, end = s + 120 < PATH_LEN ? s + 120 : PATH_LEN;
+    int s = n->path_index, end = s + 120 < len_of(e, n) ? s + 120 : len_of(e, n);
     for (int i = s; i < end; ++i) {
         float gx = path[2 * i], gy = path[2 * i + 1];
         for (int j = 0; j < e->nnpc; ++j) {
@@ -525,7 +528,8 @@ static void traffic_flow(orc_env* e, float dt, int spawn_route) {
     for (int i = 0; i < e->nnpc; ++i) {
         orc_car* c = &e->npc[i];
         const float* p = path_of(e, c);
-        int arrived = hypotf(c->x - p[2 * (PATH_LEN - 1)], c->y - p[2 * (PATH_LEN - 1) + 1]) < 20.0f;
+        const int L = len_of(e, c); /* path.back(), TrafficFlow.cpp:262-270 */
+        int arrived = hypotf(c->x - p[2 * (L - 1)], c->y - p[2 * (L - 1) + 1]) < 20.0f;
         int oos = c->x < -100.0f || c->x > (float)W + 100.0f || c->y < -100.0f || c->y > (float)H + 100.0f;
         if (!c->alive || arrived || oos) continue;
         e->npc[w++] = *c;
@@ -548,7 +552,7 @@ static void observe(const orc_env* e, float* obs) {
         row[3] = c->h / PI_F;
         const float* p = path_of(e, c);
         int ti = c->path_index + 10;
-        if (ti > PATH_LEN - 1) ti = PATH_LEN - 1;
+        if (ti > len_of(e, c) - 1) ti = len_of(e, c) - 1;
         float dx = p[2 * ti] - c->x, dy = p[2 * ti + 1] - c->y;
         row[4] = sqrtf(dx * dx + dy * dy) / (float)W;
         row[5] = wrap_angle(atan2f(-dy, dx) - c->h) / PI_F;
@@ -605,6 +609,8 @@ orc_env* orc_create(int lanes, int n, int rays, float fov, float maxd, float ste
     e->nroutes = e->P * e->P;
     e->paths = (float*)calloc((size_t)e->P * e->P * 2 * PATH_LEN, sizeof(float));
     e->intent = (int*)calloc((size_t)e->P * e->P, sizeof(int));
+    e->plen = (int*)calloc((size_t)e->P * e->P, sizeof(int));
+    for (int r = 0; r < e->P * e->P; ++r) e->plen[r] = PATH_LEN;
     for (int s = 0; s < e->P; ++s)
         for (int t = 0; t < e->P; ++t) {
             int r = s * e->P + t;
@@ -629,7 +635,7 @@ orc_env* orc_create(int lanes, int n, int rays, float fov, float maxd, float ste
 
 void orc_destroy(orc_env* e) {
     if (!e) return;
-    free(e->pts); free(e->paths); free(e->intent); free(e->rel); free(e->line_grid); free(e->troutes); free(e->lidar);
+    free(e->pts); free(e->paths); free(e->intent); free(e->plen); free(e->rel); free(e->line_grid); free(e->troutes); free(e->lidar);
     free(e);
 }
 
@@ -643,16 +649,24 @@ void orc_route_path(const orc_env* e, int r, float* out, int* intent) {
 
 /* A route of the caller's own (the reference's Car.path is a plain read-write
  * vector, cpp/Car.h:26, cpp/bindings.cpp:29; every function above reads a car's
- * path through path_of): appended to the table, returns its id. */
-int orc_add_route(orc_env* e, const float* path, int intent) {
+ * path through path_of, bounded by its size, len_of): n points (2 <= n <= 160)
+ * appended to the table, returns its id. */
+int orc_add_route(orc_env* e, const float* path, int n, int intent) {
+    if (n < 2 || n > PATH_LEN) return -1;
     float* np = (float*)realloc(e->paths, (size_t)(e->nroutes + 1) * 2 * PATH_LEN * sizeof(float));
     if (!np) return -1;
     e->paths = np;
     int* ni = (int*)realloc(e->intent, (size_t)(e->nroutes + 1) * sizeof(int));
     if (!ni) return -1;
     e->intent = ni;
-    memcpy(e->paths + (size_t)e->nroutes * 2 * PATH_LEN, path, sizeof(float) * 2 * PATH_LEN);
+    int* nl = (int*)realloc(e->plen, (size_t)(e->nroutes + 1) * sizeof(int));
+    if (!nl) return -1;
+    e->plen = nl;
+    float* row = e->paths + (size_t)e->nroutes * 2 * PATH_LEN;
+    memset(row, 0, sizeof(float) * 2 * PATH_LEN);
+    memcpy(row, path, sizeof(float) * 2 * (size_t)n);
     e->intent[e->nroutes] = intent;
+    e->plen[e->nroutes] = n;
     return e->nroutes++;
 }
 
@@ -716,7 +730,8 @@ void orc_step(orc_env* e, const float* actions, float dt, int spawn_route, float
         update_path_index(e, c);
         /* compute_progress / compute_stuck / compute_smooth, :15-46 */
         const float* p = path_of(e, c);
-        float cur = hypotf(c->x - p[2 * (PATH_LEN - 1)], c->y - p[2 * (PATH_LEN - 1) + 1]);
+        const int L = len_of(e, c); /* goal = path.back(), :16-17 */
+        float cur = hypotf(c->x - p[2 * (L - 1)], c->y - p[2 * (L - 1) + 1]);
         float rp = 0.0f;
         if (c->prev_dist > 0.0f) {
             float prog = c->prev_dist - cur;
@@ -736,8 +751,9 @@ void orc_step(orc_env* e, const float* actions, float dt, int spawn_route, float
         orc_car* c = &e->ego[i];
         if (!c->alive) { done[i] = 1; status[i] = ST_DEAD; continue; }
         const float* p = path_of(e, c);
-        float ex = p[2 * (PATH_LEN - 1)], ey = p[2 * (PATH_LEN - 1) + 1];
-        float dxr = ex - p[2 * (PATH_LEN - 2)], dyr = ey - p[2 * (PATH_LEN - 2) + 1];
+        const int L = len_of(e, c); /* path[size - 1], path[size - 2], :177-182 */
+        float ex = p[2 * (L - 1)], ey = p[2 * (L - 1) + 1];
+        float dxr = ex - p[2 * (L - 2)], dyr = ey - p[2 * (L - 2) + 1];
         int succ;
         if (fabsf(dxr) > fabsf(dyr)) succ = fabsf(c->y - ey) < 15.0f && fabsf(c->x - ex) < 40.0f;
         else succ = fabsf(c->x - ex) < 15.0f && fabsf(c->y - ey) < 40.0f;

@@ -57,7 +57,7 @@ def lib():
         L.orc_route_path.argtypes = [vp, i, vp, vp]
         L.orc_set_traffic_routes.argtypes = [vp, vp, i]
         L.orc_set_rel_angles.argtypes = [vp, vp]
-        L.orc_add_route.argtypes = [vp, vp, i]
+        L.orc_add_route.argtypes = [vp, vp, i, i]
         L.orc_reset.argtypes = [vp, vp]
         L.orc_set_state.argtypes = [vp, vp, vp, i, i]
         L.orc_get_state.argtypes = [vp, vp, vp, vp, vp]
@@ -108,10 +108,11 @@ class OracleEnv:
         return out, it.value
 
     def add_route(self, path, intent):
-        a = np.ascontiguousarray(path, np.float32).reshape(160, 2)
-        r = lib().orc_add_route(self.h, a.ctypes.data, int(intent))
+        """A written Car.path of n points, 2 <= n <= 160 (cpp/bindings.cpp:29)."""
+        a = np.ascontiguousarray(path, np.float32).reshape(-1, 2)
+        r = lib().orc_add_route(self.h, a.ctypes.data, len(a), int(intent))
         if r < 0:
-            raise MemoryError("orc_add_route")
+            raise ValueError("orc_add_route: 2 .. 160 points")
         return r
 
     def set_rel_angles(self, rel):

@@ -62,7 +62,8 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
         traffic=False, density=0.5, lanes=3, ego_routes=None, reward=None, steps=200,
         act="random", seed=0, dt=1.0 / 60.0, act_scale=1.0, zero_throttle_p=0.0,
         inject=None, notes="", warmup=0, roundtrip=False, custom_paths=None, ego_paths=None, car_lidars=None):
-    """custom_paths: [C][160][2] paths of the caller's own (Car.path writes); ego_paths: per ego
+    """custom_paths: C paths of the caller's own, [n][2] each, 2 <= n <= 160 (Car.path writes;
+    recorded padded with their last point, their lengths in custom_len); ego_paths: per ego
     the custom path written into its Car.path, or -1 (NPCs on custom path k, injected by
     `inject`, record route 1000 + k).  car_lidars: per ego None (add_car_with_route's own
     96-ray Lidar) or (rays, fov_deg, max_dist, step_size, rel_angles or None): the Lidar
@@ -163,7 +164,10 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
     if rays > 96:
         arrays["lidar"] = np.asarray(LD, np.float32)
     if cps:
-        arrays["custom_paths"] = np.stack(cps).astype(np.float32)
+        arrays["custom_paths"] = np.stack([np.concatenate([c, np.repeat(c[-1:], 160 - len(c), 0)])
+                                           for c in cps]).astype(np.float32)
+        if any(len(c) != 160 for c in cps):
+            arrays["custom_len"] = np.array([len(c) for c in cps], np.int32)
     if car_lidars:
         m = max([len(cl[4]) for cl in car_lidars if cl is not None and cl[4] is not None] + [1])
         rel = np.zeros((n, m), np.float32)
@@ -225,7 +229,7 @@ def inject_npcs(kcount: int, dims=None, custom=None):
             cj = custom[j] if custom is not None and j < len(custom) else -1
             route = int(rng.integers(0, 12))
             path = env.route_path(route) if cj < 0 else env.custom_paths[cj]
-            idx = int(rng.integers(0, 150))
+            idx = int(rng.integers(0, min(150, len(path) - 1)))
             x, y = float(path[idx, 0]), float(path[idx, 1])
             if min((x - px) ** 2 + (y - py) ** 2 for px, py in placed) < 70.0 ** 2:
                 continue
@@ -357,6 +361,27 @@ def gen_paths_traffic():
         custom_paths=[bent_npc], ego_paths=[-1], inject=inject_npcs(2, custom=[0, 0]))
 
 
+def gen_paths_short():
+    """Written Car.path of fewer than 160 points: every reader clamps to path.size()
+    (Car.cpp:56, IntersectionEnv.cpp:16-17,177-182,446, TrafficFlow.cpp:55,89,262-263)."""
+    env = R.RefEnv(num_lanes=3, traffic=True, density=0.0, routes=ROUTES3)
+    r = [env.route_path(k) for k in range(12)]
+    env.close()
+    # ego k starts on ROUTES3[k]: a cut at 100 points (the last segment inside the turn), one at 40, and
+    # a 2-point path from its start straight to point 60; ego 1 keeps its own route
+    short = [r[0][:100], r[2][:40], np.stack([r[3][0], r[3][60]])]
+    run("path_short_egos", n_agents=4, rays=64, use_team=True, steps=300, act="policy", seed=430,
+        custom_paths=short, ego_paths=[0, -1, 1, 2])
+    # traffic: the ego on a 120-point cut of its route; NPCs on 90- and 130-point cuts of traffic routes
+    # (they arrive at path.back() inside the box and leave; the ghost scan runs into the path's end)
+    env = R.RefEnv(num_lanes=3, traffic=True, density=0.0, routes=ROUTES3)
+    p5, n9, n4 = env.route_path(5), env.route_path(9), env.route_path(4)
+    env.close()
+    run("path_short_npc", n_agents=1, rays=64, traffic=True, density=0.0, steps=300, act="policy", seed=431,
+        ego_routes=[ROUTES3[5]], custom_paths=[p5[:120], n9[:90], n4[:130]], ego_paths=[0],
+        inject=inject_npcs(4, custom=[1, 2, 1, 2]))
+
+
 def rel_angles(rays: int, fov: float) -> List[float]:
     """Lidar's beam offsets (cpp/Lidar.cpp:4-14, IntersectionEnv.cpp:118-126) in float32."""
     f32 = np.float32
@@ -427,6 +452,7 @@ def _traffic():
 
 
 GROUPS = [("core", _core, True), ("dims", gen_dims, True), ("paths", gen_paths, True), ("lidars", gen_lidars, True),
+          ("paths_short", gen_paths_short, True),
           ("traffic", _traffic, False), ("dims_traffic", gen_dims_traffic, False),
           ("paths_traffic", gen_paths_traffic, False)]
 

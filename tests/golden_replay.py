@@ -72,12 +72,20 @@ class Report:
 DEFAULT_DIMS = (54.0, 24.0)  # Car::length / Car::width defaults (cpp/Car.h:19-20)
 
 
+def custom_paths(d):
+    """Scenario d's paths of the caller's own, each its own length: the file holds them padded
+    to [C][160][2] with their point counts in custom_len (absent: all 160)."""
+    if "custom_paths" not in d:
+        return []
+    cps = d["custom_paths"]
+    lens = d["custom_len"] if "custom_len" in d else [len(cp) for cp in cps]
+    return [cp[: int(n)] for cp, n in zip(cps, lens)]
+
+
 def custom_route_ids(h, d):
     """Register scenario d's paths of the caller's own (Car.path writes) on handle / oracle h
     (add_route); their ids, in the scenario's order."""
-    if "custom_paths" not in d:
-        return []
-    return [h.add_route(cp, 0) for cp in d["custom_paths"]]
+    return [h.add_route(cp, 0) for cp in custom_paths(d)]
 
 
 def ego_route_ids(h, d, L, cids):

@@ -1,6 +1,8 @@
 """Error behaviour of the C ABI (negative MEV_E* codes + mev_last_error, never an
 exception across the boundary), mirrored by the Python binding as MevError /
 IndexRangeError (IndexError, like the reference's std::out_of_range)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -78,8 +80,12 @@ def test_add_route_validates_and_extends_the_id_range(mev):
         h.add_route(bad, 0)
     with pytest.raises(mev.MevError):
         h.add_route(path, 3)
-    with pytest.raises(ValueError):
-        h.add_route(path[:100], 0)
+    for n in (0, 1, 161):  # 2 .. 160 points (the Python layer refuses, and the C ABI)
+        with pytest.raises(ValueError):
+            h.add_route(np.resize(path, (n, 2)), 0)
+        raw = np.resize(path, (max(n, 1), 2))
+        assert h._lib.mev_add_route_n(h._h, raw.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n, 0,
+                                      ctypes.byref(ctypes.c_int32())) == -1  # MEV_E_INVALID
     with pytest.raises(IndexError):
         h.route_info(P * P)
     r = h.add_route(path, 1)
@@ -96,4 +102,11 @@ def test_add_route_validates_and_extends_the_id_range(mev):
     assert (st["route"] == r).all() and st["x"][0, 0] == path[0, 0]
     with pytest.raises(IndexError):
         h.route_info(r + 1)
+    assert h.route_len(r) == 160 and h.route_len(0) == 160
+    # a 37-point path: read back padded with its last point, its length kept
+    r2 = h.add_route(path[:37], 2)
+    got, intent, _ = h.route_info(r2)
+    assert r2 == r + 1 and intent == 2 and h.route_len(r2) == 37
+    assert (got[:37].view(np.uint32) == path[:37].view(np.uint32)).all()
+    assert (got[37:].view(np.uint32) == path[36].view(np.uint32)).all()
     h.close()

@@ -287,15 +287,17 @@ def test_cpp_backend_cars_setter_and_written_path():
     other = cpp_backend.IntersectionEnv(3)
     other.set_state(snap)
     assert G.bits_equal(np.asarray(other.cars[1].path, np.float32), new_path)
-    with pytest.raises(ValueError):
-        c = other.cars
-        c[0].path = c[0].path[:100]
-        other.cars = c
+    c0 = other.cars[0].path
+    for bad in (c0[:1], c0 + c0[-1:]):  # 1 and 161 points (2 .. 160 are taken)
+        with pytest.raises(ValueError):
+            c = other.cars
+            c[0].path = bad
+            other.cars = c
     for env in envs + [other]:
         env.close()
 
 
-@pytest.mark.parametrize("name", ["dims_cfg3_policy", "dims_respawn_off", "path_bent_egos"])
+@pytest.mark.parametrize("name", ["dims_cfg3_policy", "dims_respawn_off", "path_bent_egos", "path_short_egos"])
 def test_cpp_backend_written_cars_replay_reference(name):
     """MARLEnv-style writes through the read-write cars vector (cpp/bindings.cpp:24-25,29,66):
     Car.length / Car.width and Car.path set on the cars add_car_with_route made, then the
@@ -315,7 +317,7 @@ def test_cpp_backend_written_cars_replay_reference(name):
     for k, c in enumerate(cars):
         c.length, c.width = float(f[k, 13]), float(f[k, 14])
         if eps[k] >= 0:
-            c.path = [tuple(map(float, q)) for q in g["custom_paths"][eps[k]]]
+            c.path = [tuple(map(float, q)) for q in G.custom_paths(g)[eps[k]]]
     env.cars = cars
     back = env.cars
     assert [(c.length, c.width) for c in back] == [(float(x), float(y)) for x, y in f[:, 13:15]]

@@ -36,6 +36,10 @@ CONFIGS = [
     # for egos and NPCs (NPCs spawn on them too: their first point)
     dict(name="custom_routes_n6", n=6, rays=64, custom=True),
     dict(name="custom_routes_traffic", n=3, rays=48, traffic=True, density=1.0, spawn_p=0.3, npcs=8, custom=True),
+    # written paths of fewer than 160 points (mev_add_route_n: rows padded with the last point, the SUCCESS
+    # axis from the path's own last segment); egos may sit at path_index past their path's end
+    dict(name="short_routes_n6", n=6, rays=64, use_team=True, custom="short"),
+    dict(name="short_routes_traffic", n=1, rays=64, traffic=True, density=1.0, spawn_p=0.3, npcs=8, custom="short"),
     # per-car sizes (Car::length / Car::width, cpp/Car.h:19-20; mev_set_car_dims): egos and injected NPCs of
     # random sizes, spawned NPCs of the default one; the runtime-layout kernels run these handles
     dict(name="dims_n8_r64_team", n=8, rays=64, use_team=True, dims=True),
@@ -54,9 +58,10 @@ def random_dims(rng, h):
     return ego, npc
 
 
-def custom_routes(h):
+def custom_routes(h, short=False):
     """Four 160-point routes that no lane pair generates: three lane routes bent sideways by up to 9 px
-    (a sine bump along the route's normal) and one straight diagonal across the whole intersection."""
+    (a sine bump along the route's normal) and one straight diagonal across the whole intersection.
+    short: cut to 100, 40, 2 (the first point and point 60) and 75 points."""
     out = []
     for s, t, amp in ((1, 4, 9.0), (3, 12, -6.0), (7, 10, 5.0)):
         path, intent, _ = h.route_info(h.route_id(s - 1, 12 + t - 1))
@@ -66,6 +71,9 @@ def custom_routes(h):
         out.append(((path + nrm * bump[:, None]).astype(np.float32), int(intent)))
     diag = np.stack([np.linspace(120.0, 640.0, 160), np.linspace(610.0, 140.0, 160)], 1).astype(np.float32)
     out.append((diag, 1))
+    if short:
+        out = [(out[0][0][:100], out[0][1]), (out[1][0][:40], out[1][1]),
+               (out[2][0][[0, 60]], out[2][1]), (out[3][0][:75], out[3][1])]
     return out
 
 
@@ -85,7 +93,7 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=()):
         for i in range(n):
             path, intent, spawn = h.route_info(int(ego_routes[e, i]))
             if rng.uniform() < 0.7:  # near its route
-                j = int(rng.integers(0, 150))
+                j = int(rng.integers(0, min(150, h.route_len(int(ego_routes[e, i])) - 1)))
                 x, y = path[j] + rng.normal(0, 4, 2)
                 hd = np.arctan2(-(path[j + 1, 1] - path[j, 1]), path[j + 1, 0] - path[j, 0]) + rng.normal(0, 0.2)
                 pidx = max(0, j - int(rng.integers(0, 5)))
@@ -117,7 +125,7 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=()):
                 break
             ri = int(rng.integers(0, len(troutes)))
             path, intent, spawn = h.route_info(troutes[ri])
-            j = int(rng.integers(0, 150))
+            j = int(rng.integers(0, min(150, h.route_len(troutes[ri]) - 1)))
             x, y = path[j]
             if any((x - a) ** 2 + (y - b) ** 2 < gap ** 2 for a, b in placed):
                 continue
@@ -232,13 +240,14 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0, max_npcs=64, E=2
             assert h.step_pack() * n * R_ > 512, (h.step_pack(), n, R_)
             pytest.skip("beams of the workgroup's slots exceed one LiDAR pool")
     table = ROUTES2 if lanes == 2 else ROUTES3
-    customs = custom_routes(h) if cfg.get("custom") else []
+    customs = custom_routes(h, cfg.get("custom") == "short") if cfg.get("custom") else []
     extra = [h.add_route(path, intent) for path, intent in customs]
     P = 8 * lanes
     assert extra == list(range(P * P, P * P + len(customs)))
     for r, (path, intent) in zip(extra, customs):
         got = h.route_info(r)
-        assert G.bits_equal(got[0], path) and got[1] == intent and tuple(got[2][:2]) == tuple(path[0])
+        assert h.route_len(r) == len(path)
+        assert G.bits_equal(got[0][: len(path)], path) and got[1] == intent and tuple(got[2][:2]) == tuple(path[0])
     st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0), extra)
     h.set_traffic_routes(troutes)
     dims = None
