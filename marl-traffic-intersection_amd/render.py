@@ -318,7 +318,8 @@ def handle_scene(handle, env: int = 0, show_lidar: bool = True, show_route: bool
         lidar = [(lidar_distances(obs[i], slots, maxd, step), rel, maxd) for i in range(N)]
     route0 = None
     if show_route and N:
-        route0 = (handle.route_info(int(st["route"][env, 0]))[0], int(st["path_index"][env, 0]))
+        r0 = int(st["route"][env, 0])
+        route0 = (handle.route_info(r0)[0][: handle.route_len(r0)], int(st["path_index"][env, 0]))
     return scene(L, cars, npcs, lidar, route0)
 
 
