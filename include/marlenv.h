@@ -186,9 +186,10 @@ int mev_car_dims_active(const mev_handle* h, int32_t* active);
  * read-write through cpp/bindings.cpp:92), by default the cfg's fov formula
  * (Lidar.cpp:4-14).  Lidar::update casts beam i along heading + rel_angles[i] for i < rays
  * (Lidar.cpp:24-25), so a reference Lidar whose rays was lowered casts the first rays
- * angles of its list: a handle of that many rays with those angles reproduces it.  The
- * offsets must be evenly spaced (to 1e-5 rad; the car-pair culling models the beams
- * linearly) and |angle| <= 1000. */
+ * angles of its list: a handle of that many rays with those angles reproduces it.  Any
+ * finite list with |angle| <= 1000 is taken; one the car-pair culling cannot model
+ * linearly (uneven beyond 1e-5 rad, descending, constant, wider than a revolution) is
+ * simulated without that culling (exact, slower). */
 int mev_set_beam_angles(mev_handle* h, const float* rel);
 int mev_get_beam_angles(mev_handle* h, float* rel);
 /* Ego routes for every (env, agent): route ids [E][N] (reference env.py:104-106,148-151). */

@@ -15,9 +15,9 @@ Deviations from MARLEnv (all outside the hot path):
    as in the reference, each car's rays / max_dist / step_size / rel_angles; cars of
    different configurations are stepped by one device handle per configuration, all
    fed the same calls (identical states and spawn streams), each car's observation row
-   taken from the handle of its own configuration.  rel_angles must be evenly spaced
-   (every list Lidar() or add_car_with_route makes, and any prefix of one, is), with at
-   least `rays` entries and rays >= 1 (the reference reads past the end otherwise);
+   taken from the handle of its own configuration.  rel_angles may be any finite list
+   (|angle| <= 1000 rad) with at least `rays` entries, and rays >= 1 (the reference
+   reads past the end otherwise);
    `lidars` must hold one Lidar per car, or one configuration for all of them;
  * Car.path may be any path of 2 .. 160 points (every path MARLEnv itself
    generates has 160, RouteGen.cpp:111-205); a path that is not a lane-layout route
@@ -350,7 +350,7 @@ class IntersectionEnv:
             h.set_beam_angles(np.asarray(key[4][: key[0]], np.float32))  # Lidar::rel_angles[0 .. rays)
         except _capi.MevError as e:
             h.close()
-            raise ValueError(f"Lidar.rel_angles: {e} (this backend needs evenly spaced offsets)") from None
+            raise ValueError(f"Lidar.rel_angles: {e}") from None
         return h
 
     @staticmethod

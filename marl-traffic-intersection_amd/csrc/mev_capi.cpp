@@ -119,6 +119,9 @@ struct mev_handle {
     // NPC-aware deal of the fused traffic kernel: valid while every step since the
     // last state change went through it (the rings then hold one entry per env)
     bool deal_valid = false;
+    // the rings were built by a step with MEV_AUTO_RESET: an env that ended there is in class
+    // 0 (no NPC slot loaded), which only the next step's auto-reset makes true
+    bool deal_ar = false;
     bool deal_on = true;  // mev_set_env_deal (default: on unless MEV_NO_DEAL=1)
     int deal_ring = 0;
 
@@ -229,6 +232,20 @@ extern "C" {
 static int serve_stop(mev_handle* h);  // with mev_step: the resident step server leaves the stream
 namespace {
 void serve_unlist(mev_handle* h);  // (with mev_step) the handle leaves the resident-server list
+
+// SimParams::beam_cull: the LiDAR's per-box beam culling models the offsets as
+// rel[b] = rel[0] + b*d (to 1e-5 rad, the slack its 2e-4 rad margin covers) with d > 0 and
+// the fan within one revolution, (R-1)*d <= 2*pi.  Any other list (a written
+// Lidar.rel_angles, cpp/bindings.cpp:91: descending, constant, uneven, several turns) is
+// simulated without the culling.
+int beam_cull_ok(const float* rel, int R) {
+    if (R <= 1) return 1;
+    const double d = (double(rel[R - 1]) - double(rel[0])) / double(R - 1);
+    if (!(d > 0.0) || double(R - 1) * d > 6.283185307179586 + 1.0e-4) return 0;
+    for (int b = 1; b < R - 1; ++b)
+        if (fabs(double(rel[b]) - (double(rel[0]) + b * d)) > 1.0e-5) return 0;
+    return 1;
+}
 }  // namespace
 
 const char* mev_last_error(void) { return g_err.c_str(); }
@@ -353,6 +370,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
             rel[size_t(ii)] = deg * PI_F2 / 180.0f;
         }
     }
+    h->sp.beam_cull = beam_cull_ok(rel.data(), c.lidar_rays);
     h->h_traffic = mev::default_traffic_routes(c.num_lanes);
     h->extend_route_hash();
 
@@ -827,12 +845,7 @@ int mev_set_beam_angles(mev_handle* h, const float* rel) {
     const int R = h->cfg.lidar_rays;
     for (int b = 0; b < R; ++b)
         if (!(fabsf(rel[b]) <= 1.0e3f)) return fail(MEV_E_INVALID, "beam angles must be finite, |angle| <= 1000 rad");
-    if (R > 2) {
-        const double d = (double(rel[R - 1]) - double(rel[0])) / double(R - 1);
-        for (int b = 1; b < R - 1; ++b)
-            if (fabs(double(rel[b]) - (double(rel[0]) + b * d)) > 1.0e-5)
-                return fail(MEV_E_INVALID, "beam angles must be evenly spaced (to 1e-5 rad)");
-    }
+    h->sp.beam_cull = beam_cull_ok(rel, R);  // (any other list: no culling, SimParams::beam_cull)
     HIP_TRY(hipSetDevice(h->cfg.device));
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -1307,6 +1320,10 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
     }
     // the NPC-aware deal (fused traffic k_step only; mev_set_env_deal)
     const bool deal = !serve && h->sp.traffic && h->sp.deal_cnt && h->deal_on && mev::step_kernel_for(h->sp) == 2;
+    // classes are NPC-slot counts the next step loads (mev_kernels.hip cars_pre): rings whose
+    // ended envs were put in class 0 by an auto-resetting step are not a bound for a step
+    // without the reset (the env keeps its NPCs), so such a step deals afresh
+    if (h->deal_valid && h->deal_ar && !in.auto_reset) h->deal_valid = false;
     if (deal) {
         if (!h->deal_valid) {  // fresh rings: this step deals by the identity order and builds the next
             HIP_TRY(hipMemsetAsync(h->sp.deal_cnt, 0, size_t(3) * mev::kDealRingInts * sizeof(int32_t), h->stream));
@@ -1321,6 +1338,7 @@ int mev_step(mev_handle* h, const mev_step_args* a) {
         HIP_TRY(mev::launch_step(h->sp, h->d_sp, in, o, h->stream, ev));
     }
     h->deal_valid = deal;
+    h->deal_ar = in.auto_reset != 0;
     if (deal) h->deal_ring = h->deal_ring == 2 ? 0 : h->deal_ring + 1;
     h->last = o;
     if (gather && h->world == 1) {
@@ -1750,6 +1768,9 @@ int mev_restore(mev_handle* h, const void* src, const uint8_t* env_mask, uint32_
         const std::vector<SnapField> f0 = snap_fields(h);
         h->last = save_last;
         const size_t total0 = snap_offsets(f0, E, nullptr);
+        if (hd.magic == kSnapMagic && hd.version == 1)  // (no car sizes, no route count / hash to check ids by)
+            return fail(MEV_E_INVALID, "snapshot format 1 is no longer supported (format 2 adds car sizes and the "
+                                       "route table's hash): take the snapshot again with this library");
         if (hd.magic != kSnapMagic || hd.version != kSnapVersion || hd.E != h->cfg.num_envs || hd.N != h->cfg.num_agents ||
             hd.K != h->cfg.max_npcs || hd.D != h->D || hd.nfields != int32_t(f0.size()) || hd.total_bytes != total0)
             return fail(MEV_E_INVALID, "snapshot does not match this handle");
@@ -1888,39 +1909,61 @@ int mev_comm_init(mev_handle* h, const uint8_t* id, int32_t world, int32_t rank,
     HIP_TRY(hipStreamSynchronize(h->stream));
     int rc = mev_packed_layout2(slots, h->cfg.num_agents, h->D, h->lidar_slots, h->gather_fmt, h->pk_off, &h->pk_bytes);
     if (rc) return rc;
+    // the check buffer before the communicator: once ncclCommInitRank returned, every rank
+    // must reach the exchange below (a rank that left early would hang its peers in it)
+    constexpr int kChk = 5;  // nroutes, route hash, gather format, packed bytes, ok
+    uint64_t* dchk = nullptr;
+    if (world > 1) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dchk), size_t(world + 1) * kChk * sizeof(uint64_t)));
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     ncclComm_t comm = nullptr;
     const ncclResult_t nr = ncclCommInitRank(&comm, world, u, rank);
-    if (nr != ncclSuccess) return fail(MEV_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+    if (nr != ncclSuccess) {
+        if (dchk) (void)hipFree(dchk);
+        return fail(MEV_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+    }
     h->comm = comm;
     h->world = world; h->rank = rank; h->root = root; h->slots = slots; h->gathers = 0;
     hipError_t e = hipStreamCreateWithFlags(&h->comm_stream, hipStreamNonBlocking);
-    if (e == hipSuccess && h->gather_fmt == MEV_GATHER_STATE && world > 1) {
-        // the root rebuilds every rank's observation heads from route ids with ITS route
-        // table: every rank must hold the same routes (mev_add_route, in the same order)
-        uint64_t* d = nullptr;
-        e = hipMalloc(reinterpret_cast<void**>(&d), size_t(world + 1) * 2 * sizeof(uint64_t));
-        const uint64_t mine[2] = {uint64_t(h->nroutes), h->route_hash[size_t(h->nroutes)]};
-        std::vector<uint64_t> all(size_t(world) * 2);
-        if (e == hipSuccess) e = hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice);
-        ncclResult_t ar = ncclSuccess;
-        if (e == hipSuccess) ar = ncclAllGather(d, d + 2, 2, ncclUint64, comm, h->comm_stream);
-        if (e == hipSuccess && ar == ncclSuccess) e = hipStreamSynchronize(h->comm_stream);
-        if (e == hipSuccess && ar == ncclSuccess)
-            e = hipMemcpy(all.data(), d + 2, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
-        if (d) (void)hipFree(d);
+    if (world > 1) {
+        // Every rank, whatever its format or local errors: the packed layout (format and
+        // bytes per rank) must agree, and with the state format the route tables too (the
+        // root rebuilds every rank's observation heads from route ids with ITS table:
+        // mev_add_route in the same order everywhere).  Local failures travel as ok = 0, so
+        // every rank returns the same verdict.
+        const uint64_t mine[kChk] = {uint64_t(h->nroutes), h->route_hash[size_t(h->nroutes)], uint64_t(h->gather_fmt),
+                                     uint64_t(h->pk_bytes), e == hipSuccess ? 1u : 0u};
+        std::vector<uint64_t> all(size_t(world) * kChk, 0);
+        hipError_t ce = hipMemcpy(dchk, mine, sizeof(mine), hipMemcpyHostToDevice);
+        const ncclResult_t ar = ncclAllGather(dchk, dchk + kChk, kChk, ncclUint64, comm, h->stream);
+        if (ar == ncclSuccess) {
+            const hipError_t se = hipStreamSynchronize(h->stream);
+            if (ce == hipSuccess) ce = se;
+            if (ce == hipSuccess) ce = hipMemcpy(all.data(), dchk + kChk, all.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+        }
+        (void)hipFree(dchk);
         if (ar != ncclSuccess) {
             h->free_comm();
-            return fail(MEV_E_HIP, std::string("RCCL route table check: ") + ncclGetErrorString(ar));
+            return fail(MEV_E_HIP, std::string("RCCL layout check: ") + ncclGetErrorString(ar));
         }
-        if (e == hipSuccess)
-            for (int r = 0; r < world; ++r)
-                if (all[size_t(2 * r)] != mine[0] || all[size_t(2 * r + 1)] != mine[1]) {
-                    h->free_comm();
-                    return fail(MEV_E_INVALID, "the ranks' route tables differ (mev_add_route): the state gather "
-                                               "format decodes every rank's route ids with the root's table");
-                }
+        if (ce != hipSuccess) {
+            h->free_comm();
+            return fail(MEV_E_HIP, std::string("layout check: ") + hipGetErrorString(ce));
+        }
+        for (int r = 0; r < world; ++r) {
+            const uint64_t* o = &all[size_t(r) * kChk];
+            const char* why = nullptr;
+            if (o[4] != 1) why = "a rank failed to create its communication stream";
+            else if (o[2] != mine[2] || o[3] != mine[3])
+                why = "the ranks' gather layouts differ (mev_set_gather_format, num_agents, obs_dim, slots)";
+            else if (h->gather_fmt == MEV_GATHER_STATE && (o[0] != mine[0] || o[1] != mine[1]))
+                why = "the ranks' route tables differ (mev_add_route): the state gather format decodes every "
+                      "rank's route ids with the root's table";
+            if (why) {
+                h->free_comm();
+                return fail(MEV_E_INVALID, why);
+            }
+        }
     }
     const size_t per = (rank == root) ? size_t(world) * h->pk_bytes : h->pk_bytes;
     for (int b = 0; b < 2 && e == hipSuccess; ++b) {

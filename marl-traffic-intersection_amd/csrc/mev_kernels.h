@@ -142,6 +142,12 @@ struct SimParams {
     float* ego_dim;
     float* npc_dim;
     int32_t dims;
+    // LiDAR phase 3b culls each obstacle box to the beams its angular span covers with a
+    // linear model of the offsets: rel[b] = rel[0] + b*d, d > 0, (R-1)*d <= 2*pi (every list
+    // Lidar() / add_car_with_route makes with fov > 0).  0 for any other list (descending,
+    // constant, uneven or wider than a revolution; a written Lidar.rel_angles): every beam
+    // is then resolved against every candidate box -- the same probes, no culling.
+    int32_t beam_cull;
 };
 
 // The fused traffic k_step deals envs to workgroups by their NPC count: every env

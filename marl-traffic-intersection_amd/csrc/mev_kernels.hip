@@ -17,6 +17,7 @@
 
 #include "mev_kernels.h"
 #include "mev_world.h"
+#include "mev_nsort.h"
 
 namespace mev {
 
@@ -1188,10 +1189,18 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
 // ---------------------------------------------------- observation rows ---
 // get_observations (cpp/IntersectionEnv.cpp:418-520) minus the LiDAR block:
 // ego features, path look-ahead, 5 nearest alive neighbours (egos first, then
-// NPCs; stable by distance == libstdc++ insertion sort for <= 16 candidates).
+// NPCs) in std::sort's order (:490).  The per-lane pass keeps the stable top 5,
+// which is std::sort's whenever there are at most 16 candidates (libstdc++ then
+// runs only its insertion sort) or no two of the nearest share a distance.
+// Otherwise it writes no neighbour slot and returns true, with *dlim = the
+// fifth-smallest distance, and the caller's wave runs obs_exact_neighbours for
+// the agent (mev_nsort.h).  A tie among the nearest always shows as a candidate
+// equal to a kept one when it arrives: of two equal candidates a (first) and b
+// with d <= the final fifth distance, either a is still kept when b arrives, or a
+// was pushed out by a strictly nearer one, and then the kept fifth equals d.
 template <bool TRAFFIC, class EL, class NL>
-__device__ __forceinline__ void write_obs_head_tg(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt, float tx,
-                                  float ty, float* row, bool pad = true) {
+__device__ __forceinline__ bool write_obs_head_tg(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt, float tx,
+                                  float ty, float* row, bool pad = true, float* dlim = nullptr) {
     const float x = el.x[i], y = el.y[i], v = el.v[i], h = el.h[i];
     row[0] = x / float(WIDTH);
     row[1] = y / float(HEIGHT);
@@ -1204,7 +1213,8 @@ __device__ __forceinline__ void write_obs_head_tg(const SimParams& p, int i, con
     // top-5 insertion (stable)
     float bd[NEIGHBOR_COUNT];
     int bi[NEIGHBOR_COUNT];
-    int nb = 0;
+    int nb = 0, cnt = 0;
+    bool tie = false;
     const int ncand = p.N + (TRAFFIC ? ncnt : 0);
     for (int j = 0; j < ncand; ++j) {
         float ox, oy;
@@ -1216,18 +1226,26 @@ __device__ __forceinline__ void write_obs_head_tg(const SimParams& p, int i, con
             if (!nl->alive[k]) continue;
             ox = nl->x[k]; oy = nl->y[k];
         }
+        ++cnt;
         const float dx = ox - x;
         const float dy = oy - y;
         const float d = __builtin_sqrtf(dx * dx + dy * dy);
         // stable insertion into the first 5 slots
         int pos = nb;
         while (pos > 0 && bd[pos - 1] > d) --pos;
+        tie = tie || (pos > 0 && bd[pos - 1] == d);
         if (pos >= NEIGHBOR_COUNT) continue;
         const int last = nb < NEIGHBOR_COUNT ? nb : NEIGHBOR_COUNT - 1;
         for (int q = last; q > pos; --q) { bd[q] = bd[q - 1]; bi[q] = bi[q - 1]; }
         bd[pos] = d;
         bi[pos] = j < p.N ? j : MAXN + (j - p.N);
         if (nb < NEIGHBOR_COUNT) ++nb;
+    }
+    if (cnt > 16 && tie) {  // std::sort's order: obs_exact_neighbours
+        *dlim = bd[NEIGHBOR_COUNT - 1];
+        if (pad)
+            for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
+        return true;
     }
     for (int q = 0; q < NEIGHBOR_COUNT; ++q) {
         float* o = row + 6 + 5 * q;
@@ -1248,14 +1266,163 @@ __device__ __forceinline__ void write_obs_head_tg(const SimParams& p, int i, con
     }
     if (pad)
         for (int c = OBS_HEAD + p.lidar_slots; c < p.D; ++c) row[c] = 0.0f;
+    return false;
 }
 
 template <bool TRAFFIC, class EL, class NL>
-__device__ __forceinline__ void write_obs_head(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt,
-                               const float* path, int pidx, float* row) {
+__device__ __forceinline__ bool write_obs_head(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt,
+                               const float* path, int pidx, float* row, float* dlim) {
     int tidx = pidx + 10;
     if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
-    write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, path[2 * tidx], path[2 * tidx + 1], row);
+    return write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, path[2 * tidx], path[2 * tidx + 1], row, true, dlim);
+}
+
+// The 64 lanes as the array of std::sort (mev_nsort.h): position q at lane q & 63 of
+// d0/i0 (q < 64) or d1/i1; every index is wave-uniform, so a get is a readlane into
+// SGPRs and a set one compare-and-select per register.
+struct WaveNRefs {
+    float d0, d1;
+    int i0, i1;
+    int lane;
+    // (both registers read and written, selected by value: a field chosen by q would be
+    // a pointer select, which keeps the struct out of registers)
+    __device__ __forceinline__ NRef get(int q) const {
+        const int l = q & (WAVE - 1);
+        const float e0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d0), l));
+        const float e1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d1), l));
+        const int j0 = __builtin_amdgcn_readlane(i0, l), j1 = __builtin_amdgcn_readlane(i1, l);
+        return q < WAVE ? NRef{e0, j0} : NRef{e1, j1};
+    }
+    __device__ __forceinline__ void set(int q, NRef r) {
+        const bool here = lane == (q & (WAVE - 1));
+        const bool h0 = here && q < WAVE, h1 = here && q >= WAVE;
+        d0 = h0 ? r.d : d0;
+        i0 = h0 ? r.id : i0;
+        d1 = h1 ? r.d : d1;
+        i1 = h1 ? r.id : i1;
+    }
+};
+struct WaveStack {
+    int v = 0, n = 0, lane = 0;
+    __device__ __forceinline__ void push(int w) { v = lane == n ? w : v; ++n; }
+    __device__ __forceinline__ int pop() { --n; return __builtin_amdgcn_readlane(v, n); }
+    __device__ __forceinline__ int size() const { return n; }
+};
+
+// position of the k-th (0-based) set bit of m (k < popcount(m); otherwise some bit in 0..63)
+__device__ __forceinline__ int select_bit(unsigned long long m, int k) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const int c = __builtin_popcountll((m >> pos) & ((1ull << w) - 1ull));
+        if (c <= k) { k -= c; pos += w; }
+    }
+    return pos;
+}
+
+// the lexicographic minimum of (d, position) over the wave's two slots per lane; d >= +0
+// (a distance), so its bit pattern orders like its value.  Returns the position.
+__device__ __forceinline__ int wave_argmin_dq(float d0, float d1, bool v0, bool v1, int lane) {
+    const unsigned long long k0 = v0 ? ((unsigned long long)__float_as_uint(d0) << 32) | (unsigned)lane : ~0ull;
+    const unsigned long long k1 = v1 ? ((unsigned long long)__float_as_uint(d1) << 32) | (unsigned)(lane + WAVE) : ~0ull;
+    unsigned long long k = k0 < k1 ? k0 : k1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = ((unsigned long long)(unsigned)__shfl_xor((int)(k >> 32), o) << 32) |
+                                     (unsigned)__shfl_xor((int)(unsigned)k, o);
+        k = w < k ? w : k;
+    }
+    return (int)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)k);
+}
+
+// Ego i's neighbour slots in std::sort's order (IntersectionEnv.cpp:466-507), by the whole
+// wave (every lane, wave-uniform i): the candidates in push order -- the other alive
+// egos, then the alive NPCs -- compacted into the lanes, libstdc++'s partitions over
+// them (ns_introsort, pruned at dlim), then the stable first five of that permutation
+// (its final insertion sort).  Rare: only when write_obs_head_tg found more than 16
+// candidates and an exact tie among the nearest.
+template <bool TRAFFIC, class EL, class NL>
+__device__ __forceinline__ void obs_exact_neighbours(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt,
+                                                  float dlim, float* row) {
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const float x = el.x[i], y = el.y[i], v = el.v[i], h = el.h[i];
+    const bool ve = lane < p.N && lane != i && el.alive[lane] != 0;
+    float de = 0.0f;
+    if (ve) {
+        const float dx = el.x[lane] - x, dy = el.y[lane] - y;
+        de = __builtin_sqrtf(dx * dx + dy * dy);
+    }
+    bool vn = false;
+    float dn = 0.0f;
+    if constexpr (TRAFFIC) {
+        vn = lane < ncnt && nl->alive[lane] != 0;
+        if (vn) {
+            const float dx = nl->x[lane] - x, dy = nl->y[lane] - y;
+            dn = __builtin_sqrtf(dx * dx + dy * dy);
+        }
+    }
+    const unsigned long long me = ballot(ve), mn = ballot(vn);
+    const int ne = __builtin_popcountll(me), n = ne + __builtin_popcountll(mn);
+    // position q of the push order: ego select_bit(me, q) or NPC select_bit(mn, q - ne)
+    WaveNRefs a;
+    a.lane = lane;
+    {
+        const int q = lane;
+        const int s = q < ne ? select_bit(me, q) : select_bit(mn, q - ne);
+        const float fe = __int_as_float(__builtin_amdgcn_ds_bpermute(s << 2, __float_as_int(de)));
+        const float fn = __int_as_float(__builtin_amdgcn_ds_bpermute(s << 2, __float_as_int(dn)));
+        a.d0 = q < ne ? fe : fn;
+        a.i0 = q < ne ? s : MAXN + s;
+    }
+    {
+        const int q = lane + WAVE;
+        const int s = q < ne ? select_bit(me, q) : select_bit(mn, q - ne);
+        const float fe = __int_as_float(__builtin_amdgcn_ds_bpermute(s << 2, __float_as_int(de)));
+        const float fn = __int_as_float(__builtin_amdgcn_ds_bpermute(s << 2, __float_as_int(dn)));
+        a.d1 = q < ne ? fe : fn;
+        a.i1 = q < ne ? s : MAXN + s;
+    }
+    WaveStack st;
+    st.lane = lane;
+    ns_introsort(a, n, dlim, st);
+    // the stable first five of the permutation: smallest (d, position), five times
+    bool v0 = lane < n, v1 = lane + WAVE < n;
+    int ids[NEIGHBOR_COUNT];
+#pragma unroll
+    for (int q = 0; q < NEIGHBOR_COUNT; ++q) {
+        const int pos = wave_argmin_dq(a.d0, a.d1, v0, v1, lane);
+        ids[q] = a.get(pos).id;
+        v0 = v0 && pos != lane;
+        v1 = v1 && pos != lane + WAVE;
+    }
+    int id = ids[0];
+#pragma unroll
+    for (int q = 1; q < NEIGHBOR_COUNT; ++q) id = lane == q ? ids[q] : id;
+    if (lane < NEIGHBOR_COUNT) {  // n > 16: five neighbours (the arithmetic of write_obs_head_tg)
+        float ox, oy, ov, oh;
+        int oi;
+        if (id < MAXN) { ox = el.x[id]; oy = el.y[id]; ov = el.v[id]; oh = el.h[id]; oi = el.intent[id]; }
+        else { const int k = id - MAXN; ox = nl->x[k]; oy = nl->y[k]; ov = nl->v[k]; oh = nl->h[k]; oi = nl->intent[k]; }
+        float* o = row + 6 + 5 * lane;
+        o[0] = (ox - x) / float(WIDTH);
+        o[1] = (oy - y) / float(HEIGHT);
+        o[2] = (ov - v) / PHYSICS_MAX_SPEED;
+        o[3] = wrap_angle(oh - h) / PI_F;
+        o[4] = float(oi);
+    }
+}
+
+// every lane of the wave: the agents whose write_obs_head_tg returned true (bit a of m:
+// agent a, its fifth distance in lane a of dl, its row at rows + a * ld)
+template <bool TRAFFIC, class EL, class NL>
+__device__ __forceinline__ void obs_exact_pass(const SimParams& p, unsigned long long m, float dl, const EL& el,
+                                               const NL* nl, int ncnt, float* rows, size_t ld) {
+    while (m) {
+        const int a = __builtin_ctzll(m);
+        m &= m - 1ull;
+        const float dlim = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dl), a));
+        obs_exact_neighbours<TRAFFIC>(p, a, el, nl, ncnt, dlim, rows + (size_t)a * ld);
+    }
 }
 
 // ------------------------------------------------------------- the step ---
@@ -2187,6 +2354,8 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
             }
         }
     } else {
+        bool exact = false;  // (N <= 64: one pass, lane i = agent i)
+        float dl = 0.0f;
         for (int i = tid; i < N; i += WAVE) {
             const int g = e * NE + i;
             float* row = out.obs + (size_t)g * out.obs_ld;
@@ -2195,7 +2364,11 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
                 for (int c = OBS_HEAD + p.lidar_slots; c < out.obs_ld; ++c) row[c] = 0.0f;
                 continue;
             }
-            write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row, out.obs_ld == p.D);
+            exact = write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, el.tgx[i], el.tgy[i], row, out.obs_ld == p.D, &dl);
+        }
+        if constexpr (PK == 1) {
+            const unsigned long long m = ballot(exact);
+            if (m) obs_exact_pass<TRAFFIC>(p, m, dl, el, nl, ncnt, out.obs + (size_t)e * NE * out.obs_ld, out.obs_ld);
         }
     }
     STAMP(6);
@@ -2591,7 +2764,9 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     const float rel_c1 = lane + WAVE < R ? src.rel(lane + WAVE) : 0.0f;
     // one beam: direction (Lidar.cpp:24-26) and the first probes; returns the
     // beam's result (>= 0) or -(next probe to test) - 1
-    auto setup = [&](const float4& a, float rel_b, auto small, float2& d) -> int {
+    // (uni: every lane's beam starts from the same car centre -- the wave-uniform safe bound;
+    // else a chunk of the dense layout that holds two agents' beams)
+    auto setup = [&](const float4& a, float rel_b, auto small, float2& d, auto uni) -> int {
         float sn, cs;
         if constexpr (decltype(small)::value) sincosf_below120(a.z + rel_b, &sn, &cs);
         else sincosf(a.z + rel_b, &sn, &cs);
@@ -2600,7 +2775,11 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const int px = (int)a.x, py = (int)a.y;
         const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
         const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
-        const float safe = road_safe_uniform(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
+        float safe;
+        if constexpr (decltype(uni)::value)
+            safe = road_safe_uniform(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
+        else
+            safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
         // probes 1 .. j lie within j*step <= safe of the centre (car centre on screen)
         const int k1 = pmax < (unsigned)WIDTH ? 1 + safe_steps(safe, stp, inv_stp) : 0;
         float fx, fy;
@@ -2615,7 +2794,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             const bool vb = b < R;
             const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : (vb ? src.rel(b) : 0.0f));
             float2 d;
-            const int r = setup(a, rel_b, small, d);
+            const int r = setup(a, rel_b, small, d, std::true_type{});
             if (vb) {
                 dir[j * R + b] = d;
                 res[j * R + b] = r >= 0 ? r : -r - 1;
@@ -2629,9 +2808,52 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // ILP = 2: two agents per pass, two independent dependency chains (sincosf's
     // double polynomial, the safe distance, the probes) the compiler interleaves
     // (k_step, 128 VGPRs); ILP = 1 in k_lidar, whose 64-VGPR budget would spill
+    // Dense layout (R not a multiple of 64, several agents): the pool's nal*R beams as
+    // consecutive 64-lane chunks, an agent's beams running on into the next chunk, ILP
+    // chunks per pass.  Per agent, R = 96 would take two chunks, the second half empty
+    // (and an odd agent count a discarded second chain): 20 chain-chunks for 8 agents
+    // instead of 13.
+    const bool dense = PART != 2 && (R & (WAVE - 1)) != 0 &&
+                       (nal * R + WAVE - 1) / WAVE < nal * ((R + WAVE - 1) / WAVE);
+    auto phase1_dense = [&](auto small) {
+        const float invRd = 1.0f / (float)R;
+        const int nq = nal * R;
+        for (int c0 = 0; c0 < nq; c0 += ILP * WAVE) {
+            if (PART == 0 && 4 * c0 >= nq) __builtin_amdgcn_s_setprio(kPrioP1B);
+            int q[ILP];
+            float4 a[ILP];
+            float rb[ILP];
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) {
+                q[u] = c0 + u * WAVE + lane;
+                const int qc = q[u] < nq ? q[u] : nq - 1;
+                const int j = (int)(((float)qc + 0.5f) * invRd);  // exact (see load_beam)
+                a[u] = ag[j];
+                rb[u] = src.rel(qc - j * R);
+            }
+            float2 d[ILP];
+            int r[ILP];
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rb[u], small, d[u], std::false_type{});
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) {
+                const bool vq = q[u] < nq;
+                if (vq) {
+                    dir[q[u]] = d[u];
+                    res[q[u]] = r[u] >= 0 ? r[u] : -r[u] - 1;  // result, or the next probe to test
+                }
+                const bool pend = vq && r[u] < 0;
+                const unsigned long long m = ballot(pend);
+                if (pend) queue[qn + lane_rank(m)] = (unsigned short)q[u];
+                qn += __popcll(m);
+            }
+        }
+    };
     auto phase1 = [&](auto small) {
         if constexpr (PART == 2) {  // the respawned agents only
             for (unsigned long long tm = redo; tm; tm &= tm - 1ull) pass1_one(small, __builtin_ctzll(tm));
+        } else if (dense) {
+            phase1_dense(small);
         } else {
         for (int j = 0; j < nal; j += ILP) {
             if (PART == 0 && 4 * j >= nal) __builtin_amdgcn_s_setprio(kPrioP1B);
@@ -2645,7 +2867,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 float2 d[ILP];
                 int r[ILP];
 #pragma unroll
-                for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rel_b, small, d[u]);
+                for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rel_b, small, d[u], std::true_type{});
 #pragma unroll
                 for (int u = 0; u < ILP; ++u) {
                     const bool in = j + u < nal;  // wave-uniform
@@ -2836,7 +3058,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const float ex0 = box_lo(bx.x), ex1 = box_hi(bx.y);
         const float ey0 = box_lo(bx.z), ey1 = box_hi(bx.w);
         int4 rg;
-        if (R == 1 || (a.x >= ex0 && a.x <= ex1 && a.y >= ey0 && a.y <= ey1)) {  // (on its edge too)
+        if (R == 1 || !p.beam_cull || (a.x >= ex0 && a.x <= ex1 && a.y >= ey0 && a.y <= ey1)) {  // (on its edge too)
             rg = make_int4(0 | (R << 16), 0, 0, R);  // inside the widened box: every beam
         } else {
             // the box's silhouette seen from the agent (outside it): the two corners
@@ -3293,6 +3515,8 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
         }
     }
     wave_lds_sync();
+    bool exact = false;  // (N <= 64: one pass, lane i = agent i)
+    float dl = 0.0f;
     for (int i = lane; i < N; i += WAVE) {
         const int g = e * N + i;
         float* row = out.obs + (size_t)g * p.D;
@@ -3301,9 +3525,11 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
             continue;
         }
         const float* path = p.rt.path + (size_t)egoi(p, EF_ROUTE)[g] * (2 * ROUTE_PTS);
-        write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row);
+        exact = write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row, &dl);
         for (int b = 0; b < p.lidar_slots; ++b) row[OBS_HEAD + b] = p.lidar_max * p.lidar_inv;
     }
+    const unsigned long long m = ballot(exact);
+    if (m) obs_exact_pass<TRAFFIC>(p, m, dl, el, nl, ncnt, out.obs + (size_t)e * N * p.D, (size_t)p.D);
 }
 
 static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Outputs& out, int e0, int e1,
@@ -3599,6 +3825,8 @@ __global__ __launch_bounds__(WAVE) void k_decode_state(SimParams p, const uint8_
         el.alive[lane] = sb[21 * n + a];
     }
     __syncthreads();
+    bool exact = false;  // (N <= 64: one pass, lane i = agent i)
+    float dl = 0.0f;
     for (int i = lane; i < N; i += WAVE) {
         float* row = obs + ((size_t)g * N + i) * D;
         if (!el.alive[i]) {
@@ -3614,9 +3842,11 @@ __global__ __launch_bounds__(WAVE) void k_decode_state(SimParams p, const uint8_
         const int ti = pidx + 10 < PATH_LEN - 1 ? (pidx + 10 < 0 ? 0 : pidx + 10) : PATH_LEN - 1;
         const float* path = p.rt.path + (size_t)rt * (2 * ROUTE_PTS);
         const float nan = __builtin_nanf("");
-        write_obs_head_tg<false>(p, i, el, (const NpcLDST<MAXK>*)nullptr, 0, bad ? nan : path[2 * ti],
-                                 bad ? nan : path[2 * ti + 1], row, false);
+        exact = write_obs_head_tg<false>(p, i, el, (const NpcLDST<MAXK>*)nullptr, 0, bad ? nan : path[2 * ti],
+                                         bad ? nan : path[2 * ti + 1], row, false, &dl);
     }
+    const unsigned long long m = ballot(exact);
+    if (m) obs_exact_pass<false>(p, m, dl, el, (const NpcLDST<MAXK>*)nullptr, 0, obs + (size_t)g * N * D, (size_t)D);
     // LiDAR block and padding, every lane: (agent, column) pairs
     const int tail = D - OBS_HEAD;
     for (int t = lane; t < N * tail; t += WAVE) {

@@ -537,6 +537,141 @@ static void traffic_flow(orc_env* e, float dt, int spawn_route) {
     e->nnpc = w;
 }
 
+/* ------------------------------------------------ std::sort (libstdc++) */
+/* The neighbour sort of get_observations (cpp/IntersectionEnv.cpp:466-490) is
+ * std::sort with `a.dist < b.dist`: NOT stable.  Restated from this image's
+ * GCC 11 libstdc++ (bits/stl_algo.h __sort / __introsort_loop /
+ * __unguarded_partition_pivot / __move_median_to_first / __unguarded_partition /
+ * __final_insertion_sort, bits/stl_heap.h __make_heap / __adjust_heap /
+ * __push_heap / __pop_heap / __sort_heap), which the reference build links: for
+ * more than 16 neighbours with equal distances the order of equal neighbours is
+ * the one these partitions leave, not the push order. */
+typedef struct {
+    float d;
+    const orc_car* c;
+} orc_nref; /* NeighborRef, IntersectionEnv.cpp:461-464 */
+
+static void nr_swap(orc_nref* a, orc_nref* b) { orc_nref t = *a; *a = *b; *b = t; }
+
+static void nr_push_heap(orc_nref* f, long hole, long top, orc_nref v) {
+    long parent = (hole - 1) / 2;
+    while (hole > top && f[parent].d < v.d) {
+        f[hole] = f[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    f[hole] = v;
+}
+
+static void nr_adjust_heap(orc_nref* f, long hole, long len, orc_nref v) {
+    const long top = hole;
+    long sc = hole;
+    while (sc < (len - 1) / 2) {
+        sc = 2 * (sc + 1);
+        if (f[sc].d < f[sc - 1].d) sc--;
+        f[hole] = f[sc];
+        hole = sc;
+    }
+    if ((len & 1) == 0 && sc == (len - 2) / 2) {
+        sc = 2 * (sc + 1);
+        f[hole] = f[sc - 1];
+        hole = sc - 1;
+    }
+    nr_push_heap(f, hole, top, v);
+}
+
+/* __partial_sort(first, last, last): __heap_select (= __make_heap, its loop is empty) + __sort_heap */
+static void nr_heapsort(orc_nref* f, long len) {
+    if (len >= 2)
+        for (long parent = (len - 2) / 2;; --parent) {
+            nr_adjust_heap(f, parent, len, f[parent]);
+            if (parent == 0) break;
+        }
+    for (long l = len; l > 1;) {
+        --l;
+        orc_nref v = f[l];
+        f[l] = f[0];
+        nr_adjust_heap(f, 0, l, v);
+    }
+}
+
+static void nr_introsort_loop(orc_nref* first, orc_nref* last, int depth) {
+    while (last - first > 16) {
+        if (depth == 0) {
+            nr_heapsort(first, last - first);
+            return;
+        }
+        --depth;
+        /* __unguarded_partition_pivot: median of (first+1, mid, last-1) into *first */
+        orc_nref *a = first + 1, *b = first + (last - first) / 2, *c = last - 1;
+        if (a->d < b->d) {
+            if (b->d < c->d) nr_swap(first, b);
+            else if (a->d < c->d) nr_swap(first, c);
+            else nr_swap(first, a);
+        } else if (a->d < c->d) nr_swap(first, a);
+        else if (b->d < c->d) nr_swap(first, c);
+        else nr_swap(first, b);
+        /* __unguarded_partition(first + 1, last, first) */
+        orc_nref *lo = first + 1, *hi = last;
+        for (;;) {
+            while (lo->d < first->d) ++lo;
+            --hi;
+            while (first->d < hi->d) --hi;
+            if (!(lo < hi)) break;
+            nr_swap(lo, hi);
+            ++lo;
+        }
+        nr_introsort_loop(lo, last, depth);
+        last = lo;
+    }
+}
+
+static void nr_linear_insert(orc_nref* last) { /* __unguarded_linear_insert */
+    orc_nref v = *last;
+    orc_nref* next = last - 1;
+    while (v.d < next->d) {
+        *last = *next;
+        last = next;
+        --next;
+    }
+    *last = v;
+}
+
+static void nr_insertion_sort(orc_nref* first, orc_nref* last) { /* __insertion_sort */
+    if (first == last) return;
+    for (orc_nref* i = first + 1; i != last; ++i) {
+        if (i->d < first->d) {
+            orc_nref v = *i;
+            memmove(first + 1, first, (size_t)(i - first) * sizeof(orc_nref));
+            *first = v;
+        } else {
+            nr_linear_insert(i);
+        }
+    }
+}
+
+static void nr_std_sort(orc_nref* f, int n) {
+    if (n <= 0) return;
+    int lg = 0; /* std::__lg */
+    while ((2 << lg) <= n) ++lg;
+    nr_introsort_loop(f, f + n, 2 * lg);
+    if (n > 16) { /* __final_insertion_sort */
+        nr_insertion_sort(f, f + 16);
+        for (orc_nref* i = f + 16; i != f + n; ++i) nr_linear_insert(i);
+    } else {
+        nr_insertion_sort(f, f + n);
+    }
+}
+
+/* test hook: the permutation std::sort leaves on n distances (ids in push order) */
+void orc_std_sort_perm(const float* d, int n, int* perm) {
+    orc_nref* a = (orc_nref*)malloc(sizeof(orc_nref) * (size_t)(n > 0 ? n : 1));
+    for (int k = 0; k < n; ++k) { a[k].d = d[k]; a[k].c = (const orc_car*)(uintptr_t)(k + 1); }
+    nr_std_sort(a, n);
+    for (int k = 0; k < n; ++k) perm[k] = (int)(uintptr_t)a[k].c - 1;
+    free(a);
+}
+
 /* ---------------------------------------------------------- observation */
 /* get_observations, cpp/IntersectionEnv.cpp:418-520 */
 static void observe(const orc_env* e, float* obs) {
@@ -556,33 +691,26 @@ static void observe(const orc_env* e, float* obs) {
         float dx = p[2 * ti] - c->x, dy = p[2 * ti + 1] - c->y;
         row[4] = sqrtf(dx * dx + dy * dy) / (float)W;
         row[5] = wrap_angle(atan2f(-dy, dx) - c->h) / PI_F;
-        /* neighbours: egos then NPCs; std::sort on <= 16 items is a stable insertion sort */
-        float nd[2 * MAXCARS];
-        const orc_car* nc[2 * MAXCARS];
+        /* neighbours: other alive egos, then alive NPCs (:466-488), std::sort by distance (:490) */
+        orc_nref neigh[2 * MAXCARS];
         int cnt = 0;
         for (int j = 0; j < e->n; ++j) {
             if (j == i || !e->ego[j].alive) continue;
             float ddx = e->ego[j].x - c->x, ddy = e->ego[j].y - c->y;
-            nd[cnt] = sqrtf(ddx * ddx + ddy * ddy);
-            nc[cnt++] = &e->ego[j];
+            neigh[cnt].d = sqrtf(ddx * ddx + ddy * ddy);
+            neigh[cnt++].c = &e->ego[j];
         }
         if (e->traffic)
             for (int j = 0; j < e->nnpc; ++j) {
                 if (!e->npc[j].alive) continue;
                 float ddx = e->npc[j].x - c->x, ddy = e->npc[j].y - c->y;
-                nd[cnt] = sqrtf(ddx * ddx + ddy * ddy);
-                nc[cnt++] = &e->npc[j];
+                neigh[cnt].d = sqrtf(ddx * ddx + ddy * ddy);
+                neigh[cnt++].c = &e->npc[j];
             }
-        for (int a = 1; a < cnt; ++a) { /* stable insertion sort by distance */
-            float d = nd[a];
-            const orc_car* q = nc[a];
-            int b = a;
-            while (b > 0 && d < nd[b - 1]) { nd[b] = nd[b - 1]; nc[b] = nc[b - 1]; --b; }
-            nd[b] = d; nc[b] = q;
-        }
+        nr_std_sort(neigh, cnt);
         int take = cnt < NEIGHBORS ? cnt : NEIGHBORS;
         for (int k = 0; k < take; ++k) {
-            const orc_car* o = nc[k];
+            const orc_car* o = neigh[k].c;
             float* f = row + 6 + 5 * k;
             f[0] = (o->x - c->x) / (float)W;
             f[1] = (o->y - c->y) / (float)H;

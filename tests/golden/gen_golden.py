@@ -403,6 +403,81 @@ def gen_lidars():
         car_lidars=[(32, 360.0, 150.0, 3.0, rel_angles(32, 360.0)), None], inject=inject_npcs(3))
 
 
+def inject_npc_ring(kcount: int, spread: int = 300):
+    """kcount NPCs around ego 0 at integer offsets in symmetric sets -- (a, b), (-a, b), (b, a),
+    (-b, a) -- so that many of their distances to ego 0 are exactly equal: more than 16
+    neighbour candidates with ties, where std::sort's order (IntersectionEnv.cpp:490) is not
+    the push order.  At least 60 px apart, on screen; random traffic routes and speeds."""
+    def _inj(env: R.RefEnv, rng: np.random.Generator):
+        ef, _ = env.cars(0)
+        x0, y0 = float(ef[0, 0]), float(ef[0, 1])
+        placed = [(x0, y0)]
+        tries = 0
+        while len(placed) < kcount + 1 and tries < 4000:
+            tries += 1
+            a, b = int(rng.integers(40, spread)), int(rng.integers(0, spread))
+            for dx, dy in ((a, b), (-a, b), (b, a), (-b, a)):
+                if len(placed) >= kcount + 1:
+                    break
+                x, y = x0 + dx, y0 + dy
+                if not (10 <= x <= 740 and 10 <= y <= 740):
+                    continue
+                if min((x - px) ** 2 + (y - py) ** 2 for px, py in placed) < 60.0 ** 2:
+                    continue
+                route = int(rng.integers(0, 12))
+                path = env.route_path(route)
+                f = np.zeros(R.NF, np.float32)
+                f[0], f[1] = x, y
+                f[2] = rng.uniform(0, 4)
+                f[3] = rng.uniform(-math.pi, math.pi)
+                f[6], f[7], f[9] = path[0, 0], path[0, 1], math.atan2(-(path[1, 1] - path[0, 1]), path[1, 0] - path[0, 0])
+                f[13], f[14] = 54.0, 24.0
+                i = np.array([1, 0, int(rng.integers(0, 100)), route], np.int32)
+                assert env.add_npc(route, f, i) == 0
+                placed.append((x, y))
+    return _inj
+
+
+def inject_ego_ring(env: R.RefEnv, rng: np.random.Generator):
+    """Egos 1.. around ego 0 at integer offsets in symmetric sets (inject_npc_ring's layout):
+    equal distances among more than 16 candidates."""
+    f, i = env.cars(0)
+    x0, y0 = float(f[0, 0]), float(f[0, 1])
+    placed = [(x0, y0)]
+    k = 1
+    while k < len(f):
+        a, b = int(rng.integers(40, 330)), int(rng.integers(0, 330))
+        for dx, dy in ((a, b), (-a, b), (b, a), (-b, a)):
+            if k >= len(f):
+                break
+            x, y = x0 + dx, y0 + dy
+            if not (10 <= x <= 740 and 10 <= y <= 740):
+                continue
+            if min((x - px) ** 2 + (y - py) ** 2 for px, py in placed) < 60.0 ** 2:
+                continue
+            f[k, 0], f[k, 1] = x, y
+            f[k, 2] = rng.uniform(0, 5)
+            f[k, 3] = rng.uniform(-math.pi, math.pi)
+            env.set_car(k, f[k], i[k])
+            placed.append((x, y))
+            k += 1
+
+
+def gen_ties():
+    """More than 16 neighbour candidates (IntersectionEnv.cpp:466-490): std::sort orders equal
+    distances by its partitions.  N >= 18 egos share spawn points (two cars on one point are
+    equidistant from every other) and symmetric spawn points tie too; rings of integer offsets
+    tie by construction."""
+    run("n18_team", n_agents=18, rays=96, use_team=True, steps=200, act="policy", seed=40)
+    run("n24_team", n_agents=24, rays=64, use_team=True, steps=150, act="policy", seed=41)
+    run("n32_r32", n_agents=32, rays=32, steps=60, act="policy", seed=42)
+    run("n20_ring", n_agents=20, rays=64, steps=4, act="random", seed=43, inject=inject_ego_ring)
+    run("ring_npc_k20", n_agents=1, rays=64, traffic=True, density=0.0, steps=150, act="policy", seed=44,
+        inject=inject_npc_ring(20))
+    run("ring_npc_k18_n4", n_agents=4, rays=64, traffic=True, density=0.0, steps=100, act="policy", seed=45,
+        inject=inject_npc_ring(18))
+
+
 # (name prefix or scenario name, generator, deterministic).  Traffic with density > 0 draws
 # its spawns from the reference's unseeded RNG (TrafficFlow.cpp:278,324): not reproducible.
 def _core():
@@ -452,7 +527,7 @@ def _traffic():
 
 
 GROUPS = [("core", _core, True), ("dims", gen_dims, True), ("paths", gen_paths, True), ("lidars", gen_lidars, True),
-          ("paths_short", gen_paths_short, True),
+          ("paths_short", gen_paths_short, True), ("ties", gen_ties, True),
           ("traffic", _traffic, False), ("dims_traffic", gen_dims_traffic, False),
           ("paths_traffic", gen_paths_traffic, False)]
 

@@ -42,3 +42,18 @@ def test_single_rank_dry_run():
     r = _run(["--dry-run"])
     assert r.returncode == 0, r.stderr[-2000:]
     assert json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+
+
+def test_config5_dry_run_over_8_ranks():
+    """BASELINE config 5's plumbing: 8 ranks (one per GPU on the node) over the gloo control plane,
+    128 beams, the gathered steps as the value."""
+    r = _run(["--gpus", "8", "--config", "5", "--dry-run", "--steps", "3", "--warmup", "1"], timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 8 and d["max_over_ranks"] == 8.0
+    assert d["config"] == 5 and d["rays"] == 128 and d["value_includes_gather"]
+
+
+def test_config5_refuses_no_gather():
+    r = _run(["--config", "5", "--no-gather", "--dry-run"])
+    assert r.returncode != 0 and "no-gather" in r.stderr

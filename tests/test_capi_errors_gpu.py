@@ -110,3 +110,17 @@ def test_add_route_validates_and_extends_the_id_range(mev):
     assert (got[:37].view(np.uint32) == path[:37].view(np.uint32)).all()
     assert (got[37:].view(np.uint32) == path[36].view(np.uint32)).all()
     h.close()
+
+
+def test_snapshot_format_1_is_refused_by_name(mev):
+    """A format-1 snapshot (before per-car sizes and the route hash) is refused with its own
+    message, and the handle is left as it was."""
+    h = mev.Handle(num_envs=2, num_agents=2, lidar_rays=16)
+    h.reset()
+    snap = h.snapshot()
+    old = snap.copy()
+    old[4:8] = np.frombuffer(np.uint32(1).tobytes(), np.uint8)  # SnapHeader::version
+    with pytest.raises(mev.MevError, match="format 1"):
+        h.restore(old)
+    h.restore(snap)  # the current format still restores
+    h.close()

@@ -147,7 +147,9 @@ def test_add_route_grows_tables_geometrically(mev):
 
 
 def test_beam_angles(mev):
-    """Lidar::rel_angles writes (cpp/bindings.cpp:92): evenly spaced offsets are taken, others refused;
+    """Lidar::rel_angles writes (cpp/bindings.cpp:92): any finite list with |angle| <= 1000 rad is
+    taken (lists the per-box beam culling cannot model -- uneven, descending -- run without it;
+    their simulation is pinned in test_gpu_vs_oracle.py rel_*), non-finite ones are refused;
     a handle whose rays are the first 32 of the reference's 96-beam list casts exactly those beams."""
     h = _handle(mev, lidar_rays=32, lidar_fov_deg=360.0)
     f32 = np.float32
@@ -155,9 +157,17 @@ def test_beam_angles(mev):
     rel96 = np.array([(start + f32(i) * stepd) * f32(np.pi) / f32(180.0) for i in range(96)], np.float32)
     h.set_beam_angles(rel96[:32])
     assert G.bits_equal(h.beam_angles(), rel96[:32])
+    uneven = rel96[:32].copy()
+    uneven[7] += 0.01
+    for ok in (uneven, rel96[:32][::-1].copy(), np.full(32, 0.5, np.float32)):
+        h.set_beam_angles(ok)
+        assert G.bits_equal(h.beam_angles(), ok)
     bad = rel96[:32].copy()
-    bad[7] += 0.01
+    bad[3] = np.inf
     with pytest.raises(mev.MevError):
         h.set_beam_angles(bad)
-    assert G.bits_equal(h.beam_angles(), rel96[:32])
+    bad[3] = 1001.0
+    with pytest.raises(mev.MevError):
+        h.set_beam_angles(bad)
+    assert G.bits_equal(h.beam_angles(), np.full(32, 0.5, np.float32))
     h.close()

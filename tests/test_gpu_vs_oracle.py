@@ -47,7 +47,45 @@ CONFIGS = [
     dict(name="dims_traffic_n3", n=3, rays=48, traffic=True, density=2.0, spawn_p=0.3, npcs=9, dims=True),
     dict(name="dims_traffic_n1", n=1, rays=64, traffic=True, density=0.5, spawn_p=0.2, npcs=12, npc_gap=45.0,
          dims=True),
+    # more than 16 neighbour candidates with exact distance ties (std::sort's order, IntersectionEnv.cpp:490):
+    # every car on a 30-px lattice of the road cross, half the egos parked (v = 0, zero throttle every step:
+    # they stay on their lattice points), so equal squared distances recur at every step
+    dict(name="n24_lattice_ties", n=24, rays=64, use_team=True, lattice=30, frozen=0.5),
+    dict(name="n40_lattice_ties", n=40, rays=32, lattice=30, frozen=0.6),
+    dict(name="traffic_lattice_ties", n=3, rays=48, traffic=True, density=1.0, spawn_p=0.3, npcs=24, lattice=30,
+         frozen=0.7),
+    # written Lidar.rel_angles (cpp/bindings.cpp:91) that the LiDAR's per-box beam culling cannot model
+    # (SimParams::beam_cull = 0: every beam against every candidate box): a reversed fan, uneven offsets,
+    # a fan over three revolutions, one repeated angle
+    dict(name="rel_reversed_n8", n=8, rays=32, rel="reversed"),
+    dict(name="rel_uneven_n8", n=8, rays=24, use_team=True, rel="uneven"),
+    dict(name="rel_wide_n6", n=6, rays=16, rel="wide"),
+    dict(name="rel_constant_traffic", n=2, rays=8, traffic=True, density=2.0, spawn_p=0.3, npcs=9, rel="constant"),
 ]
+
+
+def rel_list(kind, rays, rng):
+    """Beam offsets (radians) of a written Lidar.rel_angles."""
+    f32 = np.float32
+    fan = np.array([(f32(-180.0) + f32(i) * (f32(360.0) / f32(rays - 1))) * f32(np.pi) / f32(180.0)
+                    for i in range(rays)], np.float32)
+    if kind == "reversed":
+        return fan[::-1].copy()
+    if kind == "uneven":
+        return np.sort(rng.uniform(-np.pi, np.pi, rays)).astype(np.float32)
+    if kind == "wide":
+        return np.linspace(-3 * np.pi, 3 * np.pi, rays).astype(np.float32)
+    return np.full(rays, 0.3, np.float32)
+
+
+def lattice_points(rng, lanes, spacing, count):
+    """count distinct points of a `spacing`-px lattice centred on the intersection, inside the road cross."""
+    rw = 42 * lanes
+    ks = np.arange(-(375 // spacing), 375 // spacing + 1)
+    pts = [(375.0 + spacing * a, 375.0 + spacing * b) for a in ks for b in ks
+           if (abs(spacing * a) < rw or abs(spacing * b) < rw) and 0 < 375 + spacing * a < 750 and 0 < 375 + spacing * b < 750]
+    pick = rng.choice(len(pts), size=count, replace=False)
+    return [pts[k] for k in pick]
 
 
 def random_dims(rng, h):
@@ -77,7 +115,7 @@ def custom_routes(h, short=False):
     return out
 
 
-def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=()):
+def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=(), lattice=0, frozen=None):
     E = h.E
     st = h.get_state()
     ids = [h.route_id(s - 1, 4 * lanes + t - 1) for s, t in routes_table] + list(extra)
@@ -141,18 +179,30 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=()):
             st["npc_alive"][e, cnt] = 1
             cnt += 1
         st["npc_count"][e] = cnt
+    if lattice:  # every car of the env on its own lattice point; parked egos stand still
+        for e in range(E):
+            k = int(st["npc_count"][e])
+            pts = lattice_points(rng, lanes, lattice, n + k)
+            for i in range(n):
+                st["x"][e, i], st["y"][e, i] = pts[i]
+                if frozen[e, i]:
+                    st["v"][e, i] = 0.0
+            for j in range(k):
+                st["npc_x"][e, j], st["npc_y"][e, j] = pts[n + j]
     st["step_count"][:] = rng.integers(0, 5, E)
     h.set_state(st)
     return st, troutes
 
 
-def _oracle_from_state(cfg, st, e, troutes, customs=(), dims=None):
+def _oracle_from_state(cfg, st, e, troutes, customs=(), dims=None, rel=None):
     n = cfg["n"]
     meta = dict(rays=cfg["rays"], num_lanes=cfg.get("lanes", 3), n_agents=n, use_team=cfg.get("use_team", False),
                 respawn=cfg.get("respawn", True), max_steps=cfg.get("max_steps", 2000),
                 traffic=cfg.get("traffic", False), density=cfg.get("density", 0.5),
                 reward=cfg.get("reward", [10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2]))
     o = R.make_oracle(meta)
+    if rel is not None:
+        o.set_rel_angles(rel)
     for path, intent in customs:
         o.add_route(path, intent)
     o.set_traffic_routes(troutes)
@@ -239,6 +289,11 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0, max_npcs=64, E=2
         elif h.step_split() != 2:  # the early split needs the slots' beams in one 512-beam pool
             assert h.step_pack() * n * R_ > 512, (h.step_pack(), n, R_)
             pytest.skip("beams of the workgroup's slots exceed one LiDAR pool")
+    rel = None
+    if cfg.get("rel"):
+        rel = rel_list(cfg["rel"], R_, rng)
+        h.set_beam_angles(rel)
+        assert G.bits_equal(h.beam_angles(), rel)
     table = ROUTES2 if lanes == 2 else ROUTES3
     customs = custom_routes(h, cfg.get("custom") == "short") if cfg.get("custom") else []
     extra = [h.add_route(path, intent) for path, intent in customs]
@@ -248,7 +303,9 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0, max_npcs=64, E=2
         got = h.route_info(r)
         assert h.route_len(r) == len(path)
         assert G.bits_equal(got[0][: len(path)], path) and got[1] == intent and tuple(got[2][:2]) == tuple(path[0])
-    st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0), extra)
+    frozen = rng.uniform(size=(E, n)) < cfg.get("frozen", 0.0)
+    st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0), extra,
+                                cfg.get("lattice", 0), frozen)
     h.set_traffic_routes(troutes)
     dims = None
     if cfg.get("dims"):
@@ -256,7 +313,7 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0, max_npcs=64, E=2
         h.set_car_dims(*dims)
         assert h.car_dims_active()
         assert all(G.bits_equal(a, b) for a, b in zip(h.car_dims(), dims))
-    oracles = [_oracle_from_state(cfg, st, e, troutes, customs, dims) for e in range(E)]
+    oracles = [_oracle_from_state(cfg, st, e, troutes, customs, dims, rel) for e in range(E)]
     obs0 = h.observations()
     for e in range(E):
         assert G.bits_equal(obs0[e], oracles[e].observe()), f"env {e}: observation after set_state"
@@ -266,6 +323,7 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0, max_npcs=64, E=2
         acts = rng.uniform(-1, 1, (E, n, 2)).astype(np.float32)
         acts[rng.uniform(size=(E, n)) < 0.1] *= 2.5  # unclipped inputs
         acts[..., 0][rng.uniform(size=(E, n)) < 0.1] = 0.0  # exact-zero throttle (friction branch)
+        acts[..., 0][frozen] = 0.0  # parked egos (v = 0) stay on their lattice points
         spawn = None
         if cfg.get("traffic"):
             spawn = np.where(rng.uniform(size=E) < cfg["spawn_p"], rng.integers(0, len(troutes), E), -1).astype(np.int32)
