@@ -1280,6 +1280,9 @@ __device__ __forceinline__ bool write_obs_head(const SimParams& p, int i, const 
 // The 64 lanes as the array of std::sort (mev_nsort.h): position q at lane q & 63 of
 // d0/i0 (q < 64) or d1/i1; every index is wave-uniform, so a get is a readlane into
 // SGPRs and a set one compare-and-select per register.
+// TWO: positions 64 .. 127 too (more than 64 candidates possible: up to 63 other egos and
+// 64 NPCs); one half otherwise (no NPCs, or one ego and <= 64 NPC slots), half the code.
+template <bool TWO>
 struct WaveNRefs {
     float d0, d1;
     int i0, i1;
@@ -1289,17 +1292,21 @@ struct WaveNRefs {
     __device__ __forceinline__ NRef get(int q) const {
         const int l = q & (WAVE - 1);
         const float e0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d0), l));
+        const int j0 = __builtin_amdgcn_readlane(i0, l);
+        if constexpr (!TWO) return NRef{e0, j0};
         const float e1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d1), l));
-        const int j0 = __builtin_amdgcn_readlane(i0, l), j1 = __builtin_amdgcn_readlane(i1, l);
+        const int j1 = __builtin_amdgcn_readlane(i1, l);
         return q < WAVE ? NRef{e0, j0} : NRef{e1, j1};
     }
     __device__ __forceinline__ void set(int q, NRef r) {
         const bool here = lane == (q & (WAVE - 1));
-        const bool h0 = here && q < WAVE, h1 = here && q >= WAVE;
+        const bool h0 = TWO ? (here && q < WAVE) : here, h1 = here && q >= WAVE;
         d0 = h0 ? r.d : d0;
         i0 = h0 ? r.id : i0;
-        d1 = h1 ? r.d : d1;
-        i1 = h1 ? r.id : i1;
+        if constexpr (TWO) {
+            d1 = h1 ? r.d : d1;
+            i1 = h1 ? r.id : i1;
+        }
     }
 };
 struct WaveStack {
@@ -1341,7 +1348,7 @@ __device__ __forceinline__ int wave_argmin_dq(float d0, float d1, bool v0, bool 
 // them (ns_introsort, pruned at dlim), then the stable first five of that permutation
 // (its final insertion sort).  Rare: only when write_obs_head_tg found more than 16
 // candidates and an exact tie among the nearest.
-template <bool TRAFFIC, class EL, class NL>
+template <bool TRAFFIC, bool TWO, class EL, class NL>
 __device__ __forceinline__ void obs_exact_neighbours(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt,
                                                   float dlim, float* row) {
     const int lane = (int)(threadIdx.x & (WAVE - 1));
@@ -1364,8 +1371,10 @@ __device__ __forceinline__ void obs_exact_neighbours(const SimParams& p, int i, 
     const unsigned long long me = ballot(ve), mn = ballot(vn);
     const int ne = __builtin_popcountll(me), n = ne + __builtin_popcountll(mn);
     // position q of the push order: ego select_bit(me, q) or NPC select_bit(mn, q - ne)
-    WaveNRefs a;
+    WaveNRefs<TWO> a;
     a.lane = lane;
+    a.d1 = 0.0f;
+    a.i1 = 0;
     {
         const int q = lane;
         const int s = q < ne ? select_bit(me, q) : select_bit(mn, q - ne);
@@ -1374,7 +1383,7 @@ __device__ __forceinline__ void obs_exact_neighbours(const SimParams& p, int i, 
         a.d0 = q < ne ? fe : fn;
         a.i0 = q < ne ? s : MAXN + s;
     }
-    {
+    if constexpr (TWO) {
         const int q = lane + WAVE;
         const int s = q < ne ? select_bit(me, q) : select_bit(mn, q - ne);
         const float fe = __int_as_float(__builtin_amdgcn_ds_bpermute(s << 2, __float_as_int(de)));
@@ -1386,7 +1395,7 @@ __device__ __forceinline__ void obs_exact_neighbours(const SimParams& p, int i, 
     st.lane = lane;
     ns_introsort(a, n, dlim, st);
     // the stable first five of the permutation: smallest (d, position), five times
-    bool v0 = lane < n, v1 = lane + WAVE < n;
+    bool v0 = lane < n, v1 = TWO && lane + WAVE < n;
     int ids[NEIGHBOR_COUNT];
 #pragma unroll
     for (int q = 0; q < NEIGHBOR_COUNT; ++q) {
@@ -1414,14 +1423,20 @@ __device__ __forceinline__ void obs_exact_neighbours(const SimParams& p, int i, 
 
 // every lane of the wave: the agents whose write_obs_head_tg returned true (bit a of m:
 // agent a, its fifth distance in lane a of dl, its row at rows + a * ld)
-template <bool TRAFFIC, class EL, class NL>
-__device__ __forceinline__ void obs_exact_pass(const SimParams& p, unsigned long long m, float dl, const EL& el,
+#ifdef MEV_X_EXACT_CALL  // experiment: the rare pass as a real call
+#define MEV_EXACT_INLINE __noinline__
+#else
+#define MEV_EXACT_INLINE __forceinline__
+#endif
+// (TWO: more than 64 candidates possible, WaveNRefs)
+template <bool TRAFFIC, bool TWO, class EL, class NL>
+__device__ MEV_EXACT_INLINE void obs_exact_pass(const SimParams& p, unsigned long long m, float dl, const EL& el,
                                                const NL* nl, int ncnt, float* rows, size_t ld) {
     while (m) {
         const int a = __builtin_ctzll(m);
         m &= m - 1ull;
         const float dlim = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dl), a));
-        obs_exact_neighbours<TRAFFIC>(p, a, el, nl, ncnt, dlim, rows + (size_t)a * ld);
+        obs_exact_neighbours<TRAFFIC, TWO>(p, a, el, nl, ncnt, dlim, rows + (size_t)a * ld);
     }
 }
 
@@ -2277,7 +2292,10 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
     // ---- observation head (:418-520)
     QSTAMP(5);
     const int C = PK > 1 ? NE : N + (TRAFFIC ? ncnt : 0);  // neighbour candidates per agent (+ itself)
-    if (C <= 8) {
+    // (the fused kernels' compile-time layout without traffic holds N <= 8 agents: C <= 8,
+    // and the per-lane path below -- with its std::sort pass -- is not compiled into them)
+    constexpr bool kFew = !TRAFFIC && FUSED && !DIMS;
+    if (kFew || C <= 8) {
         // lane (grp, sub): agent i0 + grp, neighbour candidate sub; rank = position
         // in the stable distance order (== libstdc++ insertion sort, <= 16 elements)
         for (int i0 = 0; i0 < N; i0 += 8) {
@@ -2353,7 +2371,7 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
                 for (int cc = OBS_HEAD + p.lidar_slots + sub; cc < out.obs_ld; cc += 8) row[cc] = 0.0f;
             }
         }
-    } else {
+    } else if constexpr (!kFew) {
         bool exact = false;  // (N <= 64: one pass, lane i = agent i)
         float dl = 0.0f;
         for (int i = tid; i < N; i += WAVE) {
@@ -2368,7 +2386,11 @@ __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out
         }
         if constexpr (PK == 1) {
             const unsigned long long m = ballot(exact);
-            if (m) obs_exact_pass<TRAFFIC>(p, m, dl, el, nl, ncnt, out.obs + (size_t)e * NE * out.obs_ld, out.obs_ld);
+            // (more than 64 candidates only with the runtime layout's egos and traffic: with the
+            // compile-time traffic layout the env has one ego, and without traffic <= 63 others)
+            if (__builtin_expect(m != 0ull, 0))
+                obs_exact_pass<TRAFFIC, TRAFFIC && DIMS>(p, m, dl, el, nl, ncnt, out.obs + (size_t)e * NE * out.obs_ld,
+                                                         out.obs_ld);
         }
     }
     STAMP(6);
@@ -2764,9 +2786,9 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     const float rel_c1 = lane + WAVE < R ? src.rel(lane + WAVE) : 0.0f;
     // one beam: direction (Lidar.cpp:24-26) and the first probes; returns the
     // beam's result (>= 0) or -(next probe to test) - 1
-    // (uni: every lane's beam starts from the same car centre -- the wave-uniform safe bound;
-    // else a chunk of the dense layout that holds two agents' beams)
-    auto setup = [&](const float4& a, float rel_b, auto small, float2& d, auto uni) -> int {
+    // (uni, wave-uniform: every lane's beam starts from the same car centre -- the
+    // wave-uniform safe bound; else a chunk holding two agents' beams)
+    auto setup = [&](const float4& a, float rel_b, auto small, float2& d, bool uni) -> int {
         float sn, cs;
         if constexpr (decltype(small)::value) sincosf_below120(a.z + rel_b, &sn, &cs);
         else sincosf(a.z + rel_b, &sn, &cs);
@@ -2776,7 +2798,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const unsigned pmax = (unsigned)px > (unsigned)py ? (unsigned)px : (unsigned)py;
         const float idx = __builtin_amdgcn_rcpf(dx), idy = __builtin_amdgcn_rcpf(dy);
         float safe;
-        if constexpr (decltype(uni)::value)
+        if (uni)
             safe = road_safe_uniform(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
         else
             safe = road_safe(a.x, a.y, dx, dy, idx, idy, fabs_f(idx), fabs_f(idy), rwm, ccen, crf);
@@ -2794,7 +2816,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             const bool vb = b < R;
             const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : (vb ? src.rel(b) : 0.0f));
             float2 d;
-            const int r = setup(a, rel_b, small, d, std::true_type{});
+            const int r = setup(a, rel_b, small, d, true);
             if (vb) {
                 dir[j * R + b] = d;
                 res[j * R + b] = r >= 0 ? r : -r - 1;
@@ -2805,19 +2827,20 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             qn += __popcll(m);
         }
     };
-    // ILP = 2: two agents per pass, two independent dependency chains (sincosf's
-    // double polynomial, the safe distance, the probes) the compiler interleaves
-    // (k_step, 128 VGPRs); ILP = 1 in k_lidar, whose 64-VGPR budget would spill
-    // Dense layout (R not a multiple of 64, several agents): the pool's nal*R beams as
-    // consecutive 64-lane chunks, an agent's beams running on into the next chunk, ILP
-    // chunks per pass.  Per agent, R = 96 would take two chunks, the second half empty
-    // (and an odd agent count a discarded second chain): 20 chain-chunks for 8 agents
-    // instead of 13.
-    const bool dense = PART != 2 && (R & (WAVE - 1)) != 0 &&
-                       (nal * R + WAVE - 1) / WAVE < nal * ((R + WAVE - 1) / WAVE);
-    auto phase1_dense = [&](auto small) {
-        const float invRd = 1.0f / (float)R;
+    // The pool's nal*R beams in agent-major order as 64-lane chunks, ILP chunks per pass:
+    // ILP independent dependency chains (sincosf's double polynomial, the safe distance,
+    // the probes) the compiler interleaves (k_step, 128 VGPRs; ILP = 1 in k_lidar, whose
+    // 64-VGPR budget would spill).  R a multiple of 64: each chunk is one agent's beams
+    // (the wave-uniform safe bound); else a chunk may run from one agent's beams into the
+    // next's (the per-lane bound) -- R = 96 takes 6 chunks per 4 agents, not 8 half-empty.
+    const bool uni = (R & (WAVE - 1)) == 0 || nal == 1;
+    const float invRp = 1.0f / (float)R;
+    auto phase1 = [&](auto small) {
+        if constexpr (PART == 2) {  // the respawned agents only
+            for (unsigned long long tm = redo; tm; tm &= tm - 1ull) pass1_one(small, __builtin_ctzll(tm));
+        } else {
         const int nq = nal * R;
+        int jc = 0, bc = 0;  // (uni) the next chunk's agent and first beam
         for (int c0 = 0; c0 < nq; c0 += ILP * WAVE) {
             if (PART == 0 && 4 * c0 >= nq) __builtin_amdgcn_s_setprio(kPrioP1B);
             int q[ILP];
@@ -2825,16 +2848,29 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             float rb[ILP];
 #pragma unroll
             for (int u = 0; u < ILP; ++u) {
+                const int cq = c0 + u * WAVE < nq ? c0 + u * WAVE : c0;  // (a chunk past the pool: a copy of the first)
                 q[u] = c0 + u * WAVE + lane;
-                const int qc = q[u] < nq ? q[u] : nq - 1;
-                const int j = (int)(((float)qc + 0.5f) * invRd);  // exact (see load_beam)
-                a[u] = ag[j];
-                rb[u] = src.rel(qc - j * R);
+                if (uni) {  // chunk u of the pass: agent jc, beams bc .. bc + 63
+                    const bool in = c0 + u * WAVE < nq;
+                    const int j = in ? jc : 0, b0 = in ? bc : 0;
+                    a[u] = ag[j];
+                    // (k_step: the offsets from LDS; k_lidar: the first two chunks' offsets held
+                    // in registers, a global load per chunk would expose its latency)
+                    if constexpr (Src::kBoxLds) rb[u] = src.rel(b0 + lane);
+                    else rb[u] = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : src.rel(b0 + lane));
+                    bc += WAVE;
+                    if (bc >= R) { bc = 0; ++jc; }
+                } else {
+                    const int qc = cq + lane < nq ? cq + lane : nq - 1;
+                    const int j = (int)(((float)qc + 0.5f) * invRp);  // exact (see load_beam)
+                    a[u] = ag[j];
+                    rb[u] = src.rel(qc - j * R);
+                }
             }
             float2 d[ILP];
             int r[ILP];
 #pragma unroll
-            for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rb[u], small, d[u], std::false_type{});
+            for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rb[u], small, d[u], uni);
 #pragma unroll
             for (int u = 0; u < ILP; ++u) {
                 const bool vq = q[u] < nq;
@@ -2846,40 +2882,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                 const unsigned long long m = ballot(pend);
                 if (pend) queue[qn + lane_rank(m)] = (unsigned short)q[u];
                 qn += __popcll(m);
-            }
-        }
-    };
-    auto phase1 = [&](auto small) {
-        if constexpr (PART == 2) {  // the respawned agents only
-            for (unsigned long long tm = redo; tm; tm &= tm - 1ull) pass1_one(small, __builtin_ctzll(tm));
-        } else if (dense) {
-            phase1_dense(small);
-        } else {
-        for (int j = 0; j < nal; j += ILP) {
-            if (PART == 0 && 4 * j >= nal) __builtin_amdgcn_s_setprio(kPrioP1B);
-            float4 a[ILP];
-#pragma unroll
-            for (int u = 0; u < ILP; ++u) a[u] = ag[j + u < nal ? j + u : j];
-            for (int b0 = 0; b0 < R; b0 += WAVE) {
-                const int b = b0 + lane;
-                const bool vb = b < R;
-                const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : (vb ? src.rel(b) : 0.0f));
-                float2 d[ILP];
-                int r[ILP];
-#pragma unroll
-                for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rel_b, small, d[u], std::true_type{});
-#pragma unroll
-                for (int u = 0; u < ILP; ++u) {
-                    const bool in = j + u < nal;  // wave-uniform
-                    if (vb && in) {
-                        dir[(j + u) * R + b] = d[u];
-                        res[(j + u) * R + b] = r[u] >= 0 ? r[u] : -r[u] - 1;  // result, or the next probe to test
-                    }
-                    const bool pend = vb && in && r[u] < 0;
-                    const unsigned long long m = ballot(pend);
-                    if (pend) queue[qn + lane_rank(m)] = (unsigned short)((j + u) * R + b);
-                    qn += __popcll(m);
-                }
             }
         }
         }
@@ -3241,11 +3243,16 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
 }
 
 
-// Agents per LiDAR pool in k_step: the env's N agents in pools of at most 512
-// beams (all N in one pool at config 3).
+// Agents per LiDAR pool in k_step: the env's N agents in the fewest pools of at
+// most 512 beams, balanced (all N in one pool at config 3; 8 x 96 beams as 4 + 4
+// agents, 384 beams each, not 5 + 3: each pool's march ends on its longest beams,
+// and 4 agents of 96 beams fill six whole 64-lane chunks in phase 1).
 __host__ __device__ inline int step_pool(const SimParams& p) {
-    const int g = 512 / (p.R > 0 ? p.R : 1);
-    return g < 1 ? 1 : (g < p.N ? g : p.N);
+    int g = 512 / (p.R > 0 ? p.R : 1);
+    g = g < 1 ? 1 : g;
+    if (g >= p.N) return p.N;
+    const int pools = (p.N + g - 1) / g;
+    return (p.N + pools - 1) / pools;
 }
 
 // LDS of one k_step wave: cars LDS, the staged heads [N][31], the beam offsets
@@ -3529,7 +3536,8 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
         for (int b = 0; b < p.lidar_slots; ++b) row[OBS_HEAD + b] = p.lidar_max * p.lidar_inv;
     }
     const unsigned long long m = ballot(exact);
-    if (m) obs_exact_pass<TRAFFIC>(p, m, dl, el, nl, ncnt, out.obs + (size_t)e * N * p.D, (size_t)p.D);
+    if (__builtin_expect(m != 0ull, 0))
+        obs_exact_pass<TRAFFIC, TRAFFIC>(p, m, dl, el, nl, ncnt, out.obs + (size_t)e * N * p.D, (size_t)p.D);
 }
 
 static hipError_t launch_part(const SimParams& p, const StepInputs& in, const Outputs& out, int e0, int e1,
@@ -3846,7 +3854,8 @@ __global__ __launch_bounds__(WAVE) void k_decode_state(SimParams p, const uint8_
                                          bad ? nan : path[2 * ti + 1], row, false, &dl);
     }
     const unsigned long long m = ballot(exact);
-    if (m) obs_exact_pass<false>(p, m, dl, el, (const NpcLDST<MAXK>*)nullptr, 0, obs + (size_t)g * N * D, (size_t)D);
+    if (__builtin_expect(m != 0ull, 0))
+        obs_exact_pass<false, false>(p, m, dl, el, (const NpcLDST<MAXK>*)nullptr, 0, obs + (size_t)g * N * D, (size_t)D);
     // LiDAR block and padding, every lane: (agent, column) pairs
     const int tail = D - OBS_HEAD;
     for (int t = lane; t < N * tail; t += WAVE) {

@@ -86,16 +86,26 @@ MEV_NS_HD void ns_heapsort(Acc& a, int f, int len) {
 #ifdef MEV_NS_COUNT_HEAP
     ++MEV_NS_COUNT_HEAP;  // host test hook (tests/native/nsort_check.cpp)
 #endif
-    if (len >= 2)
-        for (int parent = (len - 2) / 2;; --parent) {
-            ns_adjust_heap(a, f, parent, len, a.get(f + parent));
-            if (parent == 0) break;
+    // one loop, one __adjust_heap site (the device inlines it once): steps t < m are
+    // __make_heap's (parent = m - 1 - t, down to 0), the rest __sort_heap's pops
+    // (l = len - 1 - (t - m), down to 1)
+    const int m = len >= 2 ? (len - 2) / 2 + 1 : 0;
+    const int steps = m + (len > 1 ? len - 1 : 0);
+    for (int t = 0; t < steps; ++t) {
+        int hole, hlen;
+        NRef v;
+        if (t < m) {
+            hole = m - 1 - t;
+            hlen = len;
+            v = a.get(f + hole);
+        } else {
+            const int l = len - 1 - (t - m);
+            v = a.get(f + l);
+            a.set(f + l, a.get(f));
+            hole = 0;
+            hlen = l;
         }
-    for (int l = len; l > 1;) {
-        --l;
-        const NRef v = a.get(f + l);
-        a.set(f + l, a.get(f));
-        ns_adjust_heap(a, f, 0, l, v);
+        ns_adjust_heap(a, f, hole, hlen, v);
     }
 }
 
