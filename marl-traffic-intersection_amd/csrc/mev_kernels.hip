@@ -1423,14 +1423,11 @@ __device__ __forceinline__ void obs_exact_neighbours(const SimParams& p, int i, 
 
 // every lane of the wave: the agents whose write_obs_head_tg returned true (bit a of m:
 // agent a, its fifth distance in lane a of dl, its row at rows + a * ld)
-#ifdef MEV_X_EXACT_CALL  // experiment: the rare pass as a real call
-#define MEV_EXACT_INLINE __noinline__
-#else
-#define MEV_EXACT_INLINE __forceinline__
-#endif
+// (inlined: as a real call -- a kernel with a call sets up a stack -- configs 3 and 4 ran
+// 41 us per step instead of 33 / 28, profiles/r6_ab_exact_call_cfg3.txt, _cfg4.txt)
 // (TWO: more than 64 candidates possible, WaveNRefs)
 template <bool TRAFFIC, bool TWO, class EL, class NL>
-__device__ MEV_EXACT_INLINE void obs_exact_pass(const SimParams& p, unsigned long long m, float dl, const EL& el,
+__device__ __forceinline__ void obs_exact_pass(const SimParams& p, unsigned long long m, float dl, const EL& el,
                                                const NL* nl, int ncnt, float* rows, size_t ld) {
     while (m) {
         const int a = __builtin_ctzll(m);
@@ -2827,61 +2824,77 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
             qn += __popcll(m);
         }
     };
-    // The pool's nal*R beams in agent-major order as 64-lane chunks, ILP chunks per pass:
-    // ILP independent dependency chains (sincosf's double polynomial, the safe distance,
-    // the probes) the compiler interleaves (k_step, 128 VGPRs; ILP = 1 in k_lidar, whose
-    // 64-VGPR budget would spill).  R a multiple of 64: each chunk is one agent's beams
-    // (the wave-uniform safe bound); else a chunk may run from one agent's beams into the
-    // next's (the per-lane bound) -- R = 96 takes 6 chunks per 4 agents, not 8 half-empty.
-    const bool uni = (R & (WAVE - 1)) == 0 || nal == 1;
-    const float invRp = 1.0f / (float)R;
+    // ILP = 2: two agents per pass, two independent dependency chains (sincosf's
+    // double polynomial, the safe distance, the probes) the compiler interleaves
+    // (k_step, 128 VGPRs); ILP = 1 in k_lidar, whose 64-VGPR budget would spill.
+    // R not a multiple of 64 (several agents): the dense layout instead -- the pool's
+    // nal*R beams as consecutive 64-lane chunks, an agent's beams running on into the
+    // next chunk, ILP chunks per pass; R = 96 takes 6 chunks per 4 agents, not 8
+    // half-empty ones.  (One loop for both measured 2 % slower at config 3: the chunk
+    // walk's bookkeeping and the offsets' LDS reads in front of every pass.)
+    const bool dense = (R & (WAVE - 1)) != 0 && nal > 1;
     auto phase1 = [&](auto small) {
         if constexpr (PART == 2) {  // the respawned agents only
             for (unsigned long long tm = redo; tm; tm &= tm - 1ull) pass1_one(small, __builtin_ctzll(tm));
-        } else {
-        const int nq = nal * R;
-        int jc = 0, bc = 0;  // (uni) the next chunk's agent and first beam
-        for (int c0 = 0; c0 < nq; c0 += ILP * WAVE) {
-            if (PART == 0 && 4 * c0 >= nq) __builtin_amdgcn_s_setprio(kPrioP1B);
-            int q[ILP];
-            float4 a[ILP];
-            float rb[ILP];
+        } else if (dense) {
+            const float invRp = 1.0f / (float)R;
+            const int nq = nal * R;
+            for (int c0 = 0; c0 < nq; c0 += ILP * WAVE) {
+                if (PART == 0 && 4 * c0 >= nq) __builtin_amdgcn_s_setprio(kPrioP1B);
+                int q[ILP];
+                float4 a[ILP];
+                float rb[ILP];
 #pragma unroll
-            for (int u = 0; u < ILP; ++u) {
-                const int cq = c0 + u * WAVE < nq ? c0 + u * WAVE : c0;  // (a chunk past the pool: a copy of the first)
-                q[u] = c0 + u * WAVE + lane;
-                if (uni) {  // chunk u of the pass: agent jc, beams bc .. bc + 63
-                    const bool in = c0 + u * WAVE < nq;
-                    const int j = in ? jc : 0, b0 = in ? bc : 0;
-                    a[u] = ag[j];
-                    // (k_step: the offsets from LDS; k_lidar: the first two chunks' offsets held
-                    // in registers, a global load per chunk would expose its latency)
-                    if constexpr (Src::kBoxLds) rb[u] = src.rel(b0 + lane);
-                    else rb[u] = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : src.rel(b0 + lane));
-                    bc += WAVE;
-                    if (bc >= R) { bc = 0; ++jc; }
-                } else {
-                    const int qc = cq + lane < nq ? cq + lane : nq - 1;
+                for (int u = 0; u < ILP; ++u) {
+                    q[u] = c0 + u * WAVE + lane;
+                    const int qc = q[u] < nq ? q[u] : nq - 1;
                     const int j = (int)(((float)qc + 0.5f) * invRp);  // exact (see load_beam)
                     a[u] = ag[j];
                     rb[u] = src.rel(qc - j * R);
                 }
-            }
-            float2 d[ILP];
-            int r[ILP];
+                float2 d[ILP];
+                int r[ILP];
 #pragma unroll
-            for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rb[u], small, d[u], uni);
+                for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rb[u], small, d[u], false);
 #pragma unroll
-            for (int u = 0; u < ILP; ++u) {
-                const bool vq = q[u] < nq;
-                if (vq) {
-                    dir[q[u]] = d[u];
-                    res[q[u]] = r[u] >= 0 ? r[u] : -r[u] - 1;  // result, or the next probe to test
+                for (int u = 0; u < ILP; ++u) {
+                    const bool vq = q[u] < nq;
+                    if (vq) {
+                        dir[q[u]] = d[u];
+                        res[q[u]] = r[u] >= 0 ? r[u] : -r[u] - 1;  // result, or the next probe to test
+                    }
+                    const bool pend = vq && r[u] < 0;
+                    const unsigned long long m = ballot(pend);
+                    if (pend) queue[qn + lane_rank(m)] = (unsigned short)q[u];
+                    qn += __popcll(m);
                 }
-                const bool pend = vq && r[u] < 0;
-                const unsigned long long m = ballot(pend);
-                if (pend) queue[qn + lane_rank(m)] = (unsigned short)q[u];
-                qn += __popcll(m);
+            }
+        } else {
+        for (int j = 0; j < nal; j += ILP) {
+            if (PART == 0 && 4 * j >= nal) __builtin_amdgcn_s_setprio(kPrioP1B);
+            float4 a[ILP];
+#pragma unroll
+            for (int u = 0; u < ILP; ++u) a[u] = ag[j + u < nal ? j + u : j];
+            for (int b0 = 0; b0 < R; b0 += WAVE) {
+                const int b = b0 + lane;
+                const bool vb = b < R;
+                const float rel_b = b0 == 0 ? rel_c0 : (b0 == WAVE ? rel_c1 : (vb ? src.rel(b) : 0.0f));
+                float2 d[ILP];
+                int r[ILP];
+#pragma unroll
+                for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rel_b, small, d[u], true);
+#pragma unroll
+                for (int u = 0; u < ILP; ++u) {
+                    const bool in = j + u < nal;  // wave-uniform
+                    if (vb && in) {
+                        dir[(j + u) * R + b] = d[u];
+                        res[(j + u) * R + b] = r[u] >= 0 ? r[u] : -r[u] - 1;  // result, or the next probe to test
+                    }
+                    const bool pend = vb && in && r[u] < 0;
+                    const unsigned long long m = ballot(pend);
+                    if (pend) queue[qn + lane_rank(m)] = (unsigned short)((j + u) * R + b);
+                    qn += __popcll(m);
+                }
             }
         }
         }
@@ -3049,6 +3062,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // a ray outside it never meets the slab, so none of its probes can land in
     // the box.
     const float rel0 = src.rel(0);
+    const bool all_beams = R == 1 || !p.beam_cull;  // (no linear model of the offsets: SimParams::beam_cull)
     const float dphi = R > 1 ? (src.rel(R - 1) - rel0) / (float)(R - 1) : 1.0f;
     const float idphi = 1.0f / dphi;
     const float period = 6.28318531f * idphi;  // beam indices per revolution
@@ -3060,7 +3074,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         const float ex0 = box_lo(bx.x), ex1 = box_hi(bx.y);
         const float ey0 = box_lo(bx.z), ey1 = box_hi(bx.w);
         int4 rg;
-        if (R == 1 || !p.beam_cull || (a.x >= ex0 && a.x <= ex1 && a.y >= ey0 && a.y <= ey1)) {  // (on its edge too)
+        if (all_beams || (a.x >= ex0 && a.x <= ex1 && a.y >= ey0 && a.y <= ey1)) {  // (on its edge too)
             rg = make_int4(0 | (R << 16), 0, 0, R);  // inside the widened box: every beam
         } else {
             // the box's silhouette seen from the agent (outside it): the two corners
@@ -3178,9 +3192,6 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (Src::kBoxLds) return;
 #endif
     // 3d: Lidar::normalized (:92-98), the LiDAR block of each alive agent's row
-    auto lidar_value = [&](int r) {
-        return ((r & 1) ? march_dist<TAB>(p, r >> 1) : p.lidar_max) * p.lidar_inv;
-    };
     if (out.lidar_u8) {  // compact gather format: one code per beam (0 no hit, k + 1 hit at probe k)
         for (int j = 0; j < nal; ++j) {
             const int g = __float_as_int(ag[j].w);
@@ -3222,7 +3233,8 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         for (int j = 0; j < nal; ++j) {
             const int g = __float_as_int(ag[j].w);
             float* row = out.obs + (size_t)g * out.obs_ld + OBS_HEAD;
-            for (int b = lane; b < p.lidar_slots; b += WAVE) row[b] = lidar_value(res[j * R + b]);
+            for (int b = lane; b < p.lidar_slots; b += WAVE)
+                row[b] = ((res[j * R + b] & 1) ? march_dist<TAB>(p, res[j * R + b] >> 1) : p.lidar_max) * p.lidar_inv;
         }
     }
 }
