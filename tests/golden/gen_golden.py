@@ -476,6 +476,10 @@ def gen_ties():
         inject=inject_npc_ring(20))
     run("ring_npc_k18_n4", n_agents=4, rays=64, traffic=True, density=0.0, steps=100, act="policy", seed=45,
         inject=inject_npc_ring(18))
+    # the largest fleets a handle takes: 64 egos (mev_create's limit), and 1 ego among 48 NPCs of 64 slots
+    run("n64_r16", n_agents=64, rays=16, steps=40, act="policy", seed=46)
+    run("ring_npc_k48", n_agents=1, rays=32, traffic=True, density=0.0, steps=80, act="policy", seed=47,
+        inject=inject_npc_ring(48, spread=340))
 
 
 # (name prefix or scenario name, generator, deterministic).  Traffic with density > 0 draws

@@ -123,13 +123,19 @@ def set_dims(h, data):
     h.set_car_dims(ego, npc)
 
 
-def make_handle(mod, meta, num_envs: int, device: int = 0):
+def npc_slots(data) -> int:
+    """NPC slots a handle needs for these scenarios: 32, or 64 past 32 NPCs (ring_npc_k48)."""
+    k = max(max(len(d["init_npc_f"]), int(d["npc_count"].max()) if len(d["npc_count"]) else 0) for d in data)
+    return 32 if k <= 32 else 64
+
+
+def make_handle(mod, meta, num_envs: int, device: int = 0, max_npcs: int = 32):
     R = int(meta["rays"])
     return mod.Handle(num_envs=num_envs, num_agents=int(meta["n_agents"]), num_lanes=int(meta["num_lanes"]),
                       lidar_rays=R, obs_dim=127 if R <= 96 else 31 + R, traffic_flow=int(meta["traffic"]),
                       traffic_density=float(meta["density"]), use_team_reward=int(meta["use_team"]),
                       respawn_enabled=int(meta["respawn"]), max_steps=int(meta["max_steps"]),
-                      reward=meta["reward"], max_npcs=32, device=device)
+                      reward=meta["reward"], max_npcs=max_npcs, device=device)
 
 
 def single_env_handle(mod, d):
@@ -137,7 +143,7 @@ def single_env_handle(mod, d):
     returns (handle, spawn_route(t) for its steps)."""
     meta = d["meta"]
     L = int(meta["num_lanes"])
-    h = make_handle(mod, meta, 1)
+    h = make_handle(mod, meta, 1, max_npcs=npc_slots([d]))
     cids = custom_route_ids(h, d)
     troutes = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["traffic_routes"]]
     h.set_traffic_routes(troutes)
@@ -179,7 +185,7 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
             assert d["meta"][k] == meta[k], f"scenario configs differ in {k}"
     B = len(data)
     L = int(meta["num_lanes"])
-    h = make_handle(mod, meta, B)
+    h = make_handle(mod, meta, B, max_npcs=npc_slots(data))
     if kernel:
         try:
             h.set_step_kernel(kernel)
