@@ -20,7 +20,7 @@ import oracle_replay as R
 pytestmark = pytest.mark.gpu
 
 E, N, RAYS, T, MAXS, DENSITY, SEED, DT = 4096, 1, 64, 300, 2000, 0.5, 3, 1.0 / 60.0
-META = dict(rays=RAYS, obs_dim=127, num_lanes=3, n_agents=N, use_team=False, respawn=True, max_steps=MAXS,
+META = dict(rays=RAYS, obs_dim=31 + RAYS, num_lanes=3, n_agents=N, use_team=False, respawn=True, max_steps=MAXS,
             traffic=True, density=DENSITY, reward=[10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2])
 M32 = 0xFFFFFFFF
 
