@@ -149,12 +149,12 @@ int mev_car_check_collision(const float* box_a, const float* box_b, int32_t* col
 int mev_num_points(const mev_handle* h, int32_t* n);
 int mev_point_xy(const mev_handle* h, int32_t point, float* xy);
 int mev_route_id(const mev_handle* h, int32_t start_point, int32_t end_point, int32_t* route);
-/* path [160][2], intent, spawn (x, y, heading) of a route (a route of n < 160
- * points reads back padded with its last point; mev_route_len gives n) */
+/* path [max(n, 160)][2], intent, spawn (x, y, heading) of a route of n points
+ * (mev_route_len; a route of n < 160 points reads back padded with its last point) */
 int mev_route_info(const mev_handle* h, int32_t route, float* path, int32_t* intent, float* spawn);
 int mev_route_len(const mev_handle* h, int32_t route, int32_t* npoints);
 int mev_path_len(void);
-/* A route of the caller's own: path [npoints][2], 2 <= npoints <= 160 (every
+/* A route of the caller's own: path [npoints][2], 2 <= npoints <= 4096 (every
  * path the reference generates has 160, RouteGen.cpp:111-205), and intent (0
  * straight, 1 left, 2 right) appended to the handle's route table; *route
  * receives its id (>= P*P, the lane-layout routes).  Cars and NPCs then take it
@@ -162,9 +162,11 @@ int mev_path_len(void);
  * heading to path[1].  Replaces assigning Car.path in the reference
  * (cpp/bindings.cpp:29, a read-write std::vector member): every reader clamps
  * to path.size() (Car.cpp:56, IntersectionEnv.cpp:177-179,446,
- * TrafficFlow.cpp:55,89,263), as the device does.  A car's path_index must stay
- * below npoints (the reference's only path_index writes are its own search and
- * the bound member); an NPC at path_index >= npoints would ghost-scan the padding.
+ * TrafficFlow.cpp:55,89,263), as the device does, also for a car whose
+ * path_index lies past its path's end (set through mev_set_state: the index
+ * search keeps it, the look-ahead clamps to path.back(), an NPC's ghost scan is
+ * empty).  A path longer than the table's rows re-lays the table out at that
+ * length rounded up to 16 points (one re-upload; every route keeps its ids).
  * mev_add_route(h, path, intent, route) = mev_add_route_n(h, path, 160, ...). */
 int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* route);
 int mev_add_route_n(mev_handle* h, const float* path, int32_t npoints, int32_t intent, int32_t* route);

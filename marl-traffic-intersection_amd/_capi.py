@@ -32,7 +32,8 @@ PACKED_FIELDS = ("obs", "reward", "done", "status", "terminated", "truncated", "
 DLPACK_OUTPUTS = ("obs", "reward", "done", "status", "terminated", "truncated", "agents_alive", "step", "gathered")
 
 STATUS_NAMES = ("ALIVE", "DEAD", "SUCCESS", "CRASH_WALL", "CRASH_LINE", "CRASH_CAR")
-PATH_LEN = 160
+PATH_LEN = 160  # every lane-layout route
+MAX_PATH_LEN = 4096  # a written path (mev_add_route_n)
 
 # exported symbols that include/marlenv.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = (
@@ -376,7 +377,8 @@ class Handle:
         return r.value
 
     def route_info(self, route: int):
-        path = np.zeros((PATH_LEN, 2), np.float32)
+        """(path [max(n, 160), 2] -- a shorter path padded with its last point --, intent, spawn)."""
+        path = np.zeros((max(PATH_LEN, self.route_len(route)), 2), np.float32)
         intent = ctypes.c_int32()
         spawn = np.zeros(3, np.float32)
         _check(self._lib.mev_route_info(self._h, int(route), path.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
@@ -384,17 +386,17 @@ class Handle:
         return path, intent.value, spawn
 
     def route_len(self, route: int) -> int:
-        """Points of a route's path (160, or a shorter path's own n; mev_route_len)."""
+        """Points of a route's path (160, or a written path's own n; mev_route_len)."""
         n = ctypes.c_int32()
         _check(self._lib.mev_route_len(self._h, int(route), ctypes.byref(n)))
         return n.value
 
     def add_route(self, path, intent: int) -> int:
-        """Append a route of the caller's own (path [n, 2] f32 with 2 <= n <= 160, intent 0 straight /
+        """Append a route of the caller's own (path [n, 2] f32 with 2 <= n <= 4096, intent 0 straight /
         1 left / 2 right) to the route table (mev_add_route_n); returns its id."""
         a = np.ascontiguousarray(path, np.float32)
-        if a.ndim != 2 or a.shape[1] != 2 or not 2 <= a.shape[0] <= PATH_LEN:
-            raise ValueError(f"a route path has 2 .. {PATH_LEN} points (x, y), got shape {a.shape}")
+        if a.ndim != 2 or a.shape[1] != 2 or not 2 <= a.shape[0] <= MAX_PATH_LEN:
+            raise ValueError(f"a route path has 2 .. {MAX_PATH_LEN} points (x, y), got shape {a.shape}")
         r = ctypes.c_int32()
         _check(self._lib.mev_add_route_n(self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), a.shape[0],
                                          int(intent), ctypes.byref(r)))

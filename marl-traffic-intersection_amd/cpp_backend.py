@@ -19,11 +19,11 @@ Deviations from MARLEnv (all outside the hot path):
    (|angle| <= 1000 rad) with at least `rays` entries, and rays >= 1 (the reference
    reads past the end otherwise);
    `lidars` must hold one Lidar per car, or one configuration for all of them;
- * Car.path may be any path of 2 .. 160 points (every path MARLEnv itself
+ * Car.path may be any path of 2 .. 4096 points (every path MARLEnv itself
    generates has 160, RouteGen.cpp:111-205); a path that is not a lane-layout route
-   is appended to the device route table (mev_add_route_n); longer paths, and
-   shorter ones than 2 points, raise ValueError, as does a traffic car whose
-   path_index is not below its path's length (its ghost scan would differ);
+   is appended to the device route table (mev_add_route_n); paths of fewer than 2 or
+   more than 4096 points raise ValueError (the reference reads path[1] of any
+   non-empty path);
  * Car.length / Car.width (bindings.cpp:24-25) are simulated per car, as in the
    reference (status corners, SAT collisions, LiDAR boxes; mev_set_car_dims), in
    |value| <= 1e4 px;
@@ -252,8 +252,8 @@ class IntersectionEnv:
         self.num_lanes = int(num_lanes)
         self._device = int(device)
         self._max_npcs = int(max_npcs)
-        self._paths = {}  # route id -> its 160 path points as (x, y) tuples (Car.path)
-        self._route_ids = None  # path bytes (f32 [160, 2]) -> route id, built on first use
+        self._paths = {}  # route id -> its path points as (x, y) tuples (Car.path)
+        self._route_ids = None  # path bytes (f32 [n, 2]) -> route id, built on first use
         self._custom: List[Tuple[np.ndarray, int]] = []  # Car.path routes of the caller's own, in id order
         self._use_team, self._respawn, self._max_steps = False, True, 2000
         self._traffic, self._density = False, 0.5
@@ -580,7 +580,7 @@ class IntersectionEnv:
 
     def _route_of(self, c: Car) -> int:
         """The route id of Car.path (read-write in MARLEnv, cpp/bindings.cpp:29): a lane-layout route or one
-        registered before, else a new route of the caller's own (mev_add_route_n; 2 .. 160 points)."""
+        registered before, else a new route of the caller's own (mev_add_route_n; 2 .. 4096 points)."""
         if len(c.path) == 0:
             if c._route >= 0:
                 return c._route
@@ -594,8 +594,8 @@ class IntersectionEnv:
         r = self._route_ids.get(want.tobytes())
         if r is not None:
             return r
-        if not 2 <= len(want) <= _capi.PATH_LEN:
-            raise ValueError(f"Car.path must have 2 .. {_capi.PATH_LEN} points (every path the reference "
+        if not 2 <= len(want) <= _capi.MAX_PATH_LEN:
+            raise ValueError(f"Car.path must have 2 .. {_capi.MAX_PATH_LEN} points (every path the reference "
                              f"generates has {_capi.PATH_LEN}, RouteGen.cpp:111-205); got {len(want)}")
         intent = min(max(int(c.intention), 0), 2)
         r = self._h.add_route(want, intent)
@@ -639,11 +639,6 @@ class IntersectionEnv:
         if n == 0:
             self._routes = []
             return
-        for c in s.traffic_cars:
-            # past the end of a short path the reference's ghost scan is empty (TrafficFlow.cpp:89);
-            # the device row repeats the last point there (mev_add_route_n)
-            if 0 < len(c.path) < _capi.PATH_LEN and c.path_index >= len(c.path):
-                raise ValueError(f"traffic car path_index {c.path_index} is past its {len(c.path)}-point path")
         if self._h is None or self._h.N != n or self._h_lidar != lidar:
             if self._h is not None:
                 self._h.close()

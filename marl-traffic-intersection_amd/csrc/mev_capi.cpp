@@ -53,8 +53,11 @@ struct mev_handle {
     int D = 0, lidar_slots = 0, P = 0, nroutes = 0;
     int route_cap = 0;  // routes the device route tables have room for (mev_add_route)
     std::vector<mev::LanePoint> pts;
-    std::vector<float> h_paths, h_spawn;  // h_paths: [nroutes][ROUTE_PTS][2] (mev_world.h)
-    std::vector<int32_t> h_len;           // points of each route's path (2 .. PATH_LEN)
+    std::vector<float> h_paths, h_spawn;  // h_paths: [nroutes][row_pts][2] (mev_world.h)
+    std::vector<int32_t> h_len;           // points of each route's path (2 .. MAX_PATH_LEN)
+    // the table's row geometry (RouteTab::plen / row): PATH_LEN / ROUTE_PTS until a written
+    // path longer than PATH_LEN is added, then that path's length rounded up to 16
+    int plen = mev::PATH_LEN, row_pts = mev::ROUTE_PTS;
     std::vector<float> h_pbox;  // [nroutes][3][4] piece bounding boxes (RouteTab::pbox)
     std::vector<int32_t> h_intent;
     // route_hash[r]: FNV-1a of routes [0, r) (paths and intents), so a snapshot or a gather
@@ -68,7 +71,16 @@ struct mev_handle {
                 const uint8_t* b = static_cast<const uint8_t*>(p);
                 for (size_t i = 0; i < n; ++i) x = (x ^ b[i]) * 1099511628211ull;
             };
-            mix(&h_paths[r * 2 * mev::ROUTE_PTS], 2 * mev::ROUTE_PTS * sizeof(float));
+            // a path as its first max(n, PATH_LEN) row points, its last segment and, up to
+            // PATH_LEN, the ROUTE_PTS row's zero tail: the same bytes whatever the row stride
+            const float* row = &h_paths[r * 2 * size_t(row_pts)];
+            const int n = std::max(h_len[r], mev::PATH_LEN);
+            mix(row, 2 * size_t(n) * sizeof(float));
+            mix(row + 2 * plen, 4 * sizeof(float));
+            if (n == mev::PATH_LEN) {
+                const float z[2 * (mev::ROUTE_PTS - mev::ROUTE_END - 2)] = {};
+                mix(z, sizeof(z));
+            }
             mix(&h_intent[r], sizeof(int32_t));
             route_hash.push_back(x);
         }
@@ -87,6 +99,7 @@ struct mev_handle {
     int32_t* d_spawn = nullptr;
     uint8_t* d_mask = nullptr;
     float* d_paths = nullptr;
+    int32_t* d_rlen = nullptr;  // [route_cap] each path's own length (RouteTab::len)
     float* d_pbox = nullptr;
     float* d_spawn_tab = nullptr;
     int32_t* d_intent = nullptr;
@@ -421,7 +434,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     A(&h->internal.step, size_t(E));
     // inputs & tables
     A(&h->d_actions, EN * 2); A(&h->d_spawn, size_t(E)); A(&h->d_mask, size_t(E));
-    A(&h->d_paths, h->h_paths.size()); A(&h->d_pbox, h->h_pbox.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
+    A(&h->d_paths, h->h_paths.size()); A(&h->d_rlen, h->h_len.size()); A(&h->d_pbox, h->h_pbox.size()); A(&h->d_spawn_tab, h->h_spawn.size()); A(&h->d_intent, h->h_intent.size());
     A(&h->d_rel, rel.size()); A(&h->d_traffic, size_t(h->P) * size_t(h->P));
     A(&h->d_reset_routes, size_t(h->P) * size_t(h->P));
     A(&h->d_lidar_table, size_t(256));
@@ -440,6 +453,7 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_spawn_tab, h->h_spawn.data(), h->h_spawn.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_pbox, h->h_pbox.data(), h->h_pbox.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_intent, h->h_intent.data(), h->h_intent.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
+    if (err == hipSuccess) err = hipMemcpyAsync(h->d_rlen, h->h_len.data(), h->h_len.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess) err = hipMemcpyAsync(h->d_rel, rel.data(), rel.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess && d_dist) err = hipMemcpyAsync(d_dist, dists.data(), dists.size() * sizeof(float), hipMemcpyHostToDevice, h->stream);
     if (err == hipSuccess)
@@ -497,6 +511,10 @@ int mev_create(const mev_config* cfg, mev_handle** out) {
     p.rt.spawn = h->d_spawn_tab;
     p.rt.pbox = reinterpret_cast<const float4*>(h->d_pbox);
     p.rt.nroutes = h->nroutes;
+    p.rt.len = h->d_rlen;
+    p.rt.plen = mev::PATH_LEN;
+    p.rt.row = mev::ROUTE_PTS;
+    p.rt.min_len = mev::PATH_LEN;
     p.rel_angles = h->d_rel;
     p.traffic_routes = h->d_traffic;
     p.n_traffic_routes = int(h->h_traffic.size());
@@ -669,7 +687,10 @@ int mev_route_len(const mev_handle* h, int32_t route, int32_t* npoints) {
 int mev_route_info(const mev_handle* h, int32_t route, float* path, int32_t* intent, float* spawn) {
     if (!h) return fail(MEV_E_INVALID, "null handle");
     if (route < 0 || route >= h->nroutes) return fail(MEV_E_RANGE, "route out of range");
-    if (path) memcpy(path, &h->h_paths[size_t(route) * 2 * mev::ROUTE_PTS], sizeof(float) * 2 * mev::PATH_LEN);
+    if (path) {  // max(n, PATH_LEN) points: a shorter path padded with its last point
+        const int n = std::max(h->h_len[size_t(route)], mev::PATH_LEN);
+        memcpy(path, &h->h_paths[size_t(route) * 2 * size_t(h->row_pts)], sizeof(float) * 2 * size_t(n));
+    }
     if (intent) *intent = h->h_intent[size_t(route)];
     if (spawn) memcpy(spawn, &h->h_spawn[size_t(3 * route)], sizeof(float) * 3);
     return MEV_OK;
@@ -679,20 +700,26 @@ int mev_add_route(mev_handle* h, const float* path, int32_t intent, int32_t* rou
     return mev_add_route_n(h, path, mev::PATH_LEN, intent, route);
 }
 
+namespace {
+// a route-table row of `plen` points: the n points, padded with the last one, then the
+// last segment at plen, plen + 1 and zeros up to plen + 16 (mev_world.h)
+void fill_row(float* row, const float* pts, int n, int plen) {
+    for (int i = 0; i < plen; ++i) {
+        const int q = i < n ? i : n - 1;
+        row[2 * i] = pts[2 * q];
+        row[2 * i + 1] = pts[2 * q + 1];
+    }
+    std::copy(pts + 2 * (n - 2), pts + 2 * n, row + 2 * plen);
+    std::fill(row + 2 * (plen + 2), row + 2 * (plen + 16), 0.0f);
+}
+}  // namespace
+
 int mev_add_route_n(mev_handle* h, const float* path_in, int32_t npoints, int32_t intent, int32_t* route) {
     if (!h || !path_in || !route) return fail(MEV_E_INVALID, "null argument");
     if (intent < 0 || intent > 2) return fail(MEV_E_INVALID, "intent must be 0 (straight), 1 (left) or 2 (right)");
-    if (npoints < 2 || npoints > mev::PATH_LEN) return fail(MEV_E_INVALID, "a route path has 2 .. 160 points");
+    if (npoints < 2 || npoints > mev::MAX_PATH_LEN) return fail(MEV_E_INVALID, "a route path has 2 .. 4096 points");
     for (int i = 0; i < 2 * npoints; ++i)
         if (!(fabsf(path_in[i]) < 1.0e6f)) return fail(MEV_E_INVALID, "path points must be finite (|coordinate| < 1e6)");
-    // the table row: the n points, padded with the last one, then the last segment (mev_world.h)
-    float path[2 * mev::ROUTE_PTS] = {};
-    for (int i = 0; i < mev::PATH_LEN; ++i) {
-        const int q = i < npoints ? i : npoints - 1;
-        path[2 * i] = path_in[2 * q];
-        path[2 * i + 1] = path_in[2 * q + 1];
-    }
-    std::copy(path_in + 2 * (npoints - 2), path_in + 2 * npoints, path + 2 * mev::ROUTE_END);
     if (h->nroutes >= 32767) return fail(MEV_E_INVALID, "too many routes (the state gather format ships i16 ids)");
     if (h->comm && h->gather_fmt == MEV_GATHER_STATE)  // every rank's route ids are decoded with the root's table
         return fail(MEV_E_INVALID, "routes cannot be added while a state-format gather communicator exists");
@@ -700,81 +727,101 @@ int mev_add_route_n(mev_handle* h, const float* path_in, int32_t npoints, int32_
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     const int r = h->nroutes;
-    h->h_paths.insert(h->h_paths.end(), path, path + 2 * mev::ROUTE_PTS);
-    h->h_len.push_back(npoints);
-    h->h_intent.push_back(intent);
-    h->h_spawn.push_back(path[0]);  // add_car_with_route's spawn: the path's first point (RouteGen.cpp:111-205)
-    h->h_spawn.push_back(path[1]);
-    h->h_spawn.push_back(mev::spawn_heading(path));
-    {
-        const int cut[4] = {0, 50, 110, mev::PATH_LEN};
+    // a path longer than the rows re-lays the whole table out at the new length (rounded up to
+    // 16 points, rows stay 128-B aligned); every row keeps its own n and its padding.  The
+    // boxes of the other rows stay: their new padding is their last point, which their third
+    // piece [110, old plen) already holds
+    const int plen = npoints > h->plen ? (npoints + 15) & ~15 : h->plen;
+    const int row_pts = plen + 16;
+    const bool relayout = plen != h->plen;
+    std::vector<float> old_paths;
+    if (relayout) {
+        old_paths.swap(h->h_paths);
+        h->h_paths.resize(size_t(r) * 2 * size_t(row_pts));
+        for (int q = 0; q < r; ++q)
+            fill_row(&h->h_paths[size_t(q) * 2 * row_pts], &old_paths[size_t(q) * 2 * h->row_pts], h->h_len[size_t(q)],
+                     plen);
+    }
+    h->h_paths.resize(size_t(r + 1) * 2 * size_t(row_pts));
+    float* row = &h->h_paths[size_t(r) * 2 * row_pts];
+    fill_row(row, path_in, npoints, plen);
+    {  // the pieces [0, 50), [50, 110), [110, plen) of the padded row
+        const int cut[4] = {0, 50, 110, plen};
         for (int q = 0; q < 3; ++q) {
-            float x0 = path[2 * cut[q]], x1 = x0, y0 = path[2 * cut[q] + 1], y1 = y0;
+            float x0 = row[2 * cut[q]], x1 = x0, y0 = row[2 * cut[q] + 1], y1 = y0;
             for (int i = cut[q]; i < cut[q + 1]; ++i) {
-                x0 = std::min(x0, path[2 * i]); x1 = std::max(x1, path[2 * i]);
-                y0 = std::min(y0, path[2 * i + 1]); y1 = std::max(y1, path[2 * i + 1]);
+                x0 = std::min(x0, row[2 * i]); x1 = std::max(x1, row[2 * i]);
+                y0 = std::min(y0, row[2 * i + 1]); y1 = std::max(y1, row[2 * i + 1]);
             }
             h->h_pbox.push_back(x0); h->h_pbox.push_back(x1); h->h_pbox.push_back(y0); h->h_pbox.push_back(y1);
         }
     }
-    // the four route tables: the new route's rows go into spare capacity; a full table is
-    // reallocated at twice the routes (so n added routes cost O(log n) reallocations, each a
-    // hipFree that waits for the device) and uploaded whole
-    const size_t per[4] = {2 * mev::ROUTE_PTS * sizeof(float), sizeof(int32_t), 3 * sizeof(float), 12 * sizeof(float)};
-    const void* src[4] = {h->h_paths.data(), h->h_intent.data(), h->h_spawn.data(), h->h_pbox.data()};
-    if (r < h->route_cap) {
-        void* cur[4] = {h->d_paths, h->d_intent, h->d_spawn_tab, h->d_pbox};
-        hipError_t e = hipSuccess;
-        for (int k = 0; k < 4 && e == hipSuccess; ++k)
-            e = hipMemcpy(static_cast<uint8_t*>(cur[k]) + size_t(r) * per[k],
-                          static_cast<const uint8_t*>(src[k]) + size_t(r) * per[k], per[k], hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            h->h_paths.resize(h->h_paths.size() - 2 * mev::ROUTE_PTS);
-            h->h_len.pop_back();
-            h->h_intent.pop_back();
-            h->h_spawn.resize(h->h_spawn.size() - 3);
-            h->h_pbox.resize(h->h_pbox.size() - 12);
-            return fail(MEV_E_HIP, std::string("route table: ") + hipGetErrorString(e));
-        }
-        h->nroutes = r + 1;
-        h->extend_route_hash();
-        h->sp.rt.nroutes = h->nroutes;
-        *route = r;
-        return MEV_OK;
-    }
-    const int cap = std::min(32767, std::max(2 * h->route_cap, r + 1));
-    hipError_t e = hipSuccess;
-    void* np[4] = {nullptr, nullptr, nullptr, nullptr};
-    for (int k = 0; k < 4 && e == hipSuccess; ++k) {
-        e = hipMalloc(&np[k], size_t(cap) * per[k]);
-        if (e == hipSuccess) e = hipMemcpy(np[k], src[k], size_t(r + 1) * per[k], hipMemcpyHostToDevice);
-    }
-    if (e != hipSuccess) {
-        for (void* q : np) if (q) (void)hipFree(q);
-        h->h_paths.resize(h->h_paths.size() - 2 * mev::ROUTE_PTS);
+    h->h_len.push_back(npoints);
+    h->h_intent.push_back(intent);
+    h->h_spawn.push_back(row[0]);  // add_car_with_route's spawn: the path's first point (RouteGen.cpp:111-205)
+    h->h_spawn.push_back(row[1]);
+    h->h_spawn.push_back(mev::spawn_heading(row));
+    auto rollback = [&]() {
+        if (relayout) h->h_paths.swap(old_paths);
+        else h->h_paths.resize(size_t(r) * 2 * size_t(row_pts));
         h->h_len.pop_back();
         h->h_intent.pop_back();
         h->h_spawn.resize(h->h_spawn.size() - 3);
         h->h_pbox.resize(h->h_pbox.size() - 12);
-        return fail(MEV_E_NOMEM, std::string("route table: ") + hipGetErrorString(e));
+    };
+    // the five route tables: the new route's rows go into spare capacity; a full table (or a
+    // re-laid-out one) is reallocated at twice the routes (so n added routes cost O(log n)
+    // reallocations, each a hipFree that waits for the device) and uploaded whole
+    const size_t per[5] = {2 * size_t(row_pts) * sizeof(float), sizeof(int32_t), 3 * sizeof(float), 12 * sizeof(float),
+                           sizeof(int32_t)};
+    const void* src[5] = {h->h_paths.data(), h->h_intent.data(), h->h_spawn.data(), h->h_pbox.data(), h->h_len.data()};
+    const int cap = r >= h->route_cap ? std::min(32767, std::max(2 * h->route_cap, r + 1)) : h->route_cap;
+    hipError_t e = hipSuccess;
+    if (cap == h->route_cap && !relayout) {
+        void* cur[5] = {h->d_paths, h->d_intent, h->d_spawn_tab, h->d_pbox, h->d_rlen};
+        for (int k = 0; k < 5 && e == hipSuccess; ++k)
+            e = hipMemcpy(static_cast<uint8_t*>(cur[k]) + size_t(r) * per[k],
+                          static_cast<const uint8_t*>(src[k]) + size_t(r) * per[k], per[k], hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            rollback();
+            return fail(MEV_E_HIP, std::string("route table: ") + hipGetErrorString(e));
+        }
+    } else {
+        void* np[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+        for (int k = 0; k < 5 && e == hipSuccess; ++k) {
+            e = hipMalloc(&np[k], size_t(cap) * per[k]);
+            if (e == hipSuccess) e = hipMemcpy(np[k], src[k], size_t(r + 1) * per[k], hipMemcpyHostToDevice);
+        }
+        if (e != hipSuccess) {
+            for (void* q : np) if (q) (void)hipFree(q);
+            rollback();
+            return fail(MEV_E_NOMEM, std::string("route table: ") + hipGetErrorString(e));
+        }
+        void* old[5] = {h->d_paths, h->d_intent, h->d_spawn_tab, h->d_pbox, h->d_rlen};
+        for (int k = 0; k < 5; ++k) {
+            for (auto& a : h->allocs)
+                if (a == old[k]) { (void)hipFree(a); a = np[k]; break; }
+        }
+        h->d_paths = static_cast<float*>(np[0]);
+        h->d_intent = static_cast<int32_t*>(np[1]);
+        h->d_spawn_tab = static_cast<float*>(np[2]);
+        h->d_pbox = static_cast<float*>(np[3]);
+        h->d_rlen = static_cast<int32_t*>(np[4]);
+        h->route_cap = cap;
     }
-    void* old[4] = {h->d_paths, h->d_intent, h->d_spawn_tab, h->d_pbox};
-    for (int k = 0; k < 4; ++k) {
-        for (auto& a : h->allocs)
-            if (a == old[k]) { (void)hipFree(a); a = np[k]; break; }
-    }
-    h->d_paths = static_cast<float*>(np[0]);
-    h->d_intent = static_cast<int32_t*>(np[1]);
-    h->d_spawn_tab = static_cast<float*>(np[2]);
-    h->d_pbox = static_cast<float*>(np[3]);
-    h->route_cap = cap;
+    h->plen = plen;
+    h->row_pts = row_pts;
     h->nroutes = r + 1;
     h->extend_route_hash();
     h->sp.rt.path = h->d_paths;
     h->sp.rt.intent = h->d_intent;
     h->sp.rt.spawn = h->d_spawn_tab;
     h->sp.rt.pbox = reinterpret_cast<const float4*>(h->d_pbox);
+    h->sp.rt.len = h->d_rlen;
     h->sp.rt.nroutes = h->nroutes;  // (the next launch refreshes the device copy of the parameters)
+    h->sp.rt.plen = plen;
+    h->sp.rt.row = row_pts;
+    h->sp.rt.min_len = std::min(h->sp.rt.min_len, int32_t(npoints));
     *route = r;
     return MEV_OK;
 }

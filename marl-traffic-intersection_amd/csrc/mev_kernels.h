@@ -41,14 +41,18 @@ struct NpcSoA {
 enum NpcField { NF_X, NF_Y, NF_V, NF_H, NF_ACC, NF_STEER, NF_PIDX, NF_ROUTE, NF_INTENT, NF_COUNT };
 
 struct RouteTab {
-    const float* path;      // [nroutes][160][2]
+    const float* path;      // [nroutes][row][2]: plen points, the last segment, zeros (mev_world.h)
     const int32_t* intent;  // [nroutes]
     const float* spawn;     // [nroutes][3]  x, y, heading
     // [nroutes][3] bounding boxes (min x, max x, min y, max y) of each route's three
-    // pieces -- points [0, 50), [50, 110), [110, 160) (RouteGen.cpp:160-237) -- for
+    // pieces -- points [0, 50), [50, 110), [110, plen) (RouteGen.cpp:160-237) -- for
     // the NPC ghost scan's prefilter
     const float4* pbox;
+    const int32_t* len;     // [nroutes] each path's own length (Car.path.size())
     int32_t nroutes;
+    int32_t plen;           // points per path in the rows (PATH_LEN, or the longest path rounded up to 16)
+    int32_t row;            // points per row (plen + 16; ROUTE_PTS for plen = PATH_LEN)
+    int32_t min_len;        // the shortest path's length (an index below it is inside every path)
 };
 
 struct Outputs {

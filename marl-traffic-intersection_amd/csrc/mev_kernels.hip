@@ -269,23 +269,6 @@ __device__ inline float march_dist(const SimParams& p, int k) {
     else return (float)k * p.lidar_step;
 }
 
-// Car::update_path_index (cpp/Car.cpp:47-74): argmin of squared distance over
-// path[idx, idx+50) — one window point per lane, strict '<' => first minimum wins.
-__device__ inline int path_index_update(const float* path, int idx, float x, float y, int lane) {
-    int start_i = idx < 0 ? 0 : idx;
-    int end_i = start_i + 50;
-    if (end_i > PATH_LEN) end_i = PATH_LEN;
-    const int i = start_i + lane;
-    float d = __builtin_inff();
-    if (lane < 50 && i < end_i) {
-        const float dx = path[2 * i] - x;
-        const float dy = path[2 * i + 1] - y;
-        d = dx * dx + dy * dy;
-    }
-    const int best = wave_argmin_first(d, (lane < 50 && i < end_i) ? i : 0x7fffffff);
-    return best == 0x7fffffff ? start_i : best;
-}
-
 // XCD-aware env order: the dispatcher deals workgroups round-robin over the 8
 // XCDs (block b -> XCD b % 8), and each XCD has its own L2.  An env's SoA
 // slices are 4 B x N per field (32 B at N = 8), so four consecutive envs share
@@ -540,18 +523,31 @@ __device__ __forceinline__ NpcPair npc_pair(int k, float x, float y, float h, fl
     return r;
 }
 
+// The ghost scan's end min(g0 + 120, path.size()) (TrafficFlow.cpp:88-89).  A row holds
+// plen points, a shorter path padded with its last point, which repeats that point's
+// verdict: so plen serves while g0 lies inside the path.  Past a path's end (an index
+// written through set_state; the window searches keep it there) the reference's scan is
+// empty.  Only an index at or beyond the table's shortest path can be there (one compare
+// on every other).
+__device__ __forceinline__ int npc_scan_end(const SimParams& p, int route, int g0) {
+    int g1 = g0 + 120 < p.rt.plen ? g0 + 120 : p.rt.plen;
+    if (__builtin_expect(g0 >= p.rt.min_len, 0)) {
+        if (g0 >= gmem(p.rt.len)[route]) g1 = g0;
+    }
+    return g1;
+}
+
 // The ghost path scan of NPC k (:157-188) with its path points path[idx0 + lane]
 // (ga) and path[idx0 + 64 + lane] (gb): the first point, in path order, within
 // SAFE of an other in em (k's filtered others; lane o holds other o's position)
 // that k yields to there (ym, or the point is within 15 of k) is the conflict;
 // its distance to k is the minimum (:183-188).  Returns the conflict distance,
 // or -1 without a conflict.
-__device__ __forceinline__ float npc_ghost_scan(int g_start, float x, float y, float2 ga, float2 gb,
+__device__ __forceinline__ float npc_ghost_scan(int g_start, int g_end, float x, float y, float2 ga, float2 gb,
                                                 unsigned long long em, unsigned long long ym, float oxj, float oyj,
                                                 int lane) {
     const float SAFE = CAR_WIDTH * 2.0f;
     const float SAFE_SQ = SAFE * SAFE;
-    const int g_end = g_start + 120 < PATH_LEN ? g_start + 120 : PATH_LEN;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
         if (g_start + c * WAVE >= g_end) break;
@@ -611,6 +607,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // per-NPC sizes (Car::length / width in the SAT and the LiDAR boxes): kernels that can
     // run a handle with cars of other sizes keep them (every entry is 54 x 24 unless p.dims)
     constexpr bool dims = NL::kDims;
+    const int plen = p.rt.plen;
 #ifdef MEV_STAMPS_N
     unsigned long long nt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long nt_prev = __builtin_amdgcn_s_memtime();
@@ -704,13 +701,13 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // each, 8 window points per lane, first minimum wins); returns the new index
     // and leaves the 64-point window in pt
     auto npc_window = [&](int kk, int idx, float x, float y, float2* pt, int& start_i) -> int {
-        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * ROUTE_PTS));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * p.rt.row));
         start_i = idx < 0 ? 0 : idx;
-        const int wcnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
+        const int wcnt = (start_i + 50 > plen) ? plen - start_i : 50;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int q = start_i + sub * 8 + j;
-            pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+            pt[j] = P[q < plen ? q : plen - 1];
         }
         float bd = __builtin_inff();
         int bi = 0x7fffffff;
@@ -743,9 +740,10 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         float2 pt[8];
         int start_i;
         const int pidx0 = npc_window(kk, nl.pidx[kk], x, y, pt, start_i);
-        // the look-ahead point min(pidx0 + 12, 159) lies in the 64-point window
-        const int tidx = pidx0 + 12 < PATH_LEN - 1 ? pidx0 + 12 : PATH_LEN - 1;
-        const int toff = tidx - start_i;
+        // the look-ahead point min(pidx0 + 12, plen - 1) lies in the 64-point window; an index
+        // at or past the row's end (a written one) has a window of copies of path.back()
+        const int tidx = pidx0 + 12 < plen - 1 ? pidx0 + 12 : plen - 1;
+        const int toff = tidx < start_i ? 0 : tidx - start_i;
         if (act && sub == (toff >> 3)) {
             float2 t = pt[0];
 #pragma unroll
@@ -766,7 +764,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             nl.pidx0[k] = pidx0;
         }
         if (act && sub == 7) {  // the route's end point, for the arrival test after the turns
-            const float2 pe = gf2(p.rt.path + (size_t)nl.route[k] * (2 * ROUTE_PTS))[PATH_LEN - 1];
+            const float2 pe = gf2(p.rt.path + (size_t)nl.route[k] * (2 * p.rt.row))[plen - 1];
             nl.endx[k] = pe.x;
             nl.endy[k] = pe.y;
         }
@@ -794,21 +792,21 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
         else __builtin_amdgcn_s_setprio(0);
     }
     // NPC kk's ghost points path[idx0 + lane] and path[idx0 + 64 + lane] (clamped;
-    // only indices below min(idx0 + 120, 160) are used)
+    // only indices below min(idx0 + 120, plen) are used)
     auto fetch_ghost = [&](int kk, float2& a, float2& b) {
-        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * ROUTE_PTS));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * p.rt.row));
         const int i0 = nl.pidx0[kk] + lane, i1 = i0 + WAVE;
-        a = P[i0 < PATH_LEN ? i0 : PATH_LEN - 1];
-        b = P[i1 < PATH_LEN ? i1 : PATH_LEN - 1];
+        a = P[i0 < plen ? i0 : plen - 1];
+        b = P[i1 < plen ? i1 : plen - 1];
     };
     // the ghost points of NPC kk in the scan layout: lane t of its 16 holds
     // path[idx0 + 8t .. idx0 + 8t + 7] (clamped; only indices below min(idx0 + 120,
-    // 160) are used)
+    // plen) are used)
     auto load_ghost8 = [&](int kk, float2* gp) {
-        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * ROUTE_PTS));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * p.rt.row));
         const int q0 = nl.pidx0[kk] + 8 * (lane & 15);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) gp[i] = P[q0 + i < PATH_LEN ? q0 + i : PATH_LEN - 1];
+        for (int i = 0; i < 8; ++i) gp[i] = P[q0 + i < plen ? q0 + i : plen - 1];
     };
     // plan every alive NPC (mixed: round B) into thr.  Lane = (NPC k of the chunk,
     // other j) over Kp = 8 / 16 / 32 / 64 others.  Then the ghost scans, four NPCs
@@ -846,15 +844,15 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             // scan window overlaps never hits, and leaves the scan's candidates
             bool reach = false;
             if (pr.pok) {
-                const int g0 = nl.pidx0[kk], g1 = g0 + 120 < PATH_LEN ? g0 + 120 : PATH_LEN;
+                const int g0 = nl.pidx0[kk], g1 = npc_scan_end(p, nl.route[kk], g0);
                 const float R2 = (CAR_WIDTH * 2.0f + 0.01f) * (CAR_WIDTH * 2.0f + 0.01f);
                 auto near_box = [&](float4 b) {
                     const float dx = fmaxf(fmaxf(b.x - oxj, oxj - b.y), 0.0f);
                     const float dy = fmaxf(fmaxf(b.z - oyj, oyj - b.w), 0.0f);
                     return dx * dx + dy * dy < R2;
                 };
-                reach = (g0 < 50 && near_box(pb0)) || (g0 < 110 && g1 > 50 && near_box(pb1)) ||
-                        (g1 > 110 && near_box(pb2));
+                reach = g0 < g1 && ((g0 < 50 && near_box(pb0)) || (g0 < 110 && g1 > 50 && near_box(pb1)) ||
+                                    (g1 > 110 && near_box(pb2)));
             }
             const unsigned long long b30 = ballot(pr.f30), b50 = ballot(pr.f50);
             const unsigned long long bok = ballot(reach), byf = ballot(pr.yfar);
@@ -914,7 +912,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             const int k = lane_npc(ks);
             const bool act = u < nb;
             const int g_start = nl.pidx0[k];
-            const int g_end = g_start + 120 < PATH_LEN ? g_start + 120 : PATH_LEN;
+            const int g_end = npc_scan_end(p, nl.route[k], g_start);
             const int q0 = g_start + 8 * (lane & 15);
             const float x = nl.x[k], y = nl.y[k];
             const unsigned long long em = act ? nl.em[k] : 0ull, ym = nl.ym[k];
@@ -986,12 +984,12 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     // and the second update_path_index (:343) over path[idx0, idx0 + 50), 8 lanes
     // per NPC (7 window points each, first minimum wins)
     auto load_window = [&](int kk, float2* w) {
-        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * ROUTE_PTS));
+        const GF2 P = gf2(p.rt.path + (size_t)nl.route[kk] * (2 * p.rt.row));
         const int pidx0 = nl.pidx0[kk];
 #pragma unroll
         for (int t = 0; t < 7; ++t) {
             const int q = pidx0 + sub * 7 + t;
-            w[t] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+            w[t] = P[q < plen ? q : plen - 1];
         }
     };
     auto move_all = [&](const float* thr, unsigned long long which) {
@@ -1010,7 +1008,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
 #pragma unroll
             for (int t = 0; t < 7; ++t) {
                 const int off = sub * 7 + t;
-                if (off < 50 && pidx0 + off < PATH_LEN) {
+                if (off < 50 && pidx0 + off < plen) {
                     const float wdx = w[t].x - kin.x, wdy = w[t].y - kin.y;
                     const float d = wdx * wdx + wdy * wdy;
                     if (d < bd) { bd = d; bi = pidx0 + off; }
@@ -1084,7 +1082,9 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             if (ballot(pr.f30)) acc_thr = -1.0f;
             else if (ballot(pr.f50)) acc_thr = (-0.2f < acc_thr) ? -0.2f : acc_thr;
             const unsigned long long em = ballot(pr.pok), ym = ballot(pr.yfar);
-            const float mc = em ? npc_ghost_scan(nl.pidx0[k], x, y, ga, gb, em, ym, oxj, oyj, lane) : -1.0f;
+            const float mc = em ? npc_ghost_scan(nl.pidx0[k], npc_scan_end(p, nl.route[k], nl.pidx0[k]), x, y, ga, gb,
+                                                 em, ym, oxj, oyj, lane)
+                                : -1.0f;
             const float thr = npc_throttle(acc_thr, mc);
             Kin kin{x, y, v, h, nl.acc[k], nl.steer[k]};
             float cn, sn;
@@ -1092,7 +1092,7 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
             // the second update_path_index (:343) over path[idx0, idx0 + 50): lane i holds
             // path[idx0 + i] among the ghost points; no later turn reads it
             const int pidx0 = nl.pidx0[k];
-            const bool wv = lane < 50 && pidx0 + lane < PATH_LEN;
+            const bool wv = lane < 50 && pidx0 + lane < plen;
             const float wdx = ga.x - kin.x, wdy = ga.y - kin.y;
             const int best = wave_argmin_dpp(wv ? wdx * wdx + wdy * wdy : __builtin_inff(),
                                              wv ? pidx0 + lane : 0x7fffffff);
@@ -1273,7 +1273,7 @@ template <bool TRAFFIC, class EL, class NL>
 __device__ __forceinline__ bool write_obs_head(const SimParams& p, int i, const EL& el, const NL* nl, int ncnt,
                                const float* path, int pidx, float* row, float* dlim) {
     int tidx = pidx + 10;
-    if (tidx > PATH_LEN - 1) tidx = PATH_LEN - 1;
+    if (tidx > p.rt.plen - 1) tidx = p.rt.plen - 1;
     return write_obs_head_tg<TRAFFIC>(p, i, el, nl, ncnt, path[2 * tidx], path[2 * tidx + 1], row, true, dlim);
 }
 
@@ -1560,10 +1560,11 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
                                            const Kin& gk, const uint8_t galive_b, const float ga0, const float ga1) {
     constexpr bool early = EARLY;
     constexpr bool dims = DIMS;
-    const GF2 P = gf2(p.rt.path + (size_t)(early ? eroute : el.route[ii]) * (2 * ROUTE_PTS));
+    const int plen = p.rt.plen;
+    const GF2 P = gf2(p.rt.path + (size_t)(early ? eroute : el.route[ii]) * (2 * p.rt.row));
     const int pidx0 = early ? epidx : el.pidx[ii];
     const int start_i = pidx0 < 0 ? 0 : pidx0;
-    const int cnt = (start_i + 50 > PATH_LEN) ? PATH_LEN - start_i : 50;
+    const int cnt = (start_i + 50 > plen) ? plen - start_i : 50;
     // the window's first point: start_i, or (early: the LDS window of round B)
     // start_i rounded down to even; the 50-point window and the look-ahead target
     // lie in [w0, w0 + 64): 8 points per lane
@@ -1574,9 +1575,9 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int q = start_i + sub * 8 + j;
-            pt[j] = P[q < PATH_LEN ? q : PATH_LEN - 1];
+            pt[j] = P[q < plen ? q : plen - 1];
         }
-        pend = P[ROUTE_END + 1]; pprev = P[ROUTE_END]; p10 = P[10];  // the row's last segment (mev_world.h)
+        pend = P[plen + 1]; pprev = P[plen]; p10 = P[10];  // the row's last segment (mev_world.h)
     }
     Kin k = early ? gk : Kin{el.x[ii], el.y[ii], el.v[ii], el.h[ii], el.acc[ii], el.steer[ii]};
     const bool alive = act && (early ? galive_b : el.alive[ii]) != 0;
@@ -1599,7 +1600,7 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
             pt[2 * m] = make_float2(q.x, q.y);
             pt[2 * m + 1] = make_float2(q.z, q.w);
         }
-        // lane (grp, 0): the row's last segment (points 160, 161); lane (grp, 1): points 10, 11
+        // lane (grp, 0): the row's last segment (points plen, plen + 1); lane (grp, 1): points 10, 11
         const float4* wx = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(el.win) + 4096 + grp * 128);
         const float4 ends = wx[0], ten = wx[1];
         pprev = make_float2(ends.x, ends.y);
@@ -1629,7 +1630,7 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
     const int pidx = alive ? (bi == 0x7fffffff ? start_i : bi) : pidx0;
     // look-ahead point of the observation (:444-452), picked from the window
     {
-        const int tidx = pidx + 10 < PATH_LEN - 1 ? pidx + 10 : PATH_LEN - 1;
+        const int tidx = pidx + 10 < plen - 1 ? pidx + 10 : plen - 1;
         const int toff = tidx - w0;
         if (act && toff >= 0 && toff < 64 && sub == (toff >> 3)) {
             float2 t = pt[0];
@@ -1897,7 +1898,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // lane (grp, sub) loads chunks 4 sub .. 4 sub + 3 (instruction m: chunk 4 sub +
     // m at win + m KB + grp * 128 + sub * 16) and reads back exactly those, so each
     // lane's 8 points arrive as 4 aligned 16-B LDS reads.  A fifth instruction brings
-    // the route row's last segment (points 160, 161: lane sub 0) and path[10, 11] (sub 1).
+    // the route row's last segment (points plen, plen + 1: lane sub 0) and path[10, 11] (sub 1).
     // Chunks past the path's end are clamped to its last one: those points lie
     // beyond every window's range and are never used.
     int eroute = 0, epidx = 0;
@@ -1912,18 +1913,18 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
         }
         const int start_i = epidx < 0 ? 0 : epidx;
         const int sub = tid & 7;
-        const uint32_t rbase = (uint32_t)eroute * (2 * ROUTE_PTS * 4);  // bytes
+        const uint32_t rbase = (uint32_t)eroute * (uint32_t)(2 * 4 * p.rt.row);  // bytes
         typedef const __attribute__((address_space(1))) char gchar;
         gchar* path_b = (gchar*)gmem(p.rt.path);
         __attribute__((address_space(3))) char* win = (__attribute__((address_space(3))) char*)el.win;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             int c = (start_i >> 1) + sub * 4 + m;
-            c = c < PATH_LEN / 2 ? c : PATH_LEN / 2 - 1;
+            c = c < (p.rt.plen >> 1) ? c : (p.rt.plen >> 1) - 1;
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(path_b + rbase + c * 16),
                                              (__attribute__((address_space(3))) void*)(win + m * 1024), 16, 0, 0);
         }
-        const int cx = sub == 0 ? ROUTE_END / 2 : 5;  // points 160, 161 (last segment) / 10, 11
+        const int cx = sub == 0 ? p.rt.plen >> 1 : 5;  // points plen, plen + 1 (last segment) / 10, 11
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(path_b + rbase + cx * 16),
                                          (__attribute__((address_space(3))) void*)(win + 4 * 1024), 16, 0, 0);
     }
@@ -3543,7 +3544,7 @@ __global__ __launch_bounds__(WAVE) void k_reset(SimParams p, const uint8_t* mask
             for (int c = 0; c < p.D; ++c) row[c] = 0.0f;
             continue;
         }
-        const float* path = p.rt.path + (size_t)egoi(p, EF_ROUTE)[g] * (2 * ROUTE_PTS);
+        const float* path = p.rt.path + (size_t)egoi(p, EF_ROUTE)[g] * (2 * p.rt.row);
         exact = write_obs_head<TRAFFIC>(p, i, el, nl, ncnt, path, el.pidx[i], row, &dl);
         for (int b = 0; b < p.lidar_slots; ++b) row[OBS_HEAD + b] = p.lidar_max * p.lidar_inv;
     }
@@ -3859,8 +3860,8 @@ __global__ __launch_bounds__(WAVE) void k_decode_state(SimParams p, const uint8_
         const bool bad = route < 0 || route >= p.rt.nroutes;
         if (bad) atomicAdd(p.overflow + 2, 1ull);
         const int rt = bad ? 0 : route;
-        const int ti = pidx + 10 < PATH_LEN - 1 ? (pidx + 10 < 0 ? 0 : pidx + 10) : PATH_LEN - 1;
-        const float* path = p.rt.path + (size_t)rt * (2 * ROUTE_PTS);
+        const int ti = pidx + 10 < p.rt.plen - 1 ? (pidx + 10 < 0 ? 0 : pidx + 10) : p.rt.plen - 1;
+        const float* path = p.rt.path + (size_t)rt * (2 * p.rt.row);
         const float nan = __builtin_nanf("");
         exact = write_obs_head_tg<false>(p, i, el, (const NpcLDST<MAXK>*)nullptr, 0, bad ? nan : path[2 * ti],
                                          bad ? nan : path[2 * ti + 1], row, false, &dl);

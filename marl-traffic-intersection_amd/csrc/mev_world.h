@@ -32,8 +32,11 @@ constexpr int PATH_LEN = 160;  // 50 + 60 + 50 points (cpp/RouteGen.cpp:160-237)
 // the look-ahead targets clamped to n-1 (IntersectionEnv.cpp:446, TrafficFlow.cpp:55),
 // the ghost scan (TrafficFlow.cpp:89-185: a repeated point repeats its verdict),
 // path.back() -- then reads exactly what the n-point path gives.
+// (A table with a written path longer than PATH_LEN has rows of plen = that length rounded
+// up to 16 points and plen + 16 points per row, the last segment at plen: RouteTab.)
 constexpr int ROUTE_END = PATH_LEN;
 constexpr int ROUTE_PTS = 176;
+constexpr int MAX_PATH_LEN = 4096;  // mev_add_route_n's bound on a written path
 constexpr int OBS_HEAD = 6 + 5 * NEIGHBOR_COUNT;  // 31
 
 enum Status : uint8_t { ST_ALIVE = 0, ST_DEAD = 1, ST_SUCCESS = 2, ST_CRASH_WALL = 3, ST_CRASH_LINE = 4, ST_CRASH_CAR = 5 };

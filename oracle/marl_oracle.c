@@ -37,7 +37,8 @@
 #define PHYSICS_MAX_SPEED 8.0f
 #define PI_F 3.14159265358979323846f
 #define NEIGHBORS 5 /* cpp/IntersectionEnv.h:19 */
-#define PATH_LEN 160
+#define PATH_LEN 160      /* every lane-layout route (RouteGen.cpp:160-237) */
+#define MAX_PATH_LEN 4096 /* orc_add_route's bound (the device's, mev_world.h MAX_PATH_LEN) */
 #define MAXCARS 256
 
 enum { ST_ALIVE = 0, ST_DEAD = 1, ST_SUCCESS = 2, ST_CRASH_WALL = 3, ST_CRASH_LINE = 4, ST_CRASH_CAR = 5 };
@@ -59,7 +60,9 @@ typedef struct orc_env {
     float rc[8];
     int P;               /* 8 * lanes lane points */
     lane_pt* pts;
-    float* paths;        /* [nroutes][160][2]: the P*P lane-layout routes, then orc_add_route's */
+    float* paths;        /* the P*P lane-layout routes ([160][2] each), then orc_add_route's ([n][2] each) */
+    size_t* poff;        /* [nroutes]: float offset of each route's path in paths */
+    size_t pfloats;      /* floats used in paths */
     int* intent;         /* [nroutes] */
     int* plen;           /* [nroutes]: points of each path (Car.path.size(); 160 for the lane routes) */
     int nroutes;
@@ -246,7 +249,7 @@ static int yellow(const orc_env* e, float x, float y) {
 }
 
 /* ------------------------------------------------------------------ cars */
-static const float* path_of(const orc_env* e, const orc_car* c) { return e->paths + (size_t)c->route * 2 * PATH_LEN; }
+static const float* path_of(const orc_env* e, const orc_car* c) { return e->paths + e->poff[c->route]; }
 static int len_of(const orc_env* e, const orc_car* c) { return e->plen[c->route]; } /* path.size() */
 
 /* Car::update, cpp/Car.cpp:9-40 */
@@ -482,7 +485,7 @@ static void plan_npc(const orc_env* e, int k, float* thr_out, float* st_out) {
 static void spawn_npc(orc_env* e, int troute) {
     if (troute < 0 || troute >= e->ntr) return;
     int rid = e->troutes[troute];
-    const float* p = e->paths + (size_t)rid * 2 * PATH_LEN;
+    const float* p = e->paths + e->poff[rid];
     /* the route's start lane point; a route of the caller's own (orc_add_route) starts at its first point */
     float sx = rid < e->P * e->P ? e->pts[rid / e->P].x : p[0], sy = rid < e->P * e->P ? e->pts[rid / e->P].y : p[1];
     const float md = CAR_LENGTH * 2.5f, md2 = md * md;
@@ -738,7 +741,9 @@ orc_env* orc_create(int lanes, int n, int rays, float fov, float maxd, float ste
     e->paths = (float*)calloc((size_t)e->P * e->P * 2 * PATH_LEN, sizeof(float));
     e->intent = (int*)calloc((size_t)e->P * e->P, sizeof(int));
     e->plen = (int*)calloc((size_t)e->P * e->P, sizeof(int));
-    for (int r = 0; r < e->P * e->P; ++r) e->plen[r] = PATH_LEN;
+    e->poff = (size_t*)calloc((size_t)e->P * e->P, sizeof(size_t));
+    for (int r = 0; r < e->P * e->P; ++r) { e->plen[r] = PATH_LEN; e->poff[r] = (size_t)r * 2 * PATH_LEN; }
+    e->pfloats = (size_t)e->P * e->P * 2 * PATH_LEN;
     for (int s = 0; s < e->P; ++s)
         for (int t = 0; t < e->P; ++t) {
             int r = s * e->P + t;
@@ -763,36 +768,40 @@ orc_env* orc_create(int lanes, int n, int rays, float fov, float maxd, float ste
 
 void orc_destroy(orc_env* e) {
     if (!e) return;
-    free(e->pts); free(e->paths); free(e->intent); free(e->plen); free(e->rel); free(e->line_grid); free(e->troutes); free(e->lidar);
+    free(e->pts); free(e->paths); free(e->intent); free(e->plen); free(e->poff); free(e->rel); free(e->line_grid); free(e->troutes); free(e->lidar);
     free(e);
 }
 
 int orc_route_id(const orc_env* e, int s, int t) { return s * e->P + t; }
 int orc_num_points(const orc_env* e) { return e->P; }
+int orc_route_len(const orc_env* e, int r) { return e->plen[r]; }
 
 void orc_route_path(const orc_env* e, int r, float* out, int* intent) {
-    memcpy(out, e->paths + (size_t)r * 2 * PATH_LEN, sizeof(float) * 2 * PATH_LEN);
+    memcpy(out, e->paths + e->poff[r], sizeof(float) * 2 * (size_t)e->plen[r]);
     *intent = e->intent[r];
 }
 
 /* A route of the caller's own (the reference's Car.path is a plain read-write
  * vector, cpp/Car.h:26, cpp/bindings.cpp:29; every function above reads a car's
- * path through path_of, bounded by its size, len_of): n points (2 <= n <= 160)
+ * path through path_of, bounded by its size, len_of): n points (2 <= n <= MAX_PATH_LEN)
  * appended to the table, returns its id. */
 int orc_add_route(orc_env* e, const float* path, int n, int intent) {
-    if (n < 2 || n > PATH_LEN) return -1;
-    float* np = (float*)realloc(e->paths, (size_t)(e->nroutes + 1) * 2 * PATH_LEN * sizeof(float));
+    if (n < 2 || n > MAX_PATH_LEN) return -1;
+    float* np = (float*)realloc(e->paths, (e->pfloats + 2 * (size_t)n) * sizeof(float));
     if (!np) return -1;
     e->paths = np;
+    size_t* no = (size_t*)realloc(e->poff, (size_t)(e->nroutes + 1) * sizeof(size_t));
+    if (!no) return -1;
+    e->poff = no;
     int* ni = (int*)realloc(e->intent, (size_t)(e->nroutes + 1) * sizeof(int));
     if (!ni) return -1;
     e->intent = ni;
     int* nl = (int*)realloc(e->plen, (size_t)(e->nroutes + 1) * sizeof(int));
     if (!nl) return -1;
     e->plen = nl;
-    float* row = e->paths + (size_t)e->nroutes * 2 * PATH_LEN;
-    memset(row, 0, sizeof(float) * 2 * PATH_LEN);
-    memcpy(row, path, sizeof(float) * 2 * (size_t)n);
+    e->poff[e->nroutes] = e->pfloats;
+    memcpy(e->paths + e->pfloats, path, sizeof(float) * 2 * (size_t)n);
+    e->pfloats += 2 * (size_t)n;
     e->intent[e->nroutes] = intent;
     e->plen[e->nroutes] = n;
     return e->nroutes++;
@@ -813,7 +822,7 @@ void orc_reset(orc_env* e, const int* routes) {
         orc_car* c = &e->ego[i];
         memset(c, 0, sizeof(*c));
         int r = routes[i];
-        const float* p = e->paths + (size_t)r * 2 * PATH_LEN;
+        const float* p = e->paths + e->poff[r];
         c->route = r;
         c->x = e->pts[r / e->P].x; c->y = e->pts[r / e->P].y; c->v = 0.0f;
         c->h = atan2f(-(p[3] - p[1]), p[2] - p[0]);

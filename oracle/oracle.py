@@ -58,6 +58,7 @@ def lib():
         L.orc_set_traffic_routes.argtypes = [vp, vp, i]
         L.orc_set_rel_angles.argtypes = [vp, vp]
         L.orc_add_route.argtypes = [vp, vp, i, i]
+        L.orc_route_len.argtypes = [vp, i]
         L.orc_reset.argtypes = [vp, vp]
         L.orc_set_state.argtypes = [vp, vp, vp, i, i]
         L.orc_get_state.argtypes = [vp, vp, vp, vp, vp]
@@ -102,17 +103,18 @@ class OracleEnv:
         return lib().orc_route_id(self.h, int(s), int(e))
 
     def route_path(self, r):
-        out = np.zeros((160, 2), np.float32)
+        """(path [n, 2], intent) of route r (n = 160 for the lane-layout routes)."""
+        out = np.zeros((lib().orc_route_len(self.h, int(r)), 2), np.float32)
         it = ctypes.c_int()
         lib().orc_route_path(self.h, int(r), out.ctypes.data, ctypes.addressof(it))
         return out, it.value
 
     def add_route(self, path, intent):
-        """A written Car.path of n points, 2 <= n <= 160 (cpp/bindings.cpp:29)."""
+        """A written Car.path of n points, 2 <= n <= 4096 (cpp/bindings.cpp:29)."""
         a = np.ascontiguousarray(path, np.float32).reshape(-1, 2)
         r = lib().orc_add_route(self.h, a.ctypes.data, len(a), int(intent))
         if r < 0:
-            raise ValueError("orc_add_route: 2 .. 160 points")
+            raise ValueError("orc_add_route: 2 .. 4096 points")
         return r
 
     def set_rel_angles(self, rel):

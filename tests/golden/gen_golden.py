@@ -62,7 +62,7 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
         traffic=False, density=0.5, lanes=3, ego_routes=None, reward=None, steps=200,
         act="random", seed=0, dt=1.0 / 60.0, act_scale=1.0, zero_throttle_p=0.0,
         inject=None, notes="", warmup=0, roundtrip=False, custom_paths=None, ego_paths=None, car_lidars=None):
-    """custom_paths: C paths of the caller's own, [n][2] each, 2 <= n <= 160 (Car.path writes;
+    """custom_paths: C paths of the caller's own, [n][2] each, 2 <= n <= 4096 (Car.path writes;
     recorded padded with their last point, their lengths in custom_len); ego_paths: per ego
     the custom path written into its Car.path, or -1 (NPCs on custom path k, injected by
     `inject`, record route 1000 + k).  car_lidars: per ego None (add_car_with_route's own
@@ -164,7 +164,8 @@ def run(name: str, *, n_agents: int, rays=96, use_team=False, respawn=True, max_
     if rays > 96:
         arrays["lidar"] = np.asarray(LD, np.float32)
     if cps:
-        arrays["custom_paths"] = np.stack([np.concatenate([c, np.repeat(c[-1:], 160 - len(c), 0)])
+        m = max([160] + [len(c) for c in cps])
+        arrays["custom_paths"] = np.stack([np.concatenate([c, np.repeat(c[-1:], m - len(c), 0)])
                                            for c in cps]).astype(np.float32)
         if any(len(c) != 160 for c in cps):
             arrays["custom_len"] = np.array([len(c) for c in cps], np.int32)
@@ -382,6 +383,66 @@ def gen_paths_short():
         inject=inject_npcs(4, custom=[1, 2, 1, 2]))
 
 
+def resample(p: np.ndarray, n: int) -> np.ndarray:
+    """Polyline p at n points, uniform in the point index (linear interpolation in f64)."""
+    p = np.asarray(p, np.float64)
+    t = np.linspace(0.0, len(p) - 1.0, n)
+    i0 = np.minimum(np.floor(t).astype(int), len(p) - 2)
+    w = (t - i0)[:, None]
+    return (p[i0] * (1.0 - w) + p[i0 + 1] * w).astype(np.float32)
+
+
+def gen_paths_long():
+    """Written Car.path of more than 160 points (every reader bounds by path.size(): the window
+    search Car.cpp:56, the look-ahead IntersectionEnv.cpp:446 / TrafficFlow.cpp:55, the ghost
+    scan TrafficFlow.cpp:89, path.back() and the last segment IntersectionEnv.cpp:16-17,177-182)."""
+    env = R.RefEnv(num_lanes=3, traffic=True, density=0.0, routes=ROUTES3)
+    r = [env.route_path(k) for k in range(12)]
+    env.close()
+    # ego 0: its route at 400 points; ego 2: its route continued straight for 90 more points past
+    # the exit (the goal off screen); ego 3: its route at 1000 points; ego 1 keeps its own route
+    ext = np.concatenate([r[2], r[2][-1] + (r[2][-1] - r[2][-2]) * np.arange(1, 91, dtype=np.float32)[:, None]])
+    run("path_long_egos", n_agents=4, rays=64, use_team=True, steps=300, act="policy", seed=432,
+        custom_paths=[resample(r[0], 400), ext, resample(r[3], 1000)], ego_paths=[0, -1, 1, 2])
+    # traffic: the ego on its route at 320 points, NPCs on traffic routes at 480 and 200 points
+    env = R.RefEnv(num_lanes=3, traffic=True, density=0.0, routes=ROUTES3)
+    p5, n9, n4 = env.route_path(5), env.route_path(9), env.route_path(4)
+    env.close()
+    run("path_long_npc", n_agents=1, rays=64, traffic=True, density=0.0, steps=300, act="policy", seed=433,
+        ego_routes=[ROUTES3[5]], custom_paths=[resample(p5, 320), resample(n9, 480), resample(n4, 200)],
+        ego_paths=[0], inject=inject_npcs(5, custom=[1, 2, 1, 2, -1]))
+
+
+def inject_npcs_past_end(env: R.RefEnv, rng: np.random.Generator):
+    """NPCs in the box whose path_index lies past the end of their Car.path (a plain write of
+    path_index / path, cpp/bindings.cpp:29-30): update_path_index keeps it there (Car.cpp:56,
+    an empty window), the look-ahead clamps to path.back() and the ghost scan is empty
+    (TrafficFlow.cpp:88-89); beside them NPCs on their full routes."""
+    # (traffic route, point of it the NPC stands on, custom path written into Car.path or -1, path_index)
+    spec = [(9, 75, 0, 75), (4, 100, 1, 100), (7, 120, -1, 170), (2, 40, -1, 38), (0, 70, -1, 68),
+            (10, 85, 0, 61), (11, 60, -1, 58)]
+    for route, idx, cj, pidx in spec:
+        path = env.route_path(route)
+        dx, dy = path[idx + 1] - path[idx]
+        f = np.zeros(R.NF, np.float32)
+        f[0], f[1] = path[idx, 0] + rng.normal(0, 1.0), path[idx, 1] + rng.normal(0, 1.0)
+        f[2] = rng.uniform(1, 5)
+        f[3] = math.atan2(-dy, dx) + rng.normal(0, 0.05)
+        f[6], f[7], f[9] = path[0, 0], path[0, 1], math.atan2(-(path[1, 1] - path[0, 1]), path[1, 0] - path[0, 0])
+        f[13], f[14] = 54.0, 24.0
+        assert env.add_npc(route, f, np.array([1, 0, pidx, route], np.int32)) == 0
+        if cj >= 0:
+            env.set_car_path(1, env.k - 1, cj)
+
+
+def gen_paths_past_end():
+    env = R.RefEnv(num_lanes=3, traffic=True, density=0.0, routes=ROUTES3)
+    n9, n4 = env.route_path(9), env.route_path(4)
+    env.close()
+    run("path_past_end_npc", n_agents=1, rays=64, traffic=True, density=0.0, steps=200, act="policy", seed=434,
+        custom_paths=[n9[:60], n4[:90]], ego_paths=[-1], inject=inject_npcs_past_end)
+
+
 def rel_angles(rays: int, fov: float) -> List[float]:
     """Lidar's beam offsets (cpp/Lidar.cpp:4-14, IntersectionEnv.cpp:118-126) in float32."""
     f32 = np.float32
@@ -531,7 +592,8 @@ def _traffic():
 
 
 GROUPS = [("core", _core, True), ("dims", gen_dims, True), ("paths", gen_paths, True), ("lidars", gen_lidars, True),
-          ("paths_short", gen_paths_short, True), ("ties", gen_ties, True),
+          ("paths_short", gen_paths_short, True), ("ties", gen_ties, True), ("paths_long", gen_paths_long, True),
+          ("paths_past_end", gen_paths_past_end, True),
           ("traffic", _traffic, False), ("dims_traffic", gen_dims_traffic, False),
           ("paths_traffic", gen_paths_traffic, False)]
 

@@ -80,7 +80,7 @@ def test_add_route_validates_and_extends_the_id_range(mev):
         h.add_route(bad, 0)
     with pytest.raises(mev.MevError):
         h.add_route(path, 3)
-    for n in (0, 1, 161):  # 2 .. 160 points (the Python layer refuses, and the C ABI)
+    for n in (0, 1, 4097):  # 2 .. 4096 points (the Python layer refuses, and the C ABI)
         with pytest.raises(ValueError):
             h.add_route(np.resize(path, (n, 2)), 0)
         raw = np.resize(path, (max(n, 1), 2))

@@ -288,7 +288,7 @@ def test_cpp_backend_cars_setter_and_written_path():
     other.set_state(snap)
     assert G.bits_equal(np.asarray(other.cars[1].path, np.float32), new_path)
     c0 = other.cars[0].path
-    for bad in (c0[:1], c0 + c0[-1:]):  # 1 and 161 points (2 .. 160 are taken)
+    for bad in (c0[:1], c0 * 26):  # 1 and 4160 points (2 .. 4096 are taken)
         with pytest.raises(ValueError):
             c = other.cars
             c[0].path = bad
@@ -297,7 +297,8 @@ def test_cpp_backend_cars_setter_and_written_path():
         env.close()
 
 
-@pytest.mark.parametrize("name", ["dims_cfg3_policy", "dims_respawn_off", "path_bent_egos", "path_short_egos"])
+@pytest.mark.parametrize("name", ["dims_cfg3_policy", "dims_respawn_off", "path_bent_egos", "path_short_egos",
+                                  "path_long_egos"])
 def test_cpp_backend_written_cars_replay_reference(name):
     """MARLEnv-style writes through the read-write cars vector (cpp/bindings.cpp:24-25,29,66):
     Car.length / Car.width and Car.path set on the cars add_car_with_route made, then the
@@ -333,6 +334,56 @@ def test_cpp_backend_written_cars_replay_reference(name):
     assert [(c.length, c.width) for c in other.cars] == [(c.length, c.width) for c in env.cars]
     env.close()
     other.close()
+
+
+@pytest.mark.parametrize("name", ["path_past_end_npc", "path_long_npc"])
+def test_cpp_backend_written_traffic_cars_replay_reference(name):
+    """NPCs written through the read-write traffic_cars vector (cpp/bindings.cpp:29-30,67) with
+    Car.path set to paths of the caller's own: cuts of traffic routes with path_index past the
+    cut's end (the reference's ghost scan is then empty, TrafficFlow.cpp:88-89) and paths of
+    200-480 points -- every recorded output bit-exact against the reference (gen_golden.py
+    gen_paths_past_end / gen_paths_long)."""
+    g = G.load(name)
+    meta = g["meta"]
+    L = meta["num_lanes"]
+    P = 8 * L
+    env = cpp_backend.IntersectionEnv(L)
+    env.configure(meta["use_team"], meta["respawn"], meta["max_steps"])
+    env.configure_traffic(meta["traffic"], meta["density"])
+    env.configure_routes([tuple(r) for r in meta["traffic_routes"]])
+    env.reset()
+    for s, t in meta["ego_routes"]:
+        env.add_car_with_route(s, t)
+    env.lidars = [cpp_backend.Lidar(meta["rays"]) for _ in meta["ego_routes"]]
+    cps = G.custom_paths(g)
+    cars = env.cars
+    for k, c in enumerate(cars):
+        if meta["ego_paths"][k] >= 0:
+            c.path = [tuple(map(float, q)) for q in cps[meta["ego_paths"][k]]]
+    env.cars = cars
+    npcs = []
+    for f, i in zip(g["init_npc_f"], g["init_npc_i"]):
+        c = cpp_backend.Car()
+        c.state = cpp_backend.State(*map(float, f[:4]))
+        c.acc, c.steering_angle = float(f[4]), float(f[5])
+        c.alive, c.intention, c.path_index = bool(i[0]), int(i[1]), int(i[2])
+        if int(i[3]) >= 1000:
+            c.path = [tuple(map(float, q)) for q in cps[int(i[3]) - 1000]]
+        else:
+            s, t = meta["traffic_routes"][int(i[3])]
+            c._route = G.point_index(s, L) * P + G.point_index(t, L)
+        npcs.append(c)
+    env.traffic_cars = npcs
+    past = [c.path_index >= len(c.path) for c in env.traffic_cars if len(c.path)]
+    if name == "path_past_end_npc":
+        assert sum(past) >= 3, past
+    assert G.bits_equal(env.get_observations()[:, :31], g["init_obs"][:, :31])
+    for t in range(len(g["actions"])):
+        a = g["actions"][t]
+        res = env.step(a[:, 0].tolist(), a[:, 1].tolist(), meta["dt"])
+        info = dict(agents_alive=res.agents_alive, step=res.step, status=res.status, done=res.done)
+        _check_step(name, g, t, res.obs, res.rewards, res.terminated, res.truncated, info)
+    env.close()
 
 
 @pytest.mark.parametrize("name", ["lidar_mixed_n4", "lidar_mixed_npc"])

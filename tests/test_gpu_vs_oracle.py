@@ -40,6 +40,12 @@ CONFIGS = [
     # axis from the path's own last segment); egos may sit at path_index past their path's end
     dict(name="short_routes_n6", n=6, rays=64, use_team=True, custom="short"),
     dict(name="short_routes_traffic", n=1, rays=64, traffic=True, density=1.0, spawn_p=0.3, npcs=8, custom="short"),
+    # written paths of more than 160 points (the table's rows re-laid out at the longest, rounded up to 16), and
+    # NPCs whose path_index lies past their path's end (the reference's ghost scan is then empty)
+    dict(name="long_routes_n6", n=6, rays=64, use_team=True, custom="long"),
+    dict(name="long_routes_traffic", n=1, rays=64, traffic=True, density=1.0, spawn_p=0.3, npcs=8, custom="long"),
+    dict(name="past_end_traffic", n=2, rays=48, traffic=True, density=1.0, spawn_p=0.3, npcs=10, custom="short",
+         past=0.4),
     # per-car sizes (Car::length / Car::width, cpp/Car.h:19-20; mev_set_car_dims): egos and injected NPCs of
     # random sizes, spawned NPCs of the default one; the runtime-layout kernels run these handles
     dict(name="dims_n8_r64_team", n=8, rays=64, use_team=True, dims=True),
@@ -96,10 +102,21 @@ def random_dims(rng, h):
     return ego, npc
 
 
-def custom_routes(h, short=False):
+def resample(p, n):
+    """Polyline p at n points, uniform in the point index (linear interpolation in f64)."""
+    p = np.asarray(p, np.float64)
+    t = np.linspace(0.0, len(p) - 1.0, n)
+    i0 = np.minimum(np.floor(t).astype(int), len(p) - 2)
+    w = (t - i0)[:, None]
+    return (p[i0] * (1.0 - w) + p[i0 + 1] * w).astype(np.float32)
+
+
+def custom_routes(h, kind=True):
     """Four 160-point routes that no lane pair generates: three lane routes bent sideways by up to 9 px
     (a sine bump along the route's normal) and one straight diagonal across the whole intersection.
-    short: cut to 100, 40, 2 (the first point and point 60) and 75 points."""
+    "short": cut to 100, 40, 2 (the first point and point 60) and 75 points; "long": resampled at
+    240, 500, 1000 and 333 points."""
+    short = kind == "short"
     out = []
     for s, t, amp in ((1, 4, 9.0), (3, 12, -6.0), (7, 10, 5.0)):
         path, intent, _ = h.route_info(h.route_id(s - 1, 12 + t - 1))
@@ -112,10 +129,17 @@ def custom_routes(h, short=False):
     if short:
         out = [(out[0][0][:100], out[0][1]), (out[1][0][:40], out[1][1]),
                (out[2][0][[0, 60]], out[2][1]), (out[3][0][:75], out[3][1])]
+    if kind == "long":
+        out = [(resample(p_, m), it) for (p_, it), m in zip(out, (240, 500, 1000, 333))]
     return out
 
 
-def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=(), lattice=0, frozen=None):
+def _place_index(rng, n):
+    """A path point to place a car at: the first 150 of a path of <= 160 points, anywhere on a longer one."""
+    return int(rng.integers(0, n - 1 if n > 160 else min(150, n - 1)))
+
+
+def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=(), lattice=0, frozen=None, past=0.0):
     E = h.E
     st = h.get_state()
     ids = [h.route_id(s - 1, 4 * lanes + t - 1) for s, t in routes_table] + list(extra)
@@ -131,7 +155,7 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=(), latt
         for i in range(n):
             path, intent, spawn = h.route_info(int(ego_routes[e, i]))
             if rng.uniform() < 0.7:  # near its route
-                j = int(rng.integers(0, min(150, h.route_len(int(ego_routes[e, i])) - 1)))
+                j = _place_index(rng, h.route_len(int(ego_routes[e, i])))
                 x, y = path[j] + rng.normal(0, 4, 2)
                 hd = np.arctan2(-(path[j + 1, 1] - path[j, 1]), path[j + 1, 0] - path[j, 0]) + rng.normal(0, 0.2)
                 pidx = max(0, j - int(rng.integers(0, 5)))
@@ -163,7 +187,7 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=(), latt
                 break
             ri = int(rng.integers(0, len(troutes)))
             path, intent, spawn = h.route_info(troutes[ri])
-            j = int(rng.integers(0, min(150, h.route_len(troutes[ri]) - 1)))
+            j = _place_index(rng, h.route_len(troutes[ri]))
             x, y = path[j]
             if any((x - a) ** 2 + (y - b) ** 2 < gap ** 2 for a, b in placed):
                 continue
@@ -174,6 +198,8 @@ def _random_state(rng, h, n, npcs, lanes, routes_table, gap=60.0, extra=(), latt
             st["npc_acc"][e, cnt] = 0.0
             st["npc_steering"][e, cnt] = rng.uniform(-0.2, 0.2)
             st["npc_path_index"][e, cnt] = max(0, j - 1)
+            if rng.uniform() < past:  # (a written path_index past the path's end)
+                st["npc_path_index"][e, cnt] = h.route_len(troutes[ri]) + int(rng.integers(0, 20))
             st["npc_route"][e, cnt] = troutes[ri]
             st["npc_intention"][e, cnt] = intent
             st["npc_alive"][e, cnt] = 1
@@ -295,7 +321,7 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0, max_npcs=64, E=2
         h.set_beam_angles(rel)
         assert G.bits_equal(h.beam_angles(), rel)
     table = ROUTES2 if lanes == 2 else ROUTES3
-    customs = custom_routes(h, cfg.get("custom") == "short") if cfg.get("custom") else []
+    customs = custom_routes(h, cfg["custom"]) if cfg.get("custom") else []
     extra = [h.add_route(path, intent) for path, intent in customs]
     P = 8 * lanes
     assert extra == list(range(P * P, P * P + len(customs)))
@@ -305,7 +331,7 @@ def _random_states_vs_oracle(mev, cfg, kernel, pack=0, split=0, max_npcs=64, E=2
         assert G.bits_equal(got[0][: len(path)], path) and got[1] == intent and tuple(got[2][:2]) == tuple(path[0])
     frozen = rng.uniform(size=(E, n)) < cfg.get("frozen", 0.0)
     st, troutes = _random_state(rng, h, n, cfg.get("npcs", 0), lanes, table, cfg.get("npc_gap", 60.0), extra,
-                                cfg.get("lattice", 0), frozen)
+                                cfg.get("lattice", 0), frozen, cfg.get("past", 0.0))
     h.set_traffic_routes(troutes)
     dims = None
     if cfg.get("dims"):
