@@ -269,6 +269,12 @@ class IntersectionEnv:
         self._fresh = True               # no step since reset: added cars start from spawn
         self._pending: List[int] = []    # cars added since the last sync
         self._traffic_routes: Optional[List[int]] = None  # None = reference default (init_traffic_routes)
+        # An env without egos still steps (IntersectionEnv.cpp:133-142: the count, truncation and the traffic
+        # run with cars empty): its handle holds one ego slot with a dead car far off the map (_NO_EGO_XY).
+        # Every ego loop of step skips a dead car, and the one reader of a dead ego, the NPC spawn test's
+        # distance to every ego (TrafficFlow.cpp:240-259), never reaches it there.
+        self._ghost = False        # self._h is such a handle
+        self._ghost_reset = False  # reset() since: the next use resets it
 
     # ------------------------------------------------------------ config
     def configure(self, use_team: bool, respawn: bool, max_steps: int):
@@ -306,6 +312,7 @@ class IntersectionEnv:
     def reset(self):
         """IntersectionEnv::reset (cpp/IntersectionEnv.cpp:66-76)."""
         self._routes, self._agent_ids, self._pending = [], [], []
+        self._ghost_reset = self._ghost
         self._next_id = 1
         self._fresh = True
         self._lidar = DEFAULT_LIDAR  # add_car_with_route gives every new car a 96-ray Lidar
@@ -359,16 +366,22 @@ class IntersectionEnv:
         keys = list(lidar[1][:n])
         return keys + [_default_key(DEFAULT_LIDAR)] * (n - len(keys))
 
-    def _sync(self) -> Optional[_capi.Handle]:
+    def _sync(self, ghost: bool = False) -> Optional[_capi.Handle]:
+        """The device handle for the cars added so far; without cars None, or (ghost) the
+        no-ego handle (see __init__)."""
         n = len(self._routes)
         if n == 0:
-            return None
+            return self._sync_ghost(ghost)
         h = self._h
-        if h is None or h.N != n or self._h_lidar != self._lidar:
+        if h is None or h.N != n or self._h_lidar != self._lidar or self._ghost:
             keep = keep_dims = None
             if h is not None and not self._fresh:
                 keep = h.get_state()  # cars added mid-episode keep the running episode
                 keep_dims = h.car_dims() if h.car_dims_active() else None
+                if self._ghost:  # (the placeholder is no car)
+                    keep = {k: v for k, v in keep.items() if k.startswith("npc_") or v.ndim == 1}
+                    keep_dims = (keep_dims[0][:, :0], keep_dims[1]) if keep_dims is not None else None
+            self._ghost = False
             if h is not None:
                 h.close()
             h = self._h = self._create(n, self._lidar)
@@ -392,11 +405,44 @@ class IntersectionEnv:
             self._pending = []
         return h
 
+    def _sync_ghost(self, create: bool) -> Optional[_capi.Handle]:
+        h = self._h
+        if h is not None and self._ghost:
+            if self._reward_dirty:
+                h.set_reward(self._reward.as_list())
+                self._reward_dirty = False
+            if self._ghost_reset:
+                h.reset()
+                self._place_ghost(h)
+                self._ghost_reset = False
+            return h
+        if not create:
+            return None
+        if h is not None:
+            h.close()
+        h = self._h = self._create(1, DEFAULT_LIDAR)
+        self._h_lidar = DEFAULT_LIDAR
+        self._ghost, self._ghost_reset, self._reward_dirty = True, False, False
+        if self._traffic_routes is not None:
+            h.set_traffic_routes(self._traffic_routes)
+        h.set_ego_routes(np.zeros((1, 1), np.int32))
+        h.reset()
+        self._place_ghost(h)
+        return h
+
+    @staticmethod
+    def _place_ghost(h, st=None):
+        st = h.get_state() if st is None else st
+        for k in ("x", "y", "spawn_x", "spawn_y"):
+            st[k][0, 0] = _NO_EGO_XY
+        st["alive"][0, 0] = 0
+        h.set_state(st)
+
     def _restore_grown(self, old, old_dims=None):
         """Old cars keep their state (and size); newly added ones start at their spawn (add_car_with_route)."""
         h = self._h
         new = h.get_state()  # after creation == a reset: every car at its spawn
-        m = old["x"].shape[1]
+        m = old["x"].shape[1] if "x" in old else 0
         for k, v in old.items():
             if k.startswith("npc_") or v.ndim == 1:
                 new[k] = v
@@ -405,7 +451,7 @@ class IntersectionEnv:
         h.set_state(new)
         if old_dims is not None:
             ego, npc = h.car_dims()
-            ego[:, :m] = old_dims[0]
+            ego[:, :m] = old_dims[0][:, :m]
             h.set_car_dims(ego, old_dims[1])
 
     @property
@@ -415,17 +461,16 @@ class IntersectionEnv:
 
     @step_count.setter
     def step_count(self, value: int):
-        h = self._sync()
+        h = self._sync(ghost=True)
         if h is not None:
             h.set_state({"step_count": np.array([int(value)], np.int32)})
 
     def step(self, throttles: Sequence[float], steerings: Sequence[float], dt: float = 1.0 / 60.0) -> StepResult:
         """IntersectionEnv::step (cpp/IntersectionEnv.cpp:133-392) on the GPU."""
         h = self._h
-        if h is None or self._pending or self._reward_dirty or h.N != len(self._routes) or self._h_lidar != self._lidar:
-            h = self._sync()
-            if h is None:
-                return StepResult()
+        if h is None or self._pending or self._reward_dirty or h.N != len(self._routes) or self._h_lidar != self._lidar \
+                or self._ghost:
+            h = self._sync(ghost=True)
         n = h.N
         # one action buffer and one output dict per handle (its args struct is reused by
         # Handle.step); the result's arrays are copies, like the reference's pybind conversions
@@ -440,11 +485,12 @@ class IntersectionEnv:
         act[0, : s.size, 1] = s
         out = h.step(act, float(dt), out=self._out)
         self._fresh = False
+        m = 0 if self._ghost else n
         res = StepResult.__new__(StepResult)
-        res.obs = out["obs"][0].copy()
-        res.rewards = out["reward"][0].copy()
-        res.done = out["done"][0].tolist()
-        res.status = [STATUS[x] for x in out["status"][0].tolist()]
+        res.obs = out["obs"][0][:m].copy()
+        res.rewards = out["reward"][0][:m].copy()
+        res.done = out["done"][0][:m].tolist()
+        res.status = [STATUS[x] for x in out["status"][0][:m].tolist()]
         res.agent_ids = list(self._agent_ids)
         res.agents_alive = int(out["agents_alive"][0])
         res.terminated = bool(out["terminated"][0])
@@ -455,7 +501,7 @@ class IntersectionEnv:
     def get_observations(self) -> np.ndarray:
         """get_observations (cpp/IntersectionEnv.cpp:418-520): float32 [n, 127]."""
         h = self._sync()
-        if h is None:
+        if h is None or self._ghost:
             return np.zeros((0, OBS_W), np.float32)
         return h.observations()[0]
 
@@ -466,7 +512,7 @@ class IntersectionEnv:
         if dims is None:
             dims = h.car_dims() if h.car_dims_active() else None
         if ego:
-            n = h.N
+            n = 0 if self._ghost else h.N
             get = lambda k, i: st[k][0, i]  # noqa: E731
             count = n
         else:
@@ -513,7 +559,7 @@ class IntersectionEnv:
         """One Lidar per car; distances recovered exactly from the observation
         (every distance is max_dist or a probe distance k*step)."""
         h = self._sync()
-        if h is None:
+        if h is None or self._ghost:
             return []
         n = h.N
         keys = self._car_keys(self._lidar, n) if self._lidar[0] == "per_car" else [_default_key(self._lidar)] * n
@@ -550,7 +596,7 @@ class IntersectionEnv:
             lidar = (int(lidar[0]), float(lidar[1]), float(lidar[2]), float(lidar[3]))
         if lidar == self._lidar:
             return
-        if self._h is not None and len(self._routes) == self._h.N:
+        if self._h is not None and len(self._routes) == self._h.N and not self._ghost:
             st = self._h.get_state()
             dims = self._h.car_dims() if self._h.car_dims_active() else None
             self._h.close()
@@ -629,27 +675,30 @@ class IntersectionEnv:
         """IntersectionEnv.traffic_cars is read-write (cpp/bindings.cpp:67): the NPC vector is replaced."""
         s = self.get_state()
         s.traffic_cars = list(cars)
-        if self._routes:
+        if self._routes or s.traffic_cars or self._ghost:
             self._apply_state(s, self._lidar)
-        elif s.traffic_cars:
-            raise ValueError("traffic cars need at least one ego car in this backend")
 
     def _apply_state(self, s: EnvState, lidar):
         n = len(s.cars)
-        if n == 0:
-            self._routes = []
-            return
-        if self._h is None or self._h.N != n or self._h_lidar != lidar:
+        if n == 0:  # the cars vector emptied: the traffic and the step count stay (the no-ego handle)
+            self._routes, self._pending = [], []
+            if not s.traffic_cars and not s.step_count and not self._ghost:
+                return
+            self._sync_ghost(True)
+            self._ghost_reset = False
+        elif self._h is None or self._h.N != n or self._h_lidar != lidar or self._ghost:
             if self._h is not None:
                 self._h.close()
             self._h = self._create(n, lidar)
             self._h_lidar = lidar
+            self._ghost = False
         routes = [self._route_of(c) for c in s.cars]
         self._routes = routes
-        self._lidar = lidar
-        if self._traffic_routes is not None:
-            self._h.set_traffic_routes(self._traffic_routes)
-        self._h.set_ego_routes(np.asarray(routes, np.int32)[None])
+        if n:
+            self._lidar = lidar
+            if self._traffic_routes is not None:
+                self._h.set_traffic_routes(self._traffic_routes)
+            self._h.set_ego_routes(np.asarray(routes, np.int32)[None])
         st = self._h.get_state()
         for i, c in enumerate(s.cars):
             st["x"][0, i], st["y"][0, i], st["v"][0, i], st["heading"][0, i] = (c.state.x, c.state.y, c.state.v,
@@ -674,9 +723,12 @@ class IntersectionEnv:
             st["npc_route"][0, j] = self._route_of(c)
         st["npc_count"][0] = k
         st["step_count"][0] = int(s.step_count)
-        self._h.set_state(st)
+        if n == 0:
+            self._place_ghost(self._h, st)
+        else:
+            self._h.set_state(st)
         # Car::length / Car::width of every car (the reference copies them with the cars)
-        ego_d = np.array([[[c.length, c.width] for c in s.cars]], np.float32)
+        ego_d = np.array([[[c.length, c.width] for c in s.cars]] if n else [[[54.0, 24.0]]], np.float32)
         npc_d = np.empty((1, self._h.K, 2), np.float32)
         npc_d[...] = (54.0, 24.0)
         if k:
@@ -704,9 +756,13 @@ class IntersectionEnv:
         if self._h is not None:
             self._h.close()
             self._h = None
+        self._ghost = False
 
 
 # reference cpp_backend.py factories
+_NO_EGO_XY = -1.0e5  # the no-ego handle's placeholder car (IntersectionEnv.__init__)
+
+
 def _require():
     if not has_cpp_backend():
         raise RuntimeError("libmarlenv_hip.so is not built: run python -c 'import __graft_entry__ as g; g.build()'")

@@ -729,7 +729,7 @@ static void observe(const orc_env* e, float* obs) {
 /* ------------------------------------------------------------ public API */
 orc_env* orc_create(int lanes, int n, int rays, float fov, float maxd, float step, int obs_dim, int use_team,
                     int respawn_on, int max_steps, int traffic, float density, const float* rc, int max_npcs) {
-    if (n < 1 || n > MAXCARS || rays < 1 || max_npcs < 0 || max_npcs > MAXCARS) return NULL;
+    if (n < 0 || n > MAXCARS || rays < 1 || max_npcs < 0 || max_npcs > MAXCARS) return NULL;  /* n = 0: an env without egos */
     orc_env* e = (orc_env*)calloc(1, sizeof(orc_env));
     e->lanes = lanes; e->n = n; e->rays = rays; e->fov = fov; e->maxd = maxd; e->step = step;
     e->obs_dim = obs_dim > 0 ? obs_dim : 31 + rays;

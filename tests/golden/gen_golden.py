@@ -222,17 +222,18 @@ def inject_npcs(kcount: int, dims=None, custom=None):
         """Place NPCs on points of random traffic routes (on their own path,
         path-aligned heading), at least 70 px apart and away from the ego."""
         ef, _ = env.cars(0)
-        placed = [(float(ef[0, 0]), float(ef[0, 1]))]
+        placed = [(float(ef[0, 0]), float(ef[0, 1]))] if len(ef) else []  # (an env may have no ego)
+        e0 = len(placed)
         tries = 0
-        while len(placed) < kcount + 1 and tries < 1000:
+        while len(placed) < kcount + e0 and tries < 1000:
             tries += 1
-            j = len(placed) - 1
+            j = len(placed) - e0
             cj = custom[j] if custom is not None and j < len(custom) else -1
             route = int(rng.integers(0, 12))
             path = env.route_path(route) if cj < 0 else env.custom_paths[cj]
             idx = int(rng.integers(0, min(150, len(path) - 1)))
             x, y = float(path[idx, 0]), float(path[idx, 1])
-            if min((x - px) ** 2 + (y - py) ** 2 for px, py in placed) < 70.0 ** 2:
+            if placed and min((x - px) ** 2 + (y - py) ** 2 for px, py in placed) < 70.0 ** 2:
                 continue
             dx, dy = path[idx + 1] - path[idx]
             f = np.zeros(R.NF, np.float32)
@@ -443,6 +444,19 @@ def gen_paths_past_end():
         custom_paths=[n9[:60], n4[:90]], ego_paths=[-1], inject=inject_npcs_past_end)
 
 
+def gen_no_ego():
+    """Traffic in an env without egos (reset, then traffic_cars written, no add_car_with_route):
+    step() still counts, truncates and runs update_traffic_flow (IntersectionEnv.cpp:133-142)."""
+    run("traffic_no_ego", n_agents=0, rays=64, traffic=True, density=0.0, steps=300, act="random", seed=435,
+        ego_routes=[], max_steps=250, inject=inject_npcs(7))
+
+
+def gen_no_ego_traffic():
+    """The same with the reference's own spawns at density 5 (recorded, replayed)."""
+    run("traffic_no_ego_d5", n_agents=0, rays=64, traffic=True, density=5.0, steps=400, act="random", seed=436,
+        ego_routes=[])
+
+
 def rel_angles(rays: int, fov: float) -> List[float]:
     """Lidar's beam offsets (cpp/Lidar.cpp:4-14, IntersectionEnv.cpp:118-126) in float32."""
     f32 = np.float32
@@ -593,9 +607,9 @@ def _traffic():
 
 GROUPS = [("core", _core, True), ("dims", gen_dims, True), ("paths", gen_paths, True), ("lidars", gen_lidars, True),
           ("paths_short", gen_paths_short, True), ("ties", gen_ties, True), ("paths_long", gen_paths_long, True),
-          ("paths_past_end", gen_paths_past_end, True),
+          ("paths_past_end", gen_paths_past_end, True), ("no_ego", gen_no_ego, True),
           ("traffic", _traffic, False), ("dims_traffic", gen_dims_traffic, False),
-          ("paths_traffic", gen_paths_traffic, False)]
+          ("paths_traffic", gen_paths_traffic, False), ("no_ego_traffic", gen_no_ego_traffic, False)]
 
 
 def check() -> int:

@@ -129,13 +129,40 @@ def npc_slots(data) -> int:
     return 32 if k <= 32 else 64
 
 
+# An env without egos (traffic_no_ego*: the reference steps its traffic with cars empty) runs on a handle
+# with one ego slot holding a dead car far off the map, as cpp_backend does: a dead ego is skipped by every
+# ego loop of IntersectionEnv::step, and the only reader of a dead ego, the NPC spawn test's distance to
+# every ego (TrafficFlow.cpp:240-259), never reaches it there.
+NO_EGO_XY = -1.0e5
+
+
+def ego_slots(meta) -> int:
+    return max(1, int(meta["n_agents"]))
+
+
 def make_handle(mod, meta, num_envs: int, device: int = 0, max_npcs: int = 32):
     R = int(meta["rays"])
-    return mod.Handle(num_envs=num_envs, num_agents=int(meta["n_agents"]), num_lanes=int(meta["num_lanes"]),
+    return mod.Handle(num_envs=num_envs, num_agents=ego_slots(meta), num_lanes=int(meta["num_lanes"]),
                       lidar_rays=R, obs_dim=127 if R <= 96 else 31 + R, traffic_flow=int(meta["traffic"]),
                       traffic_density=float(meta["density"]), use_team_reward=int(meta["use_team"]),
                       respawn_enabled=int(meta["respawn"]), max_steps=int(meta["max_steps"]),
                       reward=meta["reward"], max_npcs=max_npcs, device=device)
+
+
+def set_egos(st, b, d, routes):
+    """Env b's egos in a mev_get_state dict at scenario d's initial state (routes: their ids);
+    without egos, the placeholder slot (NO_EGO_XY)."""
+    f, i = d["init_ego_f"], d["init_ego_i"]
+    if len(f) == 0:
+        for key in EGO_F:
+            st[key][b] = 0.0
+        st["x"][b], st["y"][b] = NO_EGO_XY, NO_EGO_XY
+        st["spawn_x"][b], st["spawn_y"][b] = NO_EGO_XY, NO_EGO_XY
+        st["alive"][b], st["intention"][b], st["path_index"][b], st["route"][b] = 0, 0, 0, routes
+        return
+    for j, key in enumerate(EGO_F):
+        st[key][b] = f[:, j]
+    st["alive"][b], st["intention"][b], st["path_index"][b], st["route"][b] = i[:, 0], i[:, 1], i[:, 2], routes
 
 
 def single_env_handle(mod, d):
@@ -147,13 +174,10 @@ def single_env_handle(mod, d):
     cids = custom_route_ids(h, d)
     troutes = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["traffic_routes"]]
     h.set_traffic_routes(troutes)
-    ego_routes = np.array([ego_route_ids(h, d, L, cids)], np.int32)
+    ego_routes = np.array([(ego_route_ids(h, d, L, cids) + troutes)[: ego_slots(meta)]], np.int32)
     h.set_ego_routes(ego_routes)
     st = h.get_state()
-    f, i = d["init_ego_f"], d["init_ego_i"]
-    for j, key in enumerate(EGO_F):
-        st[key][0] = f[:, j]
-    st["alive"][0], st["intention"][0], st["path_index"][0], st["route"][0] = i[:, 0], i[:, 1], i[:, 2], ego_routes[0]
+    set_egos(st, 0, d, ego_routes[0])
     k = len(d["init_npc_f"])
     st["npc_count"][0] = k
     if k:
@@ -201,20 +225,14 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
     troutes = [h.route_id(point_index(s, L), point_index(e, L)) for s, e in meta["traffic_routes"]]
     h.set_traffic_routes(troutes)
     n = int(meta["n_agents"])
-    ego_routes = np.zeros((B, n), np.int32)
+    ego_routes = np.zeros((B, ego_slots(meta)), np.int32)
     for b, d in enumerate(data):
-        ego_routes[b] = ego_route_ids(h, d, L, cids[b])
+        ego_routes[b] = (ego_route_ids(h, d, L, cids[b]) + troutes)[: ego_slots(meta)]
     h.set_ego_routes(ego_routes)
     # initial state
     st = h.get_state()
     for b, d in enumerate(data):
-        f, i = d["init_ego_f"], d["init_ego_i"]
-        for j, key in enumerate(EGO_F):
-            st[key][b] = f[:, j]
-        st["alive"][b] = i[:, 0]
-        st["intention"][b] = i[:, 1]
-        st["path_index"][b] = i[:, 2]
-        st["route"][b] = ego_routes[b]
+        set_egos(st, b, d, ego_routes[b])
         k = len(d["init_npc_f"])
         st["npc_count"][b] = k
         if k:
@@ -233,12 +251,14 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
     reports = [Report(nm) for nm in names]
     obs0 = h.observations()
     for b, d in enumerate(data):
-        if not bits_equal(obs0[b, :, :127], d["init_obs"]):
+        if not bits_equal(obs0[b, :n, :127], d["init_obs"]):
             reports[b].add("initial obs differ")
     T = min(int(meta["steps"]), steps or 10 ** 9)
     out = h.alloc_outputs()
     for t in range(T):
         acts = np.stack([d["actions"][t] for d in data])
+        if n == 0:  # (the placeholder slot's action: a dead car reads none)
+            acts = np.zeros((B, 1, 2), np.float32)
         spawn = None
         if meta["traffic"]:
             spawn = np.array([d["spawned"][t] for d in data], np.int32)
@@ -251,7 +271,7 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
                 continue
             rep.steps = t + 1
             g_obs = d["obs"][t]
-            my = out["obs"][b]
+            my = out["obs"][b][:n]
             diff = float(np.max(np.abs(my[:, :127] - g_obs))) if my.size else 0.0
             rep.max_obs_diff = max(rep.max_obs_diff, diff)
             if not bits_equal(my[:, :127], g_obs):
@@ -260,11 +280,11 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
             if "lidar" in d and meta["rays"] > 96:
                 if not bits_equal(my[:, 31:], d["lidar"][t] * np.float32(1.0 / 250.0)):
                     rep.add(f"step {t + 1}: full lidar differs")
-            if not bits_equal(out["reward"][b], d["rew"][t]):
+            if not bits_equal(out["reward"][b][:n], d["rew"][t]):
                 rep.add(f"step {t + 1}: reward {out['reward'][b].tolist()} vs {d['rew'][t].tolist()}")
-            if not bits_equal(out["done"][b], d["done"][t]):
+            if not bits_equal(out["done"][b][:n], d["done"][t]):
                 rep.add(f"step {t + 1}: done {out['done'][b].tolist()} vs {d['done'][t].tolist()}")
-            if not bits_equal(out["status"][b], d["status"][t]):
+            if not bits_equal(out["status"][b][:n], d["status"][t]):
                 rep.add(f"step {t + 1}: status {out['status'][b].tolist()} vs {d['status'][t].tolist()}")
             fl = d["flags"][t]
             got = [int(out["terminated"][b]), int(out["truncated"][b]), int(out["agents_alive"][b]),
@@ -273,10 +293,10 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
                 rep.add(f"step {t + 1}: flags {got} vs {fl.tolist()}")
             ef, ei = d["ego_f"][t], d["ego_i"][t]
             for j, key in enumerate(EGO_F):
-                if not bits_equal(st[key][b], ef[:, j]):
+                if not bits_equal(st[key][b][:n], ef[:, j]):
                     rep.add(f"step {t + 1}: ego {key} {st[key][b][:4]} vs {ef[:4, j]}")
-            if not bits_equal(st["alive"][b], ei[:, 0].astype(np.uint8)) or \
-                    not bits_equal(st["intention"][b], ei[:, 1]) or not bits_equal(st["path_index"][b], ei[:, 2]):
+            if not bits_equal(st["alive"][b][:n], ei[:, 0].astype(np.uint8)) or \
+                    not bits_equal(st["intention"][b][:n], ei[:, 1]) or not bits_equal(st["path_index"][b][:n], ei[:, 2]):
                 rep.add(f"step {t + 1}: ego alive/intention/path_index differ")
             kc = int(d["npc_count"][t])
             if int(st["npc_count"][b]) != kc:
@@ -292,7 +312,7 @@ def replay(mod, names, steps: Optional[int] = None, stop_at_first=True, kernel: 
                     rep.add(f"step {t + 1}: npc route differ")
                 if cd is not None and not bits_equal(cd[1][b, :kc], nf[:, 13:15]):
                     rep.add(f"step {t + 1}: npc length / width differ")
-            if cd is not None and not bits_equal(cd[0][b], ef[:, 13:15]):
+            if cd is not None and not bits_equal(cd[0][b][:n], ef[:, 13:15]):
                 rep.add(f"step {t + 1}: ego length / width differ")
         if stop_at_first and all(not r.ok for r in reports):
             break

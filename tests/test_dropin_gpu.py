@@ -386,6 +386,65 @@ def test_cpp_backend_written_traffic_cars_replay_reference(name):
     env.close()
 
 
+def test_cpp_backend_traffic_without_egos_replays_reference():
+    """An env with traffic and no egos (reset, traffic_cars written, no add_car_with_route): step()
+    counts, truncates and runs the traffic (IntersectionEnv.cpp:133-142) -- the step flags and every
+    NPC's state bit-exact against the reference (gen_golden.py gen_no_ego); then egos added to the
+    running episode find the NPCs and the step count where the steps left them."""
+    g = G.load("traffic_no_ego")
+    meta = g["meta"]
+    L = meta["num_lanes"]
+    P = 8 * L
+    env = cpp_backend.IntersectionEnv(L)
+    env.configure(meta["use_team"], meta["respawn"], meta["max_steps"])
+    env.configure_traffic(meta["traffic"], meta["density"])
+    env.configure_routes([tuple(r) for r in meta["traffic_routes"]])
+    env.reset()
+    npcs = []
+    for f, i in zip(g["init_npc_f"], g["init_npc_i"]):
+        c = cpp_backend.Car()
+        c.state = cpp_backend.State(*map(float, f[:4]))
+        c.acc, c.steering_angle = float(f[4]), float(f[5])
+        c.alive, c.intention, c.path_index = bool(i[0]), int(i[1]), int(i[2])
+        s, t = meta["traffic_routes"][int(i[3])]
+        c._route = G.point_index(s, L) * P + G.point_index(t, L)
+        npcs.append(c)
+    env.traffic_cars = npcs
+    assert env.cars == [] and env.get_observations().shape == (0, 127) and len(env.traffic_cars) == len(npcs)
+    for t in range(len(g["actions"])):
+        res = env.step([], [], meta["dt"])
+        f = g["flags"][t]
+        assert (int(res.terminated), int(res.truncated), res.agents_alive, res.step) == tuple(int(x) for x in f), t
+        assert res.obs.shape == (0, 127) and len(res.rewards) == 0 and res.status == [] and res.agent_ids == []
+        tc = env.traffic_cars
+        k = int(g["npc_count"][t])
+        assert len(tc) == k, (t, len(tc), k)
+        got = np.array([[c.state.x, c.state.y, c.state.v, c.state.heading, c.acc, c.steering_angle] for c in tc],
+                       np.float32).reshape(k, 6)
+        assert G.bits_equal(got, g["npc_f"][t, :k, :6]), t
+        assert [c.path_index for c in tc] == g["npc_i"][t, :k, 2].tolist(), t
+        if t == 40:
+            snap = env.get_state()
+    assert env.step_count == len(g["actions"])
+    # egos join the running episode: NPCs and the step count carry over (add_car_with_route, :78-131)
+    other = cpp_backend.IntersectionEnv(L)
+    other.configure(meta["use_team"], meta["respawn"], meta["max_steps"])
+    other.configure_traffic(meta["traffic"], meta["density"])
+    other.configure_routes([tuple(r) for r in meta["traffic_routes"]])
+    other.set_state(snap)
+    assert other.cars == [] and other.step_count == 41 and len(other.traffic_cars) == int(g["npc_count"][40])
+    other.add_car_with_route("IN_1", "OUT_4")
+    assert len(other.cars) == 1 and other.step_count == 41
+    assert [(c.state.x, c.path_index) for c in other.traffic_cars] == [(c.state.x, c.path_index) for c in snap.traffic_cars]
+    res = other.step([0.5], [0.0], meta["dt"])
+    assert res.step == 42 and len(res.rewards) == 1 and res.obs.shape == (1, 127)
+    env.reset()  # the no-ego handle starts over: no traffic, step 0
+    assert env.traffic_cars == [] and env.step_count == 0
+    assert env.step([], []).step == 1
+    env.close()
+    other.close()
+
+
 @pytest.mark.parametrize("name", ["lidar_mixed_n4", "lidar_mixed_npc"])
 def test_cpp_backend_per_car_lidars_replay_reference(name):
     """Per-car LiDAR objects written through IntersectionEnv.lidars (cpp/bindings.cpp:68,85-92):

@@ -85,7 +85,7 @@ def test_golden_scenario_split_waves(mev, name, split):
 
 
 # (goldens with other car sizes run the runtime-layout kernel, which has no split)
-TRAFFIC_ONE_EGO = [n for n in SINGLE if G.load(n)["meta"]["traffic"] and G.load(n)["meta"]["n_agents"] == 1
+TRAFFIC_ONE_EGO = [n for n in SINGLE if G.load(n)["meta"]["traffic"] and G.load(n)["meta"]["n_agents"] <= 1
                    and not G.has_dims(G.load(n)) and G.npc_slots([G.load(n)]) == 32]
 
 
