@@ -2686,7 +2686,8 @@ struct LidarSrcLdsEnvs {
 // kinematics; 2 = phases 1-2 again for the compacted agents in `redo` (egos the car
 // part respawned since; the caller has put their new poses in ag[]), then phase 3
 // and the block writes.  0 = everything.
-template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR, bool HELP = false, int PART = 0>
+// P1 = 1: R is a multiple of 64 (the dense phase-1 walk below is not compiled in).
+template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR, bool HELP = false, int PART = 0, int P1 = 0>
 __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& out, const Src& src, const int G,
                                            const int a0, const int na, const int lane, unsigned char* base,
                                            const LidarLayout& lay, const unsigned long long redo = 0ull,
@@ -2833,7 +2834,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // next chunk, ILP chunks per pass; R = 96 takes 6 chunks per 4 agents, not 8
     // half-empty ones.  (One loop for both measured 2 % slower at config 3: the chunk
     // walk's bookkeeping and the offsets' LDS reads in front of every pass.)
-    const bool dense = (R & (WAVE - 1)) != 0 && nal > 1;
+    const bool dense = P1 != 1 && (R & (WAVE - 1)) != 0 && nal > 1;
     auto phase1 = [&](auto small) {
         if constexpr (PART == 2) {  // the respawned agents only
             for (unsigned long long tm = redo; tm; tm &= tm - 1ull) pass1_one(small, __builtin_ctzll(tm));
@@ -3402,7 +3403,8 @@ constexpr int kTsplitWpe = 6;
 constexpr int kPrioEsplitRoad = 3;
 constexpr int kPrioEsplitCars = 2;
 constexpr int kPrioEsplitCarPhase = 1;
-template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false>
+// P1 = 1: a LiDAR of a multiple of 64 beams (lidar_body's P1), the configs 3 and 5 kernel
+template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false, int P1 = 0>
 __global__ __launch_bounds__((TRAFFIC && ESPLIT) ? (PK + 1) * WAVE : (SPLIT ? 2 * WAVE : WAVE),
                              (TRAFFIC && ESPLIT) ? kTsplitWpe
                                                  : ((ESPLIT && PK == 1) ? kEsplitWpe : (SPLIT ? kSplitWpe : 4))) void k_step(
@@ -3431,6 +3433,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? kSplitWpe : 4) voi
     __shared__ uint32_t cmdw[kServeLine];
     constexpr int PK = 1;
     constexpr bool ESPLIT = false;
+    constexpr int P1 = 0;
     const int lane = threadIdx.x & (WAVE - 1);
     const bool w0 = threadIdx.x < WAVE;
     ServeBox* box = sa.box;
@@ -3724,6 +3727,8 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if ((p.R & (WAVE - 1)) == 0)
+            hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 1>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else hipLaunchKernelGGL((k_step<false, TAB, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
     } else {
         const unsigned lds = (unsigned)step_layout(p).bytes;
