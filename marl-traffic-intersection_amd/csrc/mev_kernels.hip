@@ -2686,6 +2686,9 @@ struct LidarSrcLdsEnvs {
 // kinematics; 2 = phases 1-2 again for the compacted agents in `redo` (egos the car
 // part respawned since; the caller has put their new poses in ag[]), then phase 3
 // and the block writes.  0 = everything.
+#ifndef MEV_DENSE_ILP
+#define MEV_DENSE_ILP 2
+#endif
 // P1 = 1: R is a multiple of 64 (the dense phase-1 walk below is not compiled in).
 template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR, bool HELP = false, int PART = 0, int P1 = 0>
 __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& out, const Src& src, const int G,
@@ -2841,25 +2844,26 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         } else if (dense) {
             const float invRp = 1.0f / (float)R;
             const int nq = nal * R;
-            for (int c0 = 0; c0 < nq; c0 += ILP * WAVE) {
+            constexpr int DI = ILP > 1 ? MEV_DENSE_ILP : 1;
+            for (int c0 = 0; c0 < nq; c0 += DI * WAVE) {
                 if (PART == 0 && 4 * c0 >= nq) __builtin_amdgcn_s_setprio(kPrioP1B);
-                int q[ILP];
-                float4 a[ILP];
-                float rb[ILP];
+                int q[DI];
+                float4 a[DI];
+                float rb[DI];
 #pragma unroll
-                for (int u = 0; u < ILP; ++u) {
+                for (int u = 0; u < DI; ++u) {
                     q[u] = c0 + u * WAVE + lane;
                     const int qc = q[u] < nq ? q[u] : nq - 1;
                     const int j = (int)(((float)qc + 0.5f) * invRp);  // exact (see load_beam)
                     a[u] = ag[j];
                     rb[u] = src.rel(qc - j * R);
                 }
-                float2 d[ILP];
-                int r[ILP];
+                float2 d[DI];
+                int r[DI];
 #pragma unroll
-                for (int u = 0; u < ILP; ++u) r[u] = setup(a[u], rb[u], small, d[u], false);
+                for (int u = 0; u < DI; ++u) r[u] = setup(a[u], rb[u], small, d[u], false);
 #pragma unroll
-                for (int u = 0; u < ILP; ++u) {
+                for (int u = 0; u < DI; ++u) {
                     const bool vq = q[u] < nq;
                     if (vq) {
                         dir[q[u]] = d[u];

@@ -39,7 +39,9 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                "trk": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
                "nounclust": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule=1"],
                "bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
-               "relaxocc": ["-mllvm", "--amdgpu-schedule-relaxed-occupancy"]}
+               "relaxocc": ["-mllvm", "--amdgpu-schedule-relaxed-occupancy"],
+               # the dense phase-1 walk (R not a multiple of 64) at 3 / 4 chunks per pass instead of 2
+               "dilp3": ["-DMEV_DENSE_ILP=3"], "dilp4": ["-DMEV_DENSE_ILP=4"]}
 
 
 def build(name: str, force: bool = False) -> str:
