@@ -305,9 +305,9 @@ int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave);
  * 1 = off, 2 = on (no traffic), 3 = early split (no traffic, one env per
  * workgroup, N * R <= 512: the LiDAR wave marches the road from the poses after
  * the kinematics while the car wave resolves collisions).  With traffic, one ego
- * per env, <= 32 NPC slots, R <= 128 and E a multiple of 32, the early split is
- * four envs per workgroup: one wave per env runs the NPC controller and the car
- * logic, one wave runs the four egos' kinematics, status and LiDAR beside them;
+ * per env, <= 32 NPC slots, R <= 128 and E a multiple of 16, the early split is
+ * two envs per workgroup: one wave per env runs the NPC controller and the car
+ * logic, one wave runs the two egos' kinematics, status and LiDAR beside them;
  * automatic (mode 0) for 1024 <= E <= 4096, forced by 3.  mev_get_step_split
  * returns 1 (split) or 2 (early split) when the next step uses it.  Replaces
  * nothing in the reference. */

@@ -1671,7 +1671,7 @@ int mev_set_step_split(mev_handle* h, int32_t mode) {
     if (int r_ = serve_stop(h)) return r_;  // (the server holds the stream)
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->sp.step_split = mode;
-    h->deal_valid = false;  // (the traffic early split deals 4 envs per workgroup: restart the rings)
+    h->deal_valid = false;  // (the traffic early split deals several envs per workgroup: restart the rings)
     return MEV_OK;
 }
 

@@ -284,9 +284,9 @@ __device__ inline int xcd_env(int b, int E) {
 // The env of workgroup b under the NPC-aware deal (kDealLists in mev_kernels.h):
 // list x = b % 8 (the XCD the dispatcher sends b to), rank i = b / 8 in that list's
 // descending NPC-class order, from the counts and orders step t - 1 built.
-// (k = 4 envs per workgroup, the traffic early split: workgroup b takes ranks
-// 4 (b / 8) + j, j < 4, of its list; every list holds E / 8 envs whichever kernel
-// built it, so any E divisible by 32 keeps the deal a bijection)
+// (k envs per workgroup, the traffic early split (kTsplitEnvs): workgroup b takes
+// ranks k (b / 8) + j, j < k, of its list; every list holds E / 8 envs whichever
+// kernel built it, so any E divisible by 8 k keeps the deal a bijection)
 // cls (optional): the env's NPC class in the deal, i.e. its NPC count after the previous
 // step (kDealClasses - 1: that many or more)
 __device__ inline int deal_env(const SimParams& p, int ring, int b, int k = 1, int j = 0, int* cls = nullptr) {
@@ -3391,18 +3391,27 @@ __device__ __forceinline__ void deal_append(const SimParams& p, const StepInputs
 constexpr int kSplitWpe = 4;
 constexpr int kEsplitWpe = 8;
 // the traffic early split: kTsplitEnvs envs (car waves) + one LiDAR wave per workgroup,
-// kTsplitWpe waves per SIMD (config 4: 4096 envs -> 5120 waves on 1024 SIMDs)
-constexpr int kTsplitEnvs = 4;
+// kTsplitWpe waves per SIMD (config 4: 4096 envs -> 6144 waves on 1024 SIMDs).  Two envs,
+// not four: the LiDAR wave's march of its egos' beams, which the light envs' car waves wait
+// for at barrier H, halves -- config 4 148.4 -> 150.8 M, 1024 / 2048 / 3072 envs 2-4 %
+// faster (profiles/r6_ab_ts2_*.txt; variant builds ts2* via MEV_TSPLIT_ENVS)
+#ifndef MEV_TSPLIT_ENVS
+#define MEV_TSPLIT_ENVS 2
+#endif
+constexpr int kTsplitEnvs = MEV_TSPLIT_ENVS;
 // the traffic early split's LiDAR wave issues at level 1 (its ego phase 1 and road march
 // have slack beside a heavy env's NPC phase, which sets the kernel's end): config 4
 // 143.4 -> 151.2 M against level 3 (profiles/r5_ab_tsprio*_cfg4.txt, four rounds; 2: 149 M,
 // 0: 150 M)
-constexpr int kPrioTsplitLidar = 1;
+#ifndef MEV_TSPLIT_LPRIO
+#define MEV_TSPLIT_LPRIO 1
+#endif
+constexpr int kPrioTsplitLidar = MEV_TSPLIT_LPRIO;
 constexpr int kTsplitRays = kFixedRays;  // LiDAR pool beams per env
-// (6, not the 5 that 1024 five-wave workgroups need on 1024 SIMDs: a workgroup's five waves
-// do not spread evenly over a CU's four SIMDs, and at a 5-wave budget (93 VGPRs) 4096 envs
-// did not fit one residency round -- 38.3 us against 28.7 us at 3072 envs; at 80 VGPRs
-// they do, profiles/r5_ts_wpe_cfg4.txt)
+// (6: 2048 three-wave workgroups at 4096 envs, all resident at once.  With four envs per
+// workgroup a 5-wave budget (93 VGPRs) did not fit 4096 envs in one residency round --
+// five waves do not spread evenly over a CU's four SIMDs: 38.3 us against 28.7 us at 3072
+// envs; at 80 VGPRs they did, profiles/r5_ts_wpe_cfg4.txt)
 constexpr int kTsplitWpe = 6;
 constexpr int kPrioEsplitRoad = 3;
 constexpr int kPrioEsplitCars = 2;

@@ -287,7 +287,7 @@ TRAFFIC_ONE_EGO = [c for c in CONFIGS if c.get("traffic") and c["n"] == 1 and no
 @pytest.mark.parametrize("cfg", TRAFFIC_ONE_EGO, ids=[c["name"] for c in TRAFFIC_ONE_EGO])
 def test_random_states_match_oracle_traffic_early_split(mev, cfg):
     """The traffic early split (mev_set_step_split(3), one ego and <= 32 NPC slots per
-    env, E divisible by 32: four car waves -- NPC phase and car part of one env each
+    env, E divisible by 16: two car waves -- NPC phase and car part of one env each
     -- and one LiDAR wave for their four egos per workgroup), 32 envs from random
     states: every output and the state after every step bit-exact."""
     _random_states_vs_oracle(mev, cfg, 2, 0, split=3, max_npcs=32, E=32)

@@ -91,8 +91,8 @@ TRAFFIC_ONE_EGO = [n for n in SINGLE if G.load(n)["meta"]["traffic"] and G.load(
 
 @pytest.mark.parametrize("name", TRAFFIC_ONE_EGO)
 def test_golden_scenario_traffic_early_split(mev, name):
-    """The traffic early split (four car waves -- NPC phase and car part of one env
-    each -- and one LiDAR wave for their egos per workgroup; E divisible by 32): each
+    """The traffic early split (two car waves -- NPC phase and car part of one env
+    each -- and one LiDAR wave for their egos per workgroup; E divisible by 16): each
     one-ego traffic golden replicated into 32 envs, every env bit-exact against the
     reference, with the split asserted to be the path that ran."""
     h = G.make_handle(mev, G.load(name)["meta"], 32)
