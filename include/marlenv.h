@@ -308,7 +308,7 @@ int mev_get_step_pack(const mev_handle* h, int32_t* envs_per_wave);
  * per env, <= 32 NPC slots, R <= 128 and E a multiple of 16, the early split is
  * two envs per workgroup: one wave per env runs the NPC controller and the car
  * logic, one wave runs the two egos' kinematics, status and LiDAR beside them;
- * automatic (mode 0) for 1024 <= E <= 4096, forced by 3.  mev_get_step_split
+ * automatic (mode 0) and by 3.  mev_get_step_split
  * returns 1 (split) or 2 (early split) when the next step uses it.  Replaces
  * nothing in the reference. */
 int mev_set_step_split(mev_handle* h, int32_t mode);

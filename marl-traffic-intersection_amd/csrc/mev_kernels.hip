@@ -3415,6 +3415,10 @@ constexpr int kTsplitRays = kFixedRays;  // LiDAR pool beams per env
 constexpr int kTsplitWpe = 6;
 constexpr int kPrioEsplitRoad = 3;
 constexpr int kPrioEsplitCars = 2;
+#ifndef MEV_TSPLIT_CPRIO
+#define MEV_TSPLIT_CPRIO kPrioEsplitCars
+#endif
+constexpr int kPrioTsplitCars = MEV_TSPLIT_CPRIO;  // the traffic early split's car waves
 constexpr int kPrioEsplitCarPhase = 1;
 // P1 = 1: a LiDAR of a multiple of 64 beams (lidar_body's P1), the configs 3 and 5 kernel
 template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false, int P1 = 0>
@@ -3666,13 +3670,14 @@ constexpr int kSplitMaxWg = 2048;
 // 24.1 -> 22.0 at 2, 2048 x 1 x 64 12.4 -> 10.0 at 2, 4096 x 1 x 128 15.5 -> 14.4 at 2.
 int esplit_pack(const SimParams& p) {
     // traffic: kTsplitEnvs one-ego envs per workgroup (every workgroup full, and the
-    // NPC-aware deal's lists of E / 8 envs split into whole workgroups)
-    // Automatic for 1024 <= E <= 4096 (every workgroup resident at once on the 256 CUs):
-    // config 4 33.3 -> 31.4 us, 1024 / 2048 envs 6-8 % faster; 8192 envs (two residency
-    // rounds) 55.9 -> 59.0 us, so not there (profiles/r5_ab_ts6_cfg4.txt, two rounds).
+    // NPC-aware deal's lists of E / 8 envs split into whole workgroups).  Automatic at
+    // every such E: with two envs per workgroup it beats one wave per env from 16 to
+    // 16384 envs -- 16-512 envs 25-35 %, 8192 envs 145 -> 165 M, 16384 160 -> 190 M
+    // agent-steps/s (profiles/r6_ts2_auto_*.txt).  (Round 5's four envs per workgroup
+    // lost at 8192 envs, 55.9 -> 59.0 us, profiles/r5_ab_ts6_cfg4.txt.)
     if (p.traffic)
         return fixed_fits<1, 32>(p) && p.R <= kTsplitRays && p.E % (8 * kTsplitEnvs) == 0 &&
-                       (p.step_split == 3 || (p.step_split == 0 && p.E >= 1024 && p.E <= 4096))
+                       (p.step_split == 3 || p.step_split == 0)
                    ? kTsplitEnvs
                    : 0;
     if (!fixed_fits<8, 0>(p) || p.N > 8) return 0;

@@ -247,13 +247,13 @@ def test_step_kernel_selection(mev):
     assert tiny.step_kernel() == 2  # automatic: one agent's beams fit one LiDAR wave, one launch
     tiny.close()
     # config 4 shape (1 ego, traffic, 32 NPC slots): fused automatically, as the traffic early
-    # split (two car waves + a LiDAR wave per workgroup) where E is a multiple of 16, >= 1024
+    # split (two car waves + a LiDAR wave per workgroup) where E is a multiple of 16
     t = mev.Handle(num_envs=4096, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32)
     assert t.step_kernel() == 2 and t.step_split() == 2
     t.set_step_split(1)
     assert t.step_split() == 0
     t.close()
-    for e_ in (4088, 992):  # (not a multiple of 16 / below 1024 envs: one wave per env)
+    for e_ in (4088, 1000):  # (not a multiple of 16: one wave per env)
         t = mev.Handle(num_envs=e_, num_agents=1, lidar_rays=64, traffic_flow=1, traffic_density=0.5, max_npcs=32)
         assert t.step_split() == 0, e_
         t.close()

@@ -61,8 +61,9 @@ def run(cfg, steps, warmup, step_kernel=0, pack=0, split=0):
     h.close()
     r = dict(name=cfg["name"], workload=cfg["desc"], agent_steps_per_s=round(E * N / dt, 1),
              ms_per_step=round(dt * 1e3, 5), step_kernel="k_step (fused)" if fused else "k_cars + k_lidar",
-             # traffic early split: four car waves (one env each) + one LiDAR wave per workgroup
-             envs_per_wave=pk, waves_per_workgroup=(5 if cfg.get("traffic") and split == 2 else
+             # traffic early split: two car waves (one env each) + one LiDAR wave per workgroup
+             # (kTsplitEnvs, mev_kernels.hip)
+             envs_per_wave=pk, waves_per_workgroup=(3 if cfg.get("traffic") and split == 2 else
                                                     2 if split else 1),
              mean_npcs=round(npc, 3))
     if fused:
@@ -80,7 +81,7 @@ def main():
     ap.add_argument("--only", default=None, help="comma-separated config names (e.g. cfg4)")
     ap.add_argument("--step-kernel", type=int, default=0, help="0 auto, 1 k_cars + k_lidar, 2 fused k_step")
     ap.add_argument("--pack", type=int, default=0, help="envs per fused wave: 0 auto, 1, 2, 4")
-    ap.add_argument("--split", type=int, default=0, help="two waves per fused workgroup: 0 auto, 1 off, 2 on")
+    ap.add_argument("--split", type=int, default=0, help="mev_set_step_split: 0 auto, 1 off, 2 on, 3 early split")
     ap.add_argument("--envs", type=int, default=0, help="override the configs' env count")
     a = ap.parse_args()
     res = []

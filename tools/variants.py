@@ -47,7 +47,9 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                # ... with its LiDAR wave at issue level 0 / 2 / 3 before barrier H (1 otherwise)
                "ts2p0": ["-DMEV_TSPLIT_ENVS=2", "-DMEV_TSPLIT_LPRIO=0"],
                "ts2p2": ["-DMEV_TSPLIT_ENVS=2", "-DMEV_TSPLIT_LPRIO=2"],
-               "ts2p3": ["-DMEV_TSPLIT_ENVS=2", "-DMEV_TSPLIT_LPRIO=3"]}
+               "ts2p3": ["-DMEV_TSPLIT_ENVS=2", "-DMEV_TSPLIT_LPRIO=3"],
+               # ... with its car waves starting at issue level 1 / 3 (2 otherwise)
+               "tsc1": ["-DMEV_TSPLIT_CPRIO=1"], "tsc3": ["-DMEV_TSPLIT_CPRIO=3"]}
 
 
 def build(name: str, force: bool = False) -> str:
