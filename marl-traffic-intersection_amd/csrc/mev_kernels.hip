@@ -2792,8 +2792,14 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // wave-uniform safe bound; else a chunk holding two agents' beams)
     auto setup = [&](const float4& a, float rel_b, auto small, float2& d, bool uni) -> int {
         float sn, cs;
+#if defined(MEV_EXP_FASTSIN)  // timing-only (wrong results): phase 1's beam directions by the hardware sin/cos
+        sn = __sinf(a.z + rel_b);
+        cs = __cosf(a.z + rel_b);
+        (void)small;
+#else
         if constexpr (decltype(small)::value) sincosf_below120(a.z + rel_b, &sn, &cs);
         else sincosf(a.z + rel_b, &sn, &cs);
+#endif
         const float dx = cs, dy = -sn;
         d = make_float2(dx, dy);
         const int px = (int)a.x, py = (int)a.y;

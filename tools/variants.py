@@ -49,7 +49,10 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                "ts2p2": ["-DMEV_TSPLIT_ENVS=2", "-DMEV_TSPLIT_LPRIO=2"],
                "ts2p3": ["-DMEV_TSPLIT_ENVS=2", "-DMEV_TSPLIT_LPRIO=3"],
                # ... with its car waves starting at issue level 1 / 3 (2 otherwise)
-               "tsc1": ["-DMEV_TSPLIT_CPRIO=1"], "tsc3": ["-DMEV_TSPLIT_CPRIO=3"]}
+               "tsc1": ["-DMEV_TSPLIT_CPRIO=1"], "tsc3": ["-DMEV_TSPLIT_CPRIO=3"],
+               # timing-only: LiDAR phase 1's beam directions by the hardware sin/cos instead of the
+               # glibc-exact double-precision sincosf (the upper bound of a cheaper exact one)
+               "fastsin": ["-DMEV_EXP_FASTSIN"]}
 
 
 def build(name: str, force: bool = False) -> str:
