@@ -295,7 +295,13 @@ def main():
                          "f32 = plain rows")
     ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="untimed steps for this long before the warm-up (SIMD clock ramp from idle); 0 = none")
-    ap.add_argument("--no-kernel-events", action="store_true", help="do not record per-kernel HIP events")
+    ap.add_argument("--kernel-events", action="store_true",
+                    help="record the library's per-kernel HIP events on every --event-every-th timed step (the "
+                         "fused k_step's roofline uses the stream events around the timed region instead; the "
+                         "sampled events add launch latency inside it: +0.9 us per step at 20 steps, "
+                         "profiles/r6_events_ab.txt).  Always on for the two-kernel path, whose per-kernel "
+                         "times need them")
+    ap.add_argument("--no-kernel-events", action="store_true", help="never record per-kernel HIP events")
     ap.add_argument("--event-every", type=int, default=50, help="record the per-kernel events on every n-th step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--step-kernel", type=int, default=0,
@@ -392,7 +398,9 @@ def main():
     for t in range(W):
         step(t)
     torch.cuda.synchronize(dev)
-    if not args.no_kernel_events:
+    fused = env.step_kernel() == 2  # one k_step launch per step (else k_cars + k_lidar)
+    kernel_events = (args.kernel_events or not fused) and not args.no_kernel_events
+    if kernel_events:
         env.kernel_timing(args.event_every)
     barrier()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -405,8 +413,7 @@ def main():
     elapsed = time.perf_counter() - t0
     stream_ms = ev0.elapsed_time(ev1) / K
     cars_ms = lidar_ms = None
-    fused = env.step_kernel() == 2  # one k_step launch per step (else k_cars + k_lidar)
-    if not args.no_kernel_events:
+    if kernel_events:
         c_sum, l_sum, n_steps = env.kernel_times()
         assert n_steps == (K + args.event_every - 1) // args.event_every, (n_steps, K)
         cars_ms, lidar_ms = c_sum / n_steps, l_sum / n_steps
