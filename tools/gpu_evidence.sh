@@ -36,7 +36,7 @@ if [ "$what" = bench ] || [ "$what" = all ]; then
   cut -c1-200 $OUT/kernel_stats.csv
   timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
   cat $OUT/bench.json
-  timeout -k 10 300 python bench.py --no-kernel-events --no-cpu-baseline > $OUT/bench_noevents.json 2>> $OUT/bench.err
+  timeout -k 10 300 python bench.py --kernel-events --no-cpu-baseline > $OUT/bench_events.json 2>> $OUT/bench.err
 fi
 if [ "$what" = sweep ] || [ "$what" = all ]; then
   timeout -k 10 300 python tools/bench_sweep.py --out $OUT/sweep.json > $OUT/sweep.txt 2>&1
