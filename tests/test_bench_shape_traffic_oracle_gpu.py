@@ -19,7 +19,7 @@ import oracle_replay as R
 
 pytestmark = pytest.mark.gpu
 
-E, N, RAYS, T, MAXS, DENSITY, SEED, DT = 4096, 1, 64, 300, 2000, 0.5, 3, 1.0 / 60.0
+N, RAYS, T, MAXS, DENSITY, SEED, DT = 1, 64, 300, 2000, 0.5, 3, 1.0 / 60.0
 META = dict(rays=RAYS, obs_dim=31 + RAYS, num_lanes=3, n_agents=N, use_team=False, respawn=True, max_steps=MAXS,
             traffic=True, density=DENSITY, reward=[10.0, 1.0, -0.01, -10.0, -5.0, 10.0, -0.02, 0.2])
 M32 = 0xFFFFFFFF
@@ -46,7 +46,10 @@ def spawn_draw(ctr, e, prob, nroutes):
     return int((a1 * nroutes) >> 32) if u < prob else -1
 
 
-def test_config4_full_size_sampled_envs_match_oracle(mev):
+@pytest.mark.parametrize("E", [4096, 8192])
+def test_config4_full_size_sampled_envs_match_oracle(mev, E):
+    """E = 8192: the traffic early split over two residency rounds of workgroups (automatic
+    since round 6), the deal's later workgroups starting while earlier ones have appended."""
     import torch
 
     libm = ctypes.CDLL("libm.so.6")
