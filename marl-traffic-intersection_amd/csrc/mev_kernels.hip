@@ -89,7 +89,10 @@ constexpr int kPrioP3 = 0;
 // With traffic: issue priority of the NPC controller by the NPCs an env has to
 // control (level = NPCs / kNpcPrio, capped at 3).  The env with the most NPCs is
 // the kernel's critical path (config 4: k_cars 53.9 -> 48.3 us).
-constexpr int kNpcPrio = 2;
+#ifndef MEV_NPC_PRIO
+#define MEV_NPC_PRIO 2
+#endif
+constexpr int kNpcPrio = MEV_NPC_PRIO;
 
 // --------------------------------------------------------------- helpers ---
 // A pointer the kernel reads through SimParams as a global-memory pointer.  The

@@ -52,7 +52,9 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                "tsc1": ["-DMEV_TSPLIT_CPRIO=1"], "tsc3": ["-DMEV_TSPLIT_CPRIO=3"],
                # timing-only: LiDAR phase 1's beam directions by the hardware sin/cos instead of the
                # glibc-exact double-precision sincosf (the upper bound of a cheaper exact one)
-               "fastsin": ["-DMEV_EXP_FASTSIN"]}
+               "fastsin": ["-DMEV_EXP_FASTSIN"],
+               # the NPC controller's issue level = NPCs / 1 or / 3 (2 otherwise)
+               "npcp1": ["-DMEV_NPC_PRIO=1"], "npcp3": ["-DMEV_NPC_PRIO=3"]}
 
 
 def build(name: str, force: bool = False) -> str:
