@@ -2928,6 +2928,9 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
 #endif
 
     if (PART == 0) __builtin_amdgcn_s_setprio(kPrioP2);
+#if defined(MEV_EXP_TSNOMARCH)  // timing-only (wrong results): the early splits' first part without its march
+    if constexpr (PART == 1) return;
+#endif
     // ---- phase 2: pooled road + screen march of the queued beams
     // (Lidar.cpp:31-48, first stop wins): LIDAR_NPR exact probes, then a jump
     // over the provably safe stretch after the last one

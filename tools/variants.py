@@ -54,7 +54,10 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                # glibc-exact double-precision sincosf (the upper bound of a cheaper exact one)
                "fastsin": ["-DMEV_EXP_FASTSIN"],
                # the NPC controller's issue level = NPCs / 1 or / 3 (2 otherwise)
-               "npcp1": ["-DMEV_NPC_PRIO=1"], "npcp3": ["-DMEV_NPC_PRIO=3"]}
+               "npcp1": ["-DMEV_NPC_PRIO=1"], "npcp3": ["-DMEV_NPC_PRIO=3"],
+               # timing-only: the early splits' LiDAR waves without their road march before barrier H / B
+               # (what the light workgroups' wait for it costs config 4 at most)
+               "tsnomarch": ["-DMEV_EXP_TSNOMARCH"]}
 
 
 def build(name: str, force: bool = False) -> str:
