@@ -1043,7 +1043,11 @@ __device__ int npc_phase(const SimParams& p, const StepInputs& in, int e, int cn
     NT(3);  // round A: moves
     unsigned long long done_m = alive_k;  // NPCs whose round-A move is final
     int kseq = cnt;                       // the first NPC left to the sequential turns
+#if defined(MEV_EXP_NOROUNDB)  // timing-only (wrong results): round A's moves taken as final
+    if (false) {
+#else
     if (__popcll(alive_k) >= 2) {
+#endif
         plan_all(true, nl.thr_b);
         const bool differs = lane < cnt && ((alive_k >> lane) & 1ull) &&
                              __float_as_uint(nl.thr_a[lane < cnt ? lane : 0]) !=

@@ -57,7 +57,9 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                "npcp1": ["-DMEV_NPC_PRIO=1"], "npcp3": ["-DMEV_NPC_PRIO=3"],
                # timing-only: the early splits' LiDAR waves without their road march before barrier H / B
                # (what the light workgroups' wait for it costs config 4 at most)
-               "tsnomarch": ["-DMEV_EXP_TSNOMARCH"]}
+               "tsnomarch": ["-DMEV_EXP_TSNOMARCH"],
+               # timing-only: the NPC controller without its round B (round A's moves final): its share
+               "noroundb": ["-DMEV_EXP_NOROUNDB"]}
 
 
 def build(name: str, force: bool = False) -> str:
