@@ -543,9 +543,10 @@ def main():
             tab = 'true' if dist_table_needed() else 'false'
             # the instantiation launch_fused picks at this shape (rocprofv3 prints the same arguments:
             # TRAFFIC, TAB, NM, KM, PK, SPLIT, ESPLIT, P1 -- one env per wave, no split at >= 2048
-            # workgroups; in the 8-slot layout P1 = 1 for a multiple of 64 beams, else 2)
+            # workgroups; in the 8-slot layout P1 = the beam count for 64 / 96 / 128 beams, else 1 for a multiple
+            # of 64, 2 otherwise)
             fixed8 = N_AGENTS <= 8 and RAYS <= 128
-            p1 = (1 if RAYS % 64 == 0 else 2) if fixed8 else 0
+            p1 = (RAYS if RAYS in (64, 96, 128) else (1 if RAYS % 64 == 0 else 2)) if fixed8 else 0
             kname = f"mev::k_step<false, {tab}, {8 if fixed8 else 0}, 64, 1, false, false, {p1}>"
             roofline = {
                 "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",

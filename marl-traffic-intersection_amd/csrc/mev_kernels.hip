@@ -2697,13 +2697,14 @@ struct LidarSrcLdsEnvs {
 #define MEV_DENSE_ILP 2
 #endif
 // P1 = 1: R is a multiple of 64 (the dense phase-1 walk below is not compiled in); P1 = 2: R is
-// not (the dense walk for every pool, the agent-pair loop not compiled in).
+// not (the dense walk for every pool, the agent-pair loop not compiled in); P1 >= 64: R = P1, a
+// compile-time beam count (64: config 3, 96: the reference's default LiDAR, 128: config 5).
 template <bool TAB, int ILP, class Src, int NPT = LIDAR_NPR, bool HELP = false, int PART = 0, int P1 = 0>
 __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& out, const Src& src, const int G,
                                            const int a0, const int na, const int lane, unsigned char* base,
                                            const LidarLayout& lay, const unsigned long long redo = 0ull,
                                            const unsigned long long alive_in = 0ull) {
-    const int R = p.R;
+    const int R = P1 >= WAVE ? P1 : p.R;  // (P1 >= 64: exactly that many beams, a compile-time count)
     float4* ag = reinterpret_cast<float4*>(base + lay.ag);
     float2* dir = reinterpret_cast<float2*>(base + lay.dir);
     int* res = reinterpret_cast<int*>(base + lay.res);
@@ -2851,7 +2852,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     // next chunk, ILP chunks per pass; R = 96 takes 6 chunks per 4 agents, not 8
     // half-empty ones.  (One loop for both measured 2 % slower at config 3: the chunk
     // walk's bookkeeping and the offsets' LDS reads in front of every pass.)
-    const bool dense = P1 == 2 || (P1 == 0 && (R & (WAVE - 1)) != 0 && nal > 1);
+    const bool dense = P1 >= WAVE ? (P1 & (WAVE - 1)) != 0 : (P1 == 2 || (P1 == 0 && (R & (WAVE - 1)) != 0 && nal > 1));
     auto phase1 = [&](auto small) {
         if constexpr (PART == 2) {  // the respawned agents only
             for (unsigned long long tm = redo; tm; tm &= tm - 1ull) pass1_one(small, __builtin_ctzll(tm));
@@ -3437,8 +3438,8 @@ constexpr int kPrioEsplitCars = 2;
 #endif
 constexpr int kPrioTsplitCars = MEV_TSPLIT_CPRIO;  // the traffic early split's car waves
 constexpr int kPrioEsplitCarPhase = 1;
-// P1 = 1: a LiDAR of a multiple of 64 beams (lidar_body's P1), the configs 3 and 5 kernel; 2: of
-// other beam counts (96: the reference's default LiDAR)
+// P1 (lidar_body's): 1 a LiDAR of a multiple of 64 beams, 2 of another beam count, >= 64 exactly P1
+// beams (64: config 3, 96: the reference's default LiDAR, 128: config 5)
 template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false, int P1 = 0>
 __global__ __launch_bounds__((TRAFFIC && ESPLIT) ? (PK + 1) * WAVE : (SPLIT ? 2 * WAVE : WAVE),
                              (TRAFFIC && ESPLIT) ? kTsplitWpe
@@ -3763,6 +3764,12 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if (p.R == 64)
+            hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 64>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if (p.R == 96)
+            hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 96>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if (p.R == 128)
+            hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 128>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if ((p.R & (WAVE - 1)) == 0)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 1>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 2>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
