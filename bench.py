@@ -547,7 +547,8 @@ def main():
             # of 64, 2 otherwise)
             fixed8 = N_AGENTS <= 8 and RAYS <= 128
             p1 = (RAYS if RAYS in (64, 96, 128) else (1 if RAYS % 64 == 0 else 2)) if fixed8 else 0
-            kname = f"mev::k_step<false, {tab}, {8 if fixed8 else 0}, 64, 1, false, false, {p1}>"
+            nc = 8 if fixed8 and p1 >= 64 and N_AGENTS == 8 else 0  # (compile-time agents per env)
+            kname = f"mev::k_step<false, {tab}, {8 if fixed8 else 0}, 64, 1, false, false, {p1}, {nc}>"
             roofline = {
                 "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic_of.get("k_step"),

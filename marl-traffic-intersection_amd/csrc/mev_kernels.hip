@@ -1747,7 +1747,7 @@ __device__ __forceinline__ void ego_phase1(const SimParams& p, const StepInputs&
 // SAT.  The NPC phase's spawn test reads the ego's start-of-step position, which this wave
 // keeps in envw[0..1] (the LiDAR wave overwrites el.x / el.y with the moved pose).
 template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool EARLY = false, bool ESPLIT = false, bool DIMS = false,
-          bool TSC = false>
+          bool TSC = false, int NC = 0>
 __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs& in, const Outputs& out, const int e,
                                             const CarsLDS& el, NL* nl, int npc_cls = kDealClasses - 1) {
     static_assert(!ESPLIT || FUSED, "early split: k_step");
@@ -1766,7 +1766,7 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     // memory is touched in two dependent rounds (state, then route table) and
     // written once at the end.
     const int tid = threadIdx.x & (WAVE - 1);
-    const int NE = p.N;  // agents per env
+    const int NE = NC ? NC : p.N;  // agents per env (NC: the kernel's compile-time count)
     // PK > 1 (k_step, few agents per env): the wave steps envs e .. e + npk - 1;
     // agent slot i is agent i % NE of env e + i / NE, global agent e * NE + i
     // (consecutive envs are consecutive in the SoA).  N: the wave's agent slots.
@@ -2193,11 +2193,11 @@ __device__ __forceinline__ unsigned long long ts_ego_phase(const SimParams& p, c
 // k_cars): bonuses, team mix and env flags (:320-370), the reward / done /
 // status outputs and the state write-back, the observation head (:418-520).
 // Reads only the car LDS (the LiDAR never writes it).
-template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool DIMS = false>
+template <bool TRAFFIC, bool FUSED, class NL, int PK = 1, bool DIMS = false, int NC = 0>
 __device__ __forceinline__ void cars_post(const SimParams& p, const Outputs& out, const int e, const CarsLDS& el,
                                           const NL* nl, CarsCtx& cx) {
     const int tid = threadIdx.x & (WAVE - 1);
-    const int NE = p.N;  // agents per env (PK > 1: see cars_pre)
+    const int NE = NC ? NC : p.N;  // agents per env (PK > 1: see cars_pre; NC: compile-time)
     const int npk = PK == 1 ? 1 : (p.E - e < PK ? p.E - e : PK);
     const int N = PK == 1 ? NE : npk * NE;
     const int step_no = cx.step_no, ncnt = cx.ncnt;
@@ -3440,7 +3440,8 @@ constexpr int kPrioTsplitCars = MEV_TSPLIT_CPRIO;  // the traffic early split's 
 constexpr int kPrioEsplitCarPhase = 1;
 // P1 (lidar_body's): 1 a LiDAR of a multiple of 64 beams, 2 of another beam count, >= 64 exactly P1
 // beams (64: config 3, 96: the reference's default LiDAR, 128: config 5)
-template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false, int P1 = 0>
+template <bool TRAFFIC, bool TAB, int NM, int KM = MAXK, int PK = 1, bool SPLIT = false, bool ESPLIT = false, int P1 = 0,
+          int NC = 0>
 __global__ __launch_bounds__((TRAFFIC && ESPLIT) ? (PK + 1) * WAVE : (SPLIT ? 2 * WAVE : WAVE),
                              (TRAFFIC && ESPLIT) ? kTsplitWpe
                                                  : ((ESPLIT && PK == 1) ? kEsplitWpe : (SPLIT ? kSplitWpe : 4))) void k_step(
@@ -3469,7 +3470,7 @@ __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? kSplitWpe : 4) voi
     __shared__ uint32_t cmdw[kServeLine];
     constexpr int PK = 1;
     constexpr bool ESPLIT = false;
-    constexpr int P1 = 0;
+    constexpr int P1 = 0, NC = 0;
     const int lane = threadIdx.x & (WAVE - 1);
     const bool w0 = threadIdx.x < WAVE;
     ServeBox* box = sa.box;
@@ -3764,10 +3765,16 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if (p.R == 64 && p.N == 8)
+            hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 64, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (p.R == 64)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 64>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if (p.R == 96 && p.N == 8)
+            hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 96, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (p.R == 96)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 96>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
+        else if (p.R == 128 && p.N == 8)
+            hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 128, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (p.R == 128)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 128>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if ((p.R & (WAVE - 1)) == 0)
