@@ -3750,6 +3750,8 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         const int wg = (p.E + pk - 1) / pk;
         if (step_esplit(p)) {  // early split: a car wave and a LiDAR wave per workgroup
             if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (pk == 4 && p.N == 1)  // (config 2: one agent per env at compile time)
+                hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true, 0, 1>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
