@@ -2705,6 +2705,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
                                            const LidarLayout& lay, const unsigned long long redo = 0ull,
                                            const unsigned long long alive_in = 0ull) {
     const int R = P1 >= WAVE ? P1 : p.R;  // (P1 >= 64: exactly that many beams, a compile-time count)
+    const int LS = P1 >= WAVE ? P1 : p.lidar_slots;  // (and every beam in the observation: fixed_r)
     float4* ag = reinterpret_cast<float4*>(base + lay.ag);
     float2* dir = reinterpret_cast<float2*>(base + lay.dir);
     int* res = reinterpret_cast<int*>(base + lay.res);
@@ -2729,12 +2730,12 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         for (int j = 0; j < na; ++j) {
             if ((am >> j) & 1ull) continue;
             if (out.lidar_u8) {  // compact gather format: the dead-agent code
-                uint8_t* crow = out.lidar_u8 + (size_t)(a0 + j) * p.lidar_slots;
-                for (int b = lane; b < p.lidar_slots; b += WAVE) crow[b] = (uint8_t)kLidarCodeDead;
+                uint8_t* crow = out.lidar_u8 + (size_t)(a0 + j) * LS;
+                for (int b = lane; b < LS; b += WAVE) crow[b] = (uint8_t)kLidarCodeDead;
                 continue;
             }
             float* row = out.obs + (size_t)(a0 + j) * out.obs_ld + OBS_HEAD;
-            for (int b = lane; b < p.lidar_slots; b += WAVE) row[b] = 0.0f;
+            for (int b = lane; b < LS; b += WAVE) row[b] = 0.0f;
         }
     }
     wave_lds_sync();
@@ -3219,19 +3220,19 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
     if (out.lidar_u8) {  // compact gather format: one code per beam (0 no hit, k + 1 hit at probe k)
         for (int j = 0; j < nal; ++j) {
             const int g = __float_as_int(ag[j].w);
-            uint8_t* crow = out.lidar_u8 + (size_t)g * p.lidar_slots;
-            for (int b = lane; b < p.lidar_slots; b += WAVE) {
+            uint8_t* crow = out.lidar_u8 + (size_t)g * LS;
+            for (int b = lane; b < LS; b += WAVE) {
                 const int r = res[j * R + b];
                 crow[b] = (uint8_t)((r & 1) ? (r >> 1) + 1 : 0);
             }
         }
         return;
     }
-    if (p.lidar_slots <= WAVE) {
+    if (LS <= WAVE) {
         // lane = beam: the agents' global indices come from one LDS read (readlane per
         // row) and 8 rows' results are read before any is stored (one LDS wait per 8 rows)
         const int gl = lane < nal ? __float_as_int(ag[lane].w) : 0;
-        const bool beam = lane < p.lidar_slots;
+        const bool beam = lane < LS;
         // (the LiDAR constants read once and pinned in VGPRs by one asm: the compiler cannot
         // rematerialize an asm result, so it stops re-issuing their scalar loads for every
         // row -- three dependent scalar-cache round trips per row)
@@ -3257,7 +3258,7 @@ __device__ __forceinline__ void lidar_body(const SimParams& p, const Outputs& ou
         for (int j = 0; j < nal; ++j) {
             const int g = __float_as_int(ag[j].w);
             float* row = out.obs + (size_t)g * out.obs_ld + OBS_HEAD;
-            for (int b = lane; b < p.lidar_slots; b += WAVE)
+            for (int b = lane; b < LS; b += WAVE)
                 row[b] = ((res[j * R + b] & 1) ? march_dist<TAB>(p, res[j * R + b] >> 1) : p.lidar_max) * p.lidar_inv;
         }
     }
@@ -3725,6 +3726,12 @@ bool step_split(const SimParams& p) {
     return (p.E + pk - 1) / pk <= kSplitMaxWg;
 }
 
+// the beam count a k_step instantiation fixes at compile time (its P1): 64, 96 or 128
+// beams, every one in the observation; else 0
+static int fixed_r(const SimParams& p) {
+    return (p.R == 64 || p.R == 96 || p.R == 128) && p.lidar_slots == p.R ? p.R : 0;
+}
+
 template <bool TAB>
 static void launch_fused(const SimParams& p, const SimParams* dp, const StepInputs& in, const Outputs& out,
                          hipStream_t s) {
@@ -3734,8 +3741,12 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
             if (step_esplit(p)) {  // the traffic early split: kTsplitEnvs car waves + a LiDAR wave
                 constexpr int P = kTsplitEnvs;
                 const unsigned tl = (unsigned)(P * FixedLayout<1, 32>::lidar + lidar_layout_beams(P, P * kTsplitRays, 32, false).bytes);
-                hipLaunchKernelGGL((k_step<true, TAB, 1, 32, P, true, true>), dim3(p.E / P), dim3((P + 1) * WAVE), tl, s,
-                                   dp, in, out);
+                if (fixed_r(p) == 64)  // (config 4: the beam count at compile time)
+                    hipLaunchKernelGGL((k_step<true, TAB, 1, 32, P, true, true, 64>), dim3(p.E / P), dim3((P + 1) * WAVE), tl,
+                                       s, dp, in, out);
+                else
+                    hipLaunchKernelGGL((k_step<true, TAB, 1, 32, P, true, true>), dim3(p.E / P), dim3((P + 1) * WAVE), tl, s,
+                                       dp, in, out);
                 return;
             }
             hipLaunchKernelGGL((k_step<true, TAB, 1, 32>), dim3(p.E), dim3(WAVE), lds, s, dp, in, out);
@@ -3748,9 +3759,12 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         const unsigned lds = (unsigned)FixedLayout<8>::bytes;
         const int pk = step_pack(p);
         const int wg = (p.E + pk - 1) / pk;
+        const int fr = fixed_r(p);
         if (step_esplit(p)) {  // early split: a car wave and a LiDAR wave per workgroup
             if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
-            else if (pk == 4 && p.N == 1)  // (config 2: one agent per env at compile time)
+            else if (pk == 4 && p.N == 1 && fr == 64)  // (config 2: agents per env and beams at compile time)
+                hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true, 64, 1>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (pk == 4 && p.N == 1)
                 hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true, 0, 1>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
@@ -3767,17 +3781,17 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
         if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
-        else if (p.R == 64 && p.N == 8)
+        else if (fr == 64 && p.N == 8)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 64, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
-        else if (p.R == 64)
+        else if (fr == 64)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 64>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
-        else if (p.R == 96 && p.N == 8)
+        else if (fr == 96 && p.N == 8)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 96, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
-        else if (p.R == 96)
+        else if (fr == 96)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 96>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
-        else if (p.R == 128 && p.N == 8)
+        else if (fr == 128 && p.N == 8)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 128, 8>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
-        else if (p.R == 128)
+        else if (fr == 128)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 128>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
         else if ((p.R & (WAVE - 1)) == 0)
             hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, false, false, 1>), dim3(wg), dim3(WAVE), lds, s, dp, in, out);
