@@ -2103,7 +2103,8 @@ __device__ __forceinline__ CarsCtx cars_pre(const SimParams& p, const StepInputs
     for (int pbase = 0; pbase < N * nob; pbase += WAVE) {
         const int pi = pbase + tid;
         const bool small = N <= 8 && nob <= 8;  // lane = 8a + o, no integer division
-        const int a = small ? (tid >> 3) : pi / nob, o = small ? (tid & 7) : pi - a * nob;
+        // (nob > 0 inside the loop; the guard only keeps a compile-time N = 1 from a division by zero)
+        const int a = small ? (tid >> 3) : pi / (nob > 0 ? nob : 1), o = small ? (tid & 7) : pi - a * nob;
         if (small ? (a < N && o < nob) : pi < N * nob) {
             const float cx = el.x[a], cy = el.y[a];
             if (o != a && (PK == 1 || a / NE == o / NE) && el.alive[a] &&
@@ -3465,13 +3466,13 @@ __global__ __launch_bounds__((TRAFFIC && ESPLIT) ? (PK + 1) * WAVE : (SPLIT ? 2 
 // launch a new instance; that instance starts from done[b] and never serves a
 // command twice.  Every wave reaches the exit: the poll loop is bounded by the
 // clock, a step by its own work.
-template <bool TRAFFIC, bool TAB, int NM, int KM, bool SPLIT>
+template <bool TRAFFIC, bool TAB, int NM, int KM, bool SPLIT, int SP1 = 0, int SNC = 0>
 __global__ __launch_bounds__(SPLIT ? 2 * WAVE : WAVE, SPLIT ? kSplitWpe : 4) void k_serve(
     const SimParams* __restrict__ pp, ServeArgs sa, Outputs out) {
     __shared__ uint32_t cmdw[kServeLine];
     constexpr int PK = 1;
     constexpr bool ESPLIT = false;
-    constexpr int P1 = 0, NC = 0;
+    constexpr int P1 = SP1, NC = SNC;  // (the beams and agents per env at compile time, as in k_step)
     const int lane = threadIdx.x & (WAVE - 1);
     const bool w0 = threadIdx.x < WAVE;
     ServeBox* box = sa.box;
@@ -3843,8 +3844,18 @@ hipError_t launch_serve(const SimParams& p, const SimParams* dp, const ServeArgs
         else hipLaunchKernelGGL((k_serve<true, false, 0, 64, false>), dim3(p.E), dim3(WAVE), lds, s, dp, sa, out);
     } else {
         const unsigned lds = (unsigned)FixedLayout<8>::bytes;
-        if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true>), dim3(p.E), dim3(2 * WAVE), lds, s, dp, sa, out);
-        else hipLaunchKernelGGL((k_serve<false, false, 8, MAXK, true>), dim3(p.E), dim3(2 * WAVE), lds, s, dp, sa, out);
+        // (env.py's common shapes with their counts at compile time: one agent, 8 agents x 64 beams)
+        const dim3 g(p.E), b(2 * WAVE);
+        if (p.N == 1) {
+            if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true, 0, 1>), g, b, lds, s, dp, sa, out);
+            else hipLaunchKernelGGL((k_serve<false, false, 8, MAXK, true, 0, 1>), g, b, lds, s, dp, sa, out);
+        } else if (p.N == 8 && fixed_r(p) == 64) {
+            if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true, 64, 8>), g, b, lds, s, dp, sa, out);
+            else hipLaunchKernelGGL((k_serve<false, false, 8, MAXK, true, 64, 8>), g, b, lds, s, dp, sa, out);
+        } else {
+            if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true>), g, b, lds, s, dp, sa, out);
+            else hipLaunchKernelGGL((k_serve<false, false, 8, MAXK, true>), g, b, lds, s, dp, sa, out);
+        }
     }
     return hipGetLastError();
 }
