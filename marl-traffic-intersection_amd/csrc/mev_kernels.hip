@@ -3776,6 +3776,8 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
             if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (p.N == 8 && fr == 64)  // (config 3's shape in smaller batches)
+                hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, false, 64, 8>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (p.N == 1)  // (config 1: one agent per env at compile time)
                 hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, false, 0, 1>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
