@@ -282,8 +282,10 @@ int mev_kernel_times(mev_handle* h, double* cars_ms, double* lidar_ms, int64_t* 
  * 1 = k_cars (one wave per env) then k_lidar (one wave per group of agents),
  * with the obstacle table handed over through HBM; 2 = the fused k_step, one
  * wave per env running both parts back to back from its LDS; 0 = automatic
- * (fused for E >= 1024 when its LDS -- car tables, NPC slots in traffic mode,
- * one LiDAR pool -- fits a wave's 10 KB share at 4 waves per SIMD).  Asked for
+ * (fused when its LDS -- car tables, NPC slots in traffic mode, one LiDAR pool
+ * -- fits a wave's 10 KB share at 4 waves per SIMD, and E >= 1024 or an env's
+ * beams fit one LiDAR group (N * R <= 256) or, without traffic, N <= 8 agents
+ * and R <= 128 beams).  Asked for
  * explicitly, the fused kernel runs whenever that LDS fits one workgroup
  * (64 KB); otherwise the call fails with MEV_E_INVALID.  mev_get_step_kernel returns the kernel
  * the next step will use (1 or 2).  Replaces nothing in the reference (its

@@ -3652,12 +3652,16 @@ int step_kernel_for(const SimParams& p) {
     const bool fusable = fused_fits(p);
     if (p.step_kernel == 1) return 1;
     if (p.step_kernel == 2) return fusable ? 2 : 0;
-    // auto: fused once the batch fills the chip with one wave per env (>= 4 per CU)
-    // and a wave's LDS leaves 4 waves per SIMD; smaller batches keep the LiDAR's
-    // finer per-group waves -- unless an env's beams fit one k_lidar group anyway
-    // (N * R <= 256), where the second launch buys nothing (1 env x 1 agent: 70 ->
-    // 82 k steps/s fused)
-    return (fusable && fused_lds_bytes(p) <= 10 * 1024 && (p.E >= 1024 || p.N * p.R <= 256)) ? 2 : 1;
+    // auto: fused when a wave's LDS leaves 4 waves per SIMD and either the batch fills
+    // the chip with one wave per env (>= 4 per CU), or an env's beams fit one k_lidar
+    // group anyway (N * R <= 256: the second launch buys nothing, 1 env x 1 agent 70 ->
+    // 82 k steps/s fused), or the env fits the compile-time 8-slot layout: its k_step
+    // (two waves per env below 2048 workgroups, counts at compile time) beats the
+    // LiDAR's finer per-group waves at every batch size since round 6 (8 agents x 64
+    // beams: 64 envs 21.2 -> 16.7 us, 768 envs 27.2 -> 18.3 us; profiles/r6_stepk_small.txt).
+    // Larger envs at small batches keep the two-kernel path.
+    const bool small_env = p.N * p.R <= 256 || (!p.traffic && fixed_fits<8, 0>(p));
+    return (fusable && fused_lds_bytes(p) <= 10 * 1024 && (p.E >= 1024 || small_env)) ? 2 : 1;
 }
 
 // envs per k_step wave (1, 2 or 4) for a handle without traffic whose N agents

@@ -239,10 +239,13 @@ def test_step_kernel_selection(mev):
     assert h.step_kernel() == 2
     h.close()
     small = _handle(mev, num_envs=64)
-    assert small.step_kernel() == 1  # automatic: finer LiDAR waves for small batches (8 agents x 64 beams)
-    small.set_step_kernel(2)
-    assert small.step_kernel() == 2
+    assert small.step_kernel() == 2  # automatic: the 8-slot fused kernel at every batch size (8 agents x 64 beams)
+    small.set_step_kernel(1)
+    assert small.step_kernel() == 1
     small.close()
+    big = mev.Handle(num_envs=64, num_agents=12, lidar_rays=64)
+    assert big.step_kernel() == 1  # automatic: finer LiDAR waves for small batches of larger envs
+    big.close()
     tiny = mev.Handle(num_envs=1, num_agents=1, lidar_rays=16)
     assert tiny.step_kernel() == 2  # automatic: one agent's beams fit one LiDAR wave, one launch
     tiny.close()
