@@ -3285,13 +3285,14 @@ __global__ __launch_bounds__(256, 8) void k_lidar(SimParams p, Outputs out, int 
 // most 512 beams, balanced (all N in one pool at config 3; 8 x 96 beams as 4 + 4
 // agents, 384 beams each, not 5 + 3: each pool's march ends on its longest beams,
 // and 4 agents of 96 beams fill six whole 64-lane chunks in phase 1).
-__host__ __device__ inline int step_pool(const SimParams& p) {
-    int g = 512 / (p.R > 0 ? p.R : 1);
+__host__ __device__ constexpr int step_pool_n(int N, int R) {
+    int g = 512 / (R > 0 ? R : 1);
     g = g < 1 ? 1 : g;
-    if (g >= p.N) return p.N;
-    const int pools = (p.N + g - 1) / g;
-    return (p.N + pools - 1) / pools;
+    if (g >= N) return N;
+    const int pools = (N + g - 1) / g;
+    return (N + pools - 1) / pools;
 }
+__host__ __device__ inline int step_pool(const SimParams& p) { return step_pool_n(p.N, p.R); }
 
 // LDS of one k_step wave: cars LDS, the staged heads [N][31], the beam offsets
 // [R], the env flags [8], then the LiDAR pool of step_pool(p) agents.
