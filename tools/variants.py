@@ -42,8 +42,8 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                "relaxocc": ["-mllvm", "--amdgpu-schedule-relaxed-occupancy"],
                # the dense phase-1 walk (R not a multiple of 64) at 3 / 4 chunks per pass instead of 2
                "dilp3": ["-DMEV_DENSE_ILP=3"], "dilp4": ["-DMEV_DENSE_ILP=4"],
-               # the traffic early split with 2 envs (car waves) per workgroup instead of 4
-               "ts2": ["-DMEV_TSPLIT_ENVS=2"],
+               # the traffic early split with 2 / 4 envs (car waves) per workgroup
+               "ts2": ["-DMEV_TSPLIT_ENVS=2"], "ts4": ["-DMEV_TSPLIT_ENVS=4"],
                # ... with its LiDAR wave at issue level 0 / 2 / 3 before barrier H (1 otherwise)
                "ts2p0": ["-DMEV_TSPLIT_ENVS=2", "-DMEV_TSPLIT_LPRIO=0"],
                "ts2p2": ["-DMEV_TSPLIT_ENVS=2", "-DMEV_TSPLIT_LPRIO=2"],
