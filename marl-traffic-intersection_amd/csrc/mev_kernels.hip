@@ -3781,8 +3781,12 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
             if (pk == 8) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 8, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
-            else if (p.N == 8 && fr == 64)  // (config 3's shape in smaller batches)
+            else if (p.N == 8 && fr == 64)  // (configs 3 / 5 and 96 beams' shapes in smaller batches)
                 hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, false, 64, 8>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (p.N == 8 && fr == 96)
+                hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, false, 96, 8>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (p.N == 8 && fr == 128)
+                hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, false, 128, 8>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (p.N == 1)  // (config 1: one agent per env at compile time)
                 hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, false, 0, 1>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
@@ -3851,7 +3855,7 @@ hipError_t launch_serve(const SimParams& p, const SimParams* dp, const ServeArgs
         else hipLaunchKernelGGL((k_serve<true, false, 0, 64, false>), dim3(p.E), dim3(WAVE), lds, s, dp, sa, out);
     } else {
         const unsigned lds = (unsigned)FixedLayout<8>::bytes;
-        // (env.py's common shapes with their counts at compile time: one agent, 8 agents x 64 beams)
+        // (env.py's common shapes with their counts at compile time: one agent, 8 agents x 64 / 96 beams)
         const dim3 g(p.E), b(2 * WAVE);
         if (p.N == 1) {
             if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true, 0, 1>), g, b, lds, s, dp, sa, out);
@@ -3859,6 +3863,9 @@ hipError_t launch_serve(const SimParams& p, const SimParams* dp, const ServeArgs
         } else if (p.N == 8 && fixed_r(p) == 64) {
             if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true, 64, 8>), g, b, lds, s, dp, sa, out);
             else hipLaunchKernelGGL((k_serve<false, false, 8, MAXK, true, 64, 8>), g, b, lds, s, dp, sa, out);
+        } else if (p.N == 8 && fixed_r(p) == 96) {
+            if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true, 96, 8>), g, b, lds, s, dp, sa, out);
+            else hipLaunchKernelGGL((k_serve<false, false, 8, MAXK, true, 96, 8>), g, b, lds, s, dp, sa, out);
         } else {
             if (p.dist_tab) hipLaunchKernelGGL((k_serve<false, true, 8, MAXK, true>), g, b, lds, s, dp, sa, out);
             else hipLaunchKernelGGL((k_serve<false, false, 8, MAXK, true>), g, b, lds, s, dp, sa, out);

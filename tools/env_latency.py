@@ -53,6 +53,7 @@ def main():
         ("1 agent, 64 beams (cfg2 shape; reference 24,370)", {"num_agents": 1, "traffic_flow": False}, 64),
         ("8 agents, team, 64 beams (cfg3 shape; reference 6,668)",
          {"num_agents": 8, "traffic_flow": False, "use_team_reward": True}, 64),
+        ("8 agents, 96 beams (the reference's default LiDAR)", {"num_agents": 8, "traffic_flow": False}, None),
         ("traffic 0.5, 64 beams (cfg4 shape; reference 15,120)",
          {"num_agents": 1, "traffic_flow": True, "traffic_density": 0.5}, 64),
     ]
