@@ -3773,6 +3773,10 @@ static void launch_fused(const SimParams& p, const SimParams* dp, const StepInpu
             else if (pk == 4 && p.N == 1)
                 hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true, 0, 1>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 4) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 4, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (pk == 2 && p.N == 1 && fr == 96)  // (the reference's defaults: one agent, 96 beams)
+                hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true, true, 96, 1>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
+            else if (pk == 2 && p.N == 1)
+                hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true, true, 0, 1>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else if (pk == 2) hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 2, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             else hipLaunchKernelGGL((k_step<false, TAB, 8, MAXK, 1, true, true>), dim3(wg), dim3(2 * WAVE), lds, s, dp, in, out);
             return;

@@ -21,6 +21,8 @@ CONFIGS = [
          E=4096, N=8, R=128, team=1),
     dict(name="96-beam", desc="4096 envs x 8 agents x 96 beams (reference default LiDAR), obs 127",
          E=4096, N=8, R=96, D=127),
+    dict(name="1x96", desc="4096 envs x 1 agent x 96 beams (the reference's defaults: one agent, default LiDAR)",
+         E=4096, N=1, R=96),
 ]
 
 
