@@ -248,7 +248,10 @@ def _rel_angles(rays: int, fov: float) -> List[float]:
 class IntersectionEnv:
     """MARLEnv.IntersectionEnv (reference cpp/IntersectionEnv.h:23-105) on the GPU."""
 
-    def __init__(self, num_lanes: int = 3, device: int = 0, max_npcs: int = 64):
+    def __init__(self, num_lanes: int = 3, device: int = 0, max_npcs: int = 32):
+        # max_npcs: NPC slots of the device handle.  32 (the C ABI's default) runs the compile-time
+        # one-ego kernels; spawned traffic never exceeds 15 NPCs (profiles/r6_fleet_probe.txt), and a
+        # written traffic_cars vector of more cars re-creates the handle at 64 slots (_apply_state).
         self.num_lanes = int(num_lanes)
         self._device = int(device)
         self._max_npcs = int(max_npcs)
@@ -679,6 +682,12 @@ class IntersectionEnv:
             self._apply_state(s, self._lidar)
 
     def _apply_state(self, s: EnvState, lidar):
+        n = len(s.traffic_cars)
+        if self._max_npcs < n <= 64:  # a written fleet beyond the handle's NPC slots: 64 slots (the ABI's limit)
+            self._max_npcs = 64
+            if self._h is not None:
+                self._h.close()
+            self._h, self._ghost = None, False
         n = len(s.cars)
         if n == 0:  # the cars vector emptied: the traffic and the step count stay (the no-ego handle)
             self._routes, self._pending = [], []

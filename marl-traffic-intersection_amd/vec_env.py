@@ -13,6 +13,13 @@ Two modes:
 Per-agent semantics are exactly the reference's (bit-exact, see tests/);
 auto_reset=True restarts an env in the step after it reported terminated or
 truncated, which is what an RL rollout loop does with the reference env.
+
+max_npcs (NPC slots per env, traffic mode) defaults to 32, the C ABI's default:
+spawned traffic never holds more than 15 NPCs in one env (the reference's spawn
+test, profiles/r6_fleet_probe.txt), and 32 slots run the compile-time one-ego
+kernel (4096 envs at density 0.5: 159 M agent-steps/s against 75 M with 64
+slots, profiles/r6_cfg4_k64.txt).  Pass max_npcs=64 to write up to 64 traffic
+cars per env through set_state.
 """
 from __future__ import annotations
 
@@ -44,7 +51,7 @@ class VecIntersectionEnv:
     def __init__(self, num_envs: int, num_agents: int = 8, num_lanes: int = 3, lidar_rays: int = 96,
                  obs_dim: Optional[int] = None, use_team_reward: bool = False, respawn_enabled: bool = True,
                  max_steps: int = 2000, traffic_flow: bool = False, traffic_density: float = 0.5,
-                 reward_config: Any = None, ego_routes: Optional[Sequence] = None, max_npcs: int = 64,
+                 reward_config: Any = None, ego_routes: Optional[Sequence] = None, max_npcs: int = 32,
                  seed: int = 0, device: int = 0, backend: str = "torch", auto_reset: bool = True,
                  lidar_fov_deg: float = 360.0, lidar_max_dist: float = 250.0, lidar_step: float = 4.0):
         if backend not in ("torch", "numpy"):

@@ -21,6 +21,8 @@ CONFIGS = [
          E=4096, N=8, R=128, team=1),
     dict(name="96-beam", desc="4096 envs x 8 agents x 96 beams (reference default LiDAR), obs 127",
          E=4096, N=8, R=96, D=127),
+    dict(name="cfg4-k64", desc="config 4 with 64 NPC slots per env (VecIntersectionEnv's default max_npcs)",
+         E=4096, N=1, R=64, traffic=1, K=64),
     dict(name="1x96", desc="4096 envs x 1 agent x 96 beams (the reference's defaults: one agent, default LiDAR)",
          E=4096, N=1, R=96),
 ]
@@ -34,7 +36,7 @@ def run(cfg, steps, warmup, step_kernel=0, pack=0, split=0):
     E, N, R = cfg["E"], cfg["N"], cfg["R"]
     h = mev.Handle(num_envs=E, num_agents=N, lidar_rays=R, obs_dim=cfg.get("D", 0),
                    use_team_reward=cfg.get("team", 0), traffic_flow=cfg.get("traffic", 0), traffic_density=0.5,
-                   max_npcs=32)
+                   max_npcs=cfg.get("K", 32))
     if step_kernel:
         h.set_step_kernel(step_kernel)
     if pack:
