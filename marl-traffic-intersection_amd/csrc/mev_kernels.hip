@@ -2567,7 +2567,10 @@ __device__ inline void slab_clip(float c0, float dc, float idc, float a, float b
 
 // Probes tested per step of the road march (phase 1's first probes after a beam's
 // safe stretch from the car centre, and each pooled iteration).
-constexpr int LIDAR_NPR = 2;
+#ifndef MEV_LIDAR_NPR
+#define MEV_LIDAR_NPR 2
+#endif
+constexpr int LIDAR_NPR = MEV_LIDAR_NPR;
 // The march's tail (the queue empty, the few longest beams still running, lanes
 // mostly idle): once at most kMarchHelp beams run, each gets a group of 2-8 lanes
 // that test kNptHelp consecutive probes each per step (config 3 39.4 -> 35.6 us,
@@ -3350,8 +3353,14 @@ __host__ __device__ inline bool fixed_fits(const SimParams& p) {
 // agents per phase-1 pass in k_step (independent dependency chains interleaved;
 // 3 or 4 raise register pressure and lose); 1 in the early split's LiDAR wave
 // (8 waves per SIMD)
-constexpr int kPhase1Ilp = 2;
-constexpr int kEsplitIlp = 1;
+#ifndef MEV_PHASE1_ILP
+#define MEV_PHASE1_ILP 2
+#endif
+#ifndef MEV_ESPLIT_ILP
+#define MEV_ESPLIT_ILP 1
+#endif
+constexpr int kPhase1Ilp = MEV_PHASE1_ILP;
+constexpr int kEsplitIlp = MEV_ESPLIT_ILP;
 
 // The whole step in one wave per env: cars_body, then the LiDAR of the env's
 // N agents in pools, from the same wave's LDS.  No HBM hand-off, no second

@@ -59,7 +59,10 @@ EXPERIMENTS = {"stampsr": ["-DMEV_STAMPS", "-DMEV_STAMPS_R"],
                # (what the light workgroups' wait for it costs config 4 at most)
                "tsnomarch": ["-DMEV_EXP_TSNOMARCH"],
                # timing-only: the NPC controller without its round B (round A's moves final): its share
-               "noroundb": ["-DMEV_EXP_NOROUNDB"]}
+               "noroundb": ["-DMEV_EXP_NOROUNDB"],
+               # k_step's phase-1 ILP (agents per pass) 3 / 4, the early split's 2, LiDAR probes per ray 1 / 4
+               "p1ilp3": ["-DMEV_PHASE1_ILP=3"], "p1ilp4": ["-DMEV_PHASE1_ILP=4"], "eilp2": ["-DMEV_ESPLIT_ILP=2"],
+               "npr1": ["-DMEV_LIDAR_NPR=1"], "npr4": ["-DMEV_LIDAR_NPR=4"]}
 
 
 def build(name: str, force: bool = False) -> str:
